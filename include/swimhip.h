@@ -1,0 +1,188 @@
+/*
+ * swimhip.h — C ABI of libswimhip.so, the MI355X-native SWIM membership simulator.
+ *
+ * The library replaces, for N simulated members at once, the per-period hot path of
+ * scalecube-cluster (reference @ /root/reference, v2.4.2-SNAPSHOT):
+ *
+ *   FailureDetectorImpl.doPing / doPingReq / onPing / onPingReq / onTransitPingAck
+ *       cluster/src/main/java/io/scalecube/cluster/fdetector/FailureDetectorImpl.java:126-305
+ *   GossipProtocolImpl.doSpreadGossip / onGossipReq / selectGossipMembers / sweepGossips
+ *       cluster/src/main/java/io/scalecube/cluster/gossip/GossipProtocolImpl.java:139-304
+ *   MembershipProtocolImpl.updateMembership / onFailureDetectorEvent / doSync / onSync /
+ *       onSyncAck / onSuspicionTimeout
+ *       cluster/src/main/java/io/scalecube/cluster/membership/MembershipProtocolImpl.java:304-673
+ *   MembershipRecord.isOverrides
+ *       cluster/src/main/java/io/scalecube/cluster/membership/MembershipRecord.java:66-84
+ *   NetworkEmulator loss / block (fault injection seam)
+ *       cluster-testlib/src/main/java/io/scalecube/cluster/utils/NetworkEmulator.java:166-180,348-351
+ *
+ * The reference has no SPI for these protocols: ClusterImpl hard-wires them
+ * (cluster/src/main/java/io/scalecube/cluster/ClusterImpl.java:180-210). This ABI sits
+ * *below* MembershipProtocol (MembershipProtocol.java:14-65) for all members at once; a
+ * host binds it through Panama FFM / ctypes. Discrete replay
+ * semantics (period = pingInterval, G gossip rounds per period, SYNC stagger) are fixed in
+ * DESIGN.md §3.
+ *
+ * Conventions: plain C types only; the caller owns every buffer passed in; handles are
+ * opaque; every entry point returns 0 or a negative SWIM_E* status (no exceptions cross
+ * the ABI, mirroring the reference, which never throws protocol failures to callers —
+ * FailureDetectorImpl.java:307-309, MembershipProtocolImpl.java:540). Message loss is
+ * protocol semantics, never an error. One host thread per handle.
+ */
+#ifndef SWIMHIP_H
+#define SWIMHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define SWIM_OK 0
+#define SWIM_EINVAL (-22)    /* bad argument / config                                    */
+#define SWIM_ENOMEM (-12)    /* device allocation failed                                 */
+#define SWIM_EHIP (-5)       /* HIP runtime error (incl. "no GPU")                       */
+#define SWIM_ERCCL (-6)      /* RCCL error (multi-GPU)                                   */
+#define SWIM_EOVERFLOW (-75) /* a bounded simulator buffer (events, gossips, syncs) overflowed */
+
+/* ---- packed membership record (MembershipRecord.java:12-16, MemberStatus.java:3-16) ---
+ * cell = incarnation << 2 | code ; code 1 = ALIVE, 2 = SUSPECT ; 0 = absent (no record in
+ * membershipTable) ; 0xFFFFFFFF = DEAD. isOverrides(r1, r0) (MembershipRecord.java:66-84)
+ * becomes:  r0 == 0 ? code(r1) == ALIVE : r1 > r0  (unsigned).                           */
+#define SWIM_ABSENT 0u
+#define SWIM_ALIVE 1u
+#define SWIM_SUSPECT 2u
+#define SWIM_DEAD 0xFFFFFFFFu
+#define SWIM_PACK(inc, code) ((((uint32_t)(inc)) << 2) | (uint32_t)(code))
+
+/* ---- membership events (api/membership/MembershipEvent.java:13-67) -------------------- */
+#define SWIM_EV_ADDED 1
+#define SWIM_EV_REMOVED 2
+#define SWIM_EV_UPDATED 3
+
+/* update reasons (MembershipProtocolImpl.java:58-64) */
+#define SWIM_R_FAILURE_DETECTOR_EVENT 0
+#define SWIM_R_MEMBERSHIP_GOSSIP 1
+#define SWIM_R_SYNC 2
+#define SWIM_R_INITIAL_SYNC 3
+#define SWIM_R_SUSPICION_TIMEOUT 4
+
+typedef struct swim_event {
+  uint64_t period;   /* protocol period in which the event was emitted                   */
+  uint32_t observer; /* member whose MembershipProtocol emitted it                       */
+  uint32_t subject;  /* member the event is about                                        */
+  uint32_t record;   /* packed record (REMOVED: the record that was removed)             */
+  uint8_t type;      /* SWIM_EV_*                                                        */
+  uint8_t reason;    /* SWIM_R_*                                                         */
+  uint8_t phase;     /* sub-phase of the period (0 = FD, 1..G = gossip rounds, ...)      */
+  uint8_t pad;
+} swim_event;
+
+/* ---- configuration: 1:1 with the reference config surface + simulator-only fields ----
+ * FailureDetectorConfig (api/fdetector/FailureDetectorConfig.java:8-24)
+ * GossipConfig          (api/gossip/GossipConfig.java:8-22)
+ * MembershipConfig      (api/membership/MembershipConfig.java:13-30)
+ * ClusterConfig         (api/ClusterConfig.java:24-43)                                    */
+typedef struct swim_config {
+  uint32_t n_members;   /* N simulated members (ids 0..N-1)                               */
+  uint32_t mode;        /* 0 = dense N x N views                                          */
+  uint64_t seed;        /* Philox key                                                     */
+  int32_t ping_interval_ms;
+  int32_t ping_timeout_ms;
+  int32_t ping_req_members;
+  int32_t gossip_fanout;
+  int32_t gossip_interval_ms;
+  int32_t gossip_repeat_mult;
+  int32_t sync_interval_ms;
+  int32_t sync_timeout_ms;
+  int32_t suspicion_mult;
+  int32_t metadata_timeout_ms;
+  uint32_t n_seeds;         /* MembershipConfig.seedMembers = members [0, n_seeds)        */
+  uint32_t gossip_capacity; /* live gossip slots (power of two; 0 = default)              */
+  uint32_t event_capacity;  /* buffered MembershipEvents (0 = events not recorded)        */
+  uint32_t sync_capacity;   /* SYNC requests per period (0 = default)                     */
+  uint32_t dirty_capacity;  /* gossip (observer, subject) inbox cells per round (0 = default) */
+  uint32_t flags;           /* reserved, 0                                                */
+} swim_config;
+
+typedef struct swim_stats {
+  uint64_t period;            /* periods stepped so far                                   */
+  uint64_t fd_probes;         /* doPing calls that selected a target                      */
+  uint64_t fd_direct_ok;      /* direct PING acknowledged                                 */
+  uint64_t fd_ping_req;       /* probes that went to ping-req                             */
+  uint64_t fd_suspect_events; /* FailureDetectorEvent(SUSPECT) published                  */
+  uint64_t fd_alive_events;   /* FailureDetectorEvent(ALIVE) published                    */
+  uint64_t gossips_created;   /* GossipProtocol.spread() calls                            */
+  uint64_t gossip_first_receipts; /* onGossipReq with a new gossip id                     */
+  uint64_t gossip_sends;      /* GossipRequest messages whose receiver lacked the gossip  */
+  uint64_t syncs_sent;        /* SYNC messages (periodic + FD-triggered)                  */
+  uint64_t syncs_delivered;
+  uint64_t sync_acks_delivered;
+  uint64_t records_accepted;  /* updateMembership calls that changed the table            */
+  uint64_t events_added;
+  uint64_t events_removed;
+  uint64_t suspicion_timeouts;
+  uint64_t refutations;       /* onSelfMemberDetected                                     */
+  uint64_t overflow;          /* bit mask of overflowed buffers (0 = none)                */
+  uint64_t live_gossip_slots; /* gossip slots currently in use                            */
+  uint64_t not_converged;     /* (alive observer, crashed subject) cells still present    */
+} swim_stats;
+
+typedef struct swim_handle swim_handle;
+
+/* Lifecycle. ClusterImpl.doStart0 wiring (core/ClusterImpl.java:170-227) for N members that
+ * start converged: every view holds every member ALIVE inc 0. */
+int swim_create(const swim_config* cfg, swim_handle** out);
+int swim_destroy(swim_handle* h);
+
+/* Fault injection (NetworkEmulator.java:81-98,166-180): uniform outbound loss in basis
+ * points (0..10000; 10000 = blockAllOutbound). */
+int swim_set_loss(swim_handle* h, uint32_t loss_bp);
+/* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
+ * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */
+int swim_set_partition(swim_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1);
+/* Directed link block a->b (NetworkEmulator.blockOutbound(Address...) :105-119). */
+int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked);
+/* Crash = transport.stop() (MembershipProtocolTest.java:991-1000): the member stops
+ * sending, receiving, answering and firing timers, from the next period on. */
+int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
+
+/* Advance `periods` protocol periods (FD, G gossip rounds, suspicion
+ * timeouts, SYNC/SYNC_ACK). Asynchronous to the host only inside the call. */
+int swim_step(swim_handle* h, uint32_t periods);
+/* Same, enqueued on the handle's stream without a final device sync (bench timing). */
+int swim_step_async(swim_handle* h, uint32_t periods);
+int swim_sync(swim_handle* h);
+
+/* MembershipEvents in canonical order (period, observer, phase, subject, type). */
+int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);
+/* One observer's membershipTable as packed cells (n = n_members). */
+int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);
+/* Suspicion deadlines (period at which the timer fires, 0 = none) for one observer. */
+int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);
+/* Order-independent 64-bit digests of all views and all deadlines. */
+int swim_digest(swim_handle* h, uint64_t* view_digest, uint64_t* deadline_digest);
+/* Per-subject convergence: number of alive observers whose view holds the subject, and the
+ * last period in which any observer removed it. Arrays of n_members entries. */
+int swim_read_presence(swim_handle* h, uint32_t* present, uint32_t* last_removed, uint32_t n);
+int swim_stats_get(swim_handle* h, swim_stats* out);
+const char* swim_last_error(swim_handle* h);
+
+/* Device known-answer check of the packed isOverrides (MembershipRecordTest.java:46-108):
+ * out[i] = isOverrides(r1[i], r0[i]) computed by a gfx950 kernel. No handle needed. */
+int swim_kat_is_overrides(const uint32_t* r1, const uint32_t* r0, uint8_t* out, uint64_t n);
+/* Device Philox4x32-10 draws (counter = {a,b,c,tick}, key = seed ^ kind) for RNG parity. */
+int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint32_t* out, uint64_t n);
+
+/* Kernel timing for the bench: the last step's per-kernel-class device time (ms, HIP events
+ * on the handle's stream). idx: 0 fd, 1 gossip_send, 2 gossip_apply, 3 suspicion, 4 sync_merge,
+ * 5 sync_ack. Returns accumulated time since the last reset. */
+int swim_kernel_time(swim_handle* h, uint32_t idx, double* ms, uint64_t* launches);
+int swim_kernel_time_reset(swim_handle* h, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWIMHIP_H */

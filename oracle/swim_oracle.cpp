@@ -1,0 +1,899 @@
+// swim_oracle.cpp — CPU oracle for the SWIM hot path. TEST INFRASTRUCTURE ONLY.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+// and only as the checker. It is a sequential, single-threaded restatement of the reference's
+// protocol logic (scalecube-cluster @ /root/reference), written member-by-member the way the
+// Java code runs on each member's single-threaded scheduler (ClusterImpl.java:178), under the
+// discrete replay semantics fixed in DESIGN.md §3. Every function cites the reference lines
+// it restates. Abbreviations:
+//   MPI = cluster/src/main/java/io/scalecube/cluster/membership/MembershipProtocolImpl.java
+//   FDI = cluster/src/main/java/io/scalecube/cluster/fdetector/FailureDetectorImpl.java
+//   GPI = cluster/src/main/java/io/scalecube/cluster/gossip/GossipProtocolImpl.java
+//   MR  = cluster/src/main/java/io/scalecube/cluster/membership/MembershipRecord.java
+//   CM  = cluster/src/main/java/io/scalecube/cluster/ClusterMath.java
+//   NE  = cluster-testlib/src/main/java/io/scalecube/cluster/utils/NetworkEmulator.java
+//   NET = cluster-testlib/src/main/java/io/scalecube/cluster/utils/NetworkEmulatorTransport.java
+//
+// Parity: isOverrides is pinned by MembershipRecordTest (the reference's only bit-exact
+// golden); everything RNG-driven is pinned by behavioural scenario restatements and
+// self-consistency fixtures (the reference cannot run here: no JVM). See DESIGN.md §6.
+
+#include "swim_oracle.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11). Replaces every JDK RNG call site
+// on the path: Collections.shuffle (FDI:346,360; GPI:260), ThreadLocalRandom (FDI:326;
+// MPI:420,424; NE:350).
+// ---------------------------------------------------------------------------------------
+struct U4 {
+  uint32_t v[4];
+};
+
+inline void mulhilo(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  *lo = (uint32_t)p;
+}
+
+U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo(0xD2511F53u, c.v[0], &hi0, &lo0);
+    mulhilo(0xCD9E8D57u, c.v[2], &hi1, &lo1);
+    U4 n;
+    n.v[0] = hi1 ^ c.v[1] ^ k0;
+    n.v[1] = lo1;
+    n.v[2] = hi0 ^ c.v[3] ^ k1;
+    n.v[3] = lo0;
+    c = n;
+  }
+  return c;
+}
+
+inline uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// Message kinds and selection purposes.
+enum Kind : uint32_t {
+  K_PING = 1,
+  K_ACK = 2,
+  K_PING_REQ = 3,
+  K_PROXY_PING = 4,
+  K_PROXY_ACK = 5,
+  K_FWD_ACK = 6,
+  K_GOSSIP = 7,
+  K_SYNC = 8,
+  K_SYNC_ACK = 9,
+  K_MREQ = 10,
+  K_MRESP = 11,
+  K_FD_PERM = 16,
+  K_GOSSIP_PERM = 17,
+  K_PROXY_PERM = 18,
+  K_SYNC_PICK = 19,
+};
+
+inline U4 draw4(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick) {
+  U4 ctr = {{a, b, c, tick}};
+  return philox4x32_10(ctr, (uint32_t)seed ^ (kind * 0x9E3779B9u), (uint32_t)(seed >> 32));
+}
+
+inline uint32_t draw(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick) {
+  return draw4(seed, kind, a, b, c, tick).v[0];
+}
+
+// Keyed bijection on [0, n): 4-round balanced Feistel on the next even power of two with
+// cycle walking. Stands in for a Collections.shuffle'd member list (FDI:340-349,355-360;
+// GPI:253-274): position p of the shuffled list = perm(p).
+uint32_t perm(uint32_t x, uint32_t n, const uint32_t* k) {
+  uint32_t bits = 2;
+  while ((1ull << bits) < (uint64_t)n) ++bits;
+  if (bits & 1) ++bits;
+  const uint32_t half = bits / 2;
+  const uint32_t mask = (1u << half) - 1u;
+  do {
+    uint32_t L = x >> half, R = x & mask;
+    for (int r = 0; r < 4; ++r) {
+      uint32_t F = fmix32(R ^ k[r]) & mask;
+      uint32_t nl = R;
+      R = L ^ F;
+      L = nl;
+    }
+    x = (L << half) | R;
+  } while (x >= n);
+  return x;
+}
+
+// ---------------------------------------------------------------------------------------
+// ClusterMath (CM:23-135).
+// ---------------------------------------------------------------------------------------
+inline int32_t ceil_log2(int32_t num) {  // CM:133-135: 32 - numberOfLeadingZeros(num)
+  return num <= 0 ? (num == 0 ? 0 : 32) : 32 - __builtin_clz((uint32_t)num);
+}
+inline int32_t periods_to_spread(int32_t rm, int32_t n) { return rm * ceil_log2(n); }              // CM:111-113
+inline int32_t periods_to_sweep(int32_t rm, int32_t n) { return 2 * (periods_to_spread(rm, n) + 1); }  // CM:99-102
+inline int32_t suspicion_periods(int32_t mult, int32_t n) { return mult * ceil_log2(n); }            // CM:123-125 / pingInterval
+
+// ---------------------------------------------------------------------------------------
+// MembershipRecord.isOverrides (MR:66-84) on the packed encoding of include/swimhip.h.
+// ---------------------------------------------------------------------------------------
+inline uint32_t code_of(uint32_t r) { return r & 3u; }
+inline uint32_t inc_of(uint32_t r) { return r >> 2; }
+inline bool is_overrides(uint32_t r1, uint32_t r0) {
+  if (r0 == SWIM_ABSENT) return r1 != SWIM_DEAD && code_of(r1) == SWIM_ALIVE;  // MR:67-69
+  if (r0 == SWIM_DEAD) return false;                                              // MR:73-75
+  if (r1 == SWIM_DEAD) return true;                                               // MR:76-78
+  if (inc_of(r1) == inc_of(r0))                                                   // MR:79-80
+    return code_of(r1) != code_of(r0) && code_of(r1) == SWIM_SUSPECT;
+  return inc_of(r1) > inc_of(r0);                                                 // MR:82
+}
+
+// ---------------------------------------------------------------------------------------
+// Simulation state.
+// ---------------------------------------------------------------------------------------
+struct Gossip {  // Gossip.java:7-49 + GossipRequest payload (MembershipRecord)
+  uint32_t origin, seq, subject, record, hash;
+  int64_t create;
+  int32_t holders;  // members whose gossips map currently holds it
+};
+
+// GossipProtocolImpl.gossips (GPI:49): gossipId -> GossipState.infectionPeriod
+// (GossipState.java:14). Gossip ids (origin, seq) are also numbered globally in creation order
+// (gid); each member's map is a direct-mapped table keyed by gid that stores the full key, so
+// find/put/erase are exact map operations (a collision with a live entry grows every table).
+struct GossipMap {
+  std::vector<uint32_t> key;  // gid, or EMPTY
+  std::vector<int64_t> inf;
+};
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+
+struct Member {
+  std::vector<uint32_t> table;          // MPI:87 membershipTable (+ MPI:88 members: cell != 0)
+  uint32_t others = 0;                  // members.size() - 1 == pingMembers == remoteMembers
+  int32_t delta = 0;                    // deferred member-count change of the current phase
+  std::map<uint32_t, uint64_t> timers;  // MPI:101 suspicionTimeoutTasks: subject -> fire period
+  uint32_t fd_epoch = 0, fd_cursor = 0; // FDI:49-50 pingMembers order + pingMemberIndex
+  uint32_t g_epoch = 0, g_cursor = 0;   // GPI:52-53 remoteMembers order + remoteMembersIndex
+  GossipMap gossips;                    // GPI:49 gossips
+  uint32_t gossip_seq = 0;              // GPI:48 gossipCounter
+  uint32_t sync_fd = 0xFFFFFFFFu;       // FD-triggered SYNC target of this period (MPI:385-397)
+  bool alive = true;
+};
+
+struct SyncReq {
+  uint32_t from, to, kind;  // kind 0 = periodic doSync (MPI:304-320), 1 = FD-triggered (MPI:389-397)
+};
+
+}  // namespace
+
+struct oracle_handle {
+  swim_config cfg;
+  uint32_t N;
+  uint32_t G, S, TPP;
+  int32_t sweepmax;
+  uint64_t seed;
+  uint64_t period = 0;
+  uint32_t loss_bp = 0;
+  std::vector<uint8_t> group;
+  uint64_t part_t0 = 0, part_t1 = 0;
+  std::vector<uint8_t> link;  // directed block bitmap, lazily allocated
+  std::vector<Member> m;
+  std::vector<Gossip> registry;  // by gid
+  uint32_t gbase = 0;            // every gid below is held by nobody
+  uint32_t rc = 64;              // capacity of each member's GossipMap (power of two)
+  std::vector<swim_event> events;
+  swim_stats st;
+  std::vector<uint32_t> pres, last_removed;
+  // pending gossip-delivered records per receiver: subject -> lattice max
+  std::vector<std::map<uint32_t, uint32_t>> inbox;
+};
+
+namespace {
+
+inline uint32_t ghash(uint32_t origin, uint32_t seq) { return fmix32(origin ^ fmix32(seq + 0x9E3779B9u)); }
+
+inline uint32_t tick_of(const oracle_handle* h, uint32_t phase) { return (uint32_t)(h->period * h->TPP + phase); }
+
+// NetworkEmulatorTransport.send/requestResponse (NET:44-70) + NetworkEmulator.evaluateLoss
+// (NE:348-351) + crash (transport stopped) + partition cut: is message src->dst delivered?
+bool delivered(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
+  if (!h->m[src].alive || !h->m[dst].alive) return false;
+  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[src] != h->group[dst]) return false;
+  if (!h->link.empty()) {
+    uint64_t bit = (uint64_t)src * h->N + dst;
+    if (h->link[bit >> 3] & (1u << (bit & 7))) return false;
+  }
+  if (h->loss_bp == 0) return true;      // NE:349 lossPercent > 0
+  if (h->loss_bp >= 10000) return false; // NE:350 lossPercent >= 100
+  uint32_t thr = (uint32_t)(((uint64_t)h->loss_bp << 32) / 10000u);
+  return draw(h->seed, kind, src, dst, c, tick) >= thr;  // NE:350 nextInt(100) < loss => lost
+}
+
+void perm_keys(const oracle_handle* h, uint32_t kind, uint32_t member, uint32_t epoch, uint32_t* k) {
+  U4 r = draw4(h->seed, kind, member, epoch, 0, 0);
+  for (int i = 0; i < 4; ++i) k[i] = r.v[i];
+}
+
+void emit_event(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t type, uint32_t reason, uint32_t phase,
+                uint32_t record) {
+  if (type == SWIM_EV_ADDED) h->st.events_added++;
+  if (type == SWIM_EV_REMOVED) h->st.events_removed++;
+  if (h->cfg.event_capacity == 0) return;
+  swim_event e;
+  std::memset(&e, 0, sizeof e);
+  e.period = h->period;
+  e.observer = obs;
+  e.subject = subj;
+  e.record = record;
+  e.type = (uint8_t)type;
+  e.reason = (uint8_t)reason;
+  e.phase = (uint8_t)phase;
+  h->events.push_back(e);
+}
+
+int64_t gossip_find(const oracle_handle* h, const Member& me, uint32_t gid) {
+  const uint32_t s = gid & (h->rc - 1);
+  return me.gossips.key[s] == gid ? me.gossips.inf[s] : -1;
+}
+
+void gossip_erase(oracle_handle* h, Member& me, uint32_t gid) {
+  const uint32_t s = gid & (h->rc - 1);
+  if (me.gossips.key[s] != gid) return;
+  me.gossips.key[s] = EMPTY;
+  h->registry[gid].holders--;
+}
+
+void gossip_grow(oracle_handle* h) {
+  h->rc *= 2;
+  for (auto& mm : h->m) {
+    GossipMap nm;
+    nm.key.assign(h->rc, EMPTY);
+    nm.inf.assign(h->rc, 0);
+    for (size_t s = 0; s < mm.gossips.key.size(); ++s) {
+      const uint32_t g = mm.gossips.key[s];
+      if (g == EMPTY) continue;
+      nm.key[g & (h->rc - 1)] = g;
+      nm.inf[g & (h->rc - 1)] = mm.gossips.inf[s];
+    }
+    mm.gossips = std::move(nm);
+  }
+}
+
+void gossip_put(oracle_handle* h, Member& me, uint32_t gid, int64_t inf) {
+  for (;;) {
+    const uint32_t s = gid & (h->rc - 1);
+    const uint32_t k = me.gossips.key[s];
+    if (k == gid) {
+      me.gossips.inf[s] = inf;
+      return;
+    }
+    if (k == EMPTY) {
+      me.gossips.key[s] = gid;
+      me.gossips.inf[s] = inf;
+      h->registry[gid].holders++;
+      return;
+    }
+    gossip_grow(h);  // another live gossip owns the slot
+  }
+}
+
+// GossipProtocolImpl.spread -> createAndPutGossip (GPI:124-128,163-169,211-213): the new
+// gossip's infectionPeriod is the gossip module's *next* round (`currentPeriod`).
+void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t record, int64_t create_round) {
+  Member& o = h->m[origin];
+  uint32_t seq = o.gossip_seq++;
+  const uint32_t gid = (uint32_t)h->registry.size();
+  h->registry.push_back(Gossip{origin, seq, subject, record, ghash(origin, seq), create_round, 0});
+  gossip_put(h, o, gid, create_round);
+  h->st.gossips_created++;
+}
+
+// MetadataStoreImpl.fetchMetadata (core/metadata/MetadataStoreImpl.java:151-193) as a
+// liveness round trip: GET_METADATA_REQ obs->subj and GET_METADATA_RESP subj->obs delivered
+// and the subject serving (onMetadataRequest :209-249).
+bool fetch_ok(const oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t attempt, uint32_t tick) {
+  return delivered(h, K_MREQ, obs, subj, attempt, tick) && delivered(h, K_MRESP, subj, obs, attempt, tick);
+}
+
+// MembershipProtocolImpl.updateMembership (MPI:481-547) with its callees onSelfMemberDetected
+// (MPI:549-569), onDeadMemberDetected (MPI:571-587), onAliveMemberDetected (MPI:589-610),
+// scheduleSuspicionTimeoutTask (MPI:620-635), cancelSuspicionTimeoutTask (MPI:612-618),
+// spreadMembershipGossipUnlessGossiped (MPI:649-656).
+//   others_snap: the observer's member count at phase start
+void update_membership(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t r1, uint32_t reason, uint32_t phase,
+                       uint32_t attempt, uint32_t tick, uint32_t others_snap, int64_t create_round) {
+  Member& me = h->m[obs];
+  uint32_t& cell = me.table[subj];
+  const uint32_t r0 = cell;
+  if (!is_overrides(r1, r0)) return;  // MPI:489-496 (equal records never override)
+  const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;  // MPI:652-653
+  if (subj == obs) {  // MPI:499-501 -> onSelfMemberDetected MPI:549-569
+    uint32_t inc1 = (r1 == SWIM_DEAD) ? inc_of(r0) : inc_of(r1);
+    uint32_t r2 = SWIM_PACK(std::max(inc_of(r0), inc1) + 1u, code_of(r0));
+    cell = r2;
+    h->st.records_accepted++;
+    h->st.refutations++;
+    spread_gossip(h, obs, obs, r2, create_round);  // MPI:567 (always spread)
+    return;
+  }
+  if (r1 == SWIM_DEAD) {  // MPI:507-509 -> onDeadMemberDetected MPI:571-587
+    me.timers.erase(subj);
+    cell = SWIM_ABSENT;  // r0 != null guaranteed by isOverrides
+    me.delta -= 1;
+    h->st.records_accepted++;
+    if (me.alive && subj != obs) {
+      h->pres[subj]--;
+      h->last_removed[subj] = std::max<uint32_t>(h->last_removed[subj], (uint32_t)h->period + 1u);
+    }
+    emit_event(h, obs, subj, SWIM_EV_REMOVED, reason, phase, r0);
+    return;
+  }
+  if (code_of(r1) == SWIM_SUSPECT) {  // MPI:511-516
+    cell = r1;
+    h->st.records_accepted++;
+    if (me.timers.find(subj) == me.timers.end())  // computeIfAbsent (MPI:627-634)
+      me.timers[subj] = h->period + (uint64_t)suspicion_periods(h->cfg.suspicion_mult, (int32_t)others_snap + 1);
+    if (spread) spread_gossip(h, obs, subj, r1, create_round);
+    return;
+  }
+  // ALIVE with r0 == null or r0.inc < r1.inc (MPI:518-542)
+  if (!fetch_ok(h, obs, subj, attempt, tick)) return;  // MPI:540 failed fetch silently skipped
+  me.timers.erase(subj);                               // MPI:534
+  if (spread) spread_gossip(h, obs, subj, r1, create_round);  // MPI:535
+  cell = r1;                                                  // MPI:604
+  h->st.records_accepted++;
+  if (r0 == SWIM_ABSENT) {  // MPI:597-598 ADDED (UPDATED needs metadata versions: not modelled)
+    me.delta += 1;
+    if (me.alive && subj != obs) h->pres[subj]++;
+    emit_event(h, obs, subj, SWIM_EV_ADDED, reason, phase, r1);
+  }
+}
+
+void finish_phase(oracle_handle* h) {
+  for (auto& mm : h->m) {
+    mm.others = (uint32_t)((int32_t)mm.others + mm.delta);
+    mm.delta = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// FailureDetectorImpl (FDI).
+// ---------------------------------------------------------------------------------------
+// selectPingMember (FDI:340-349): round robin over a shuffled list; reshuffle on wrap.
+uint32_t select_ping_member(oracle_handle* h, uint32_t i) {
+  Member& me = h->m[i];
+  uint32_t k[4];
+  perm_keys(h, K_FD_PERM, i, me.fd_epoch, k);
+  for (;;) {
+    if (me.fd_cursor >= h->N) {
+      me.fd_cursor = 0;
+      me.fd_epoch++;
+      perm_keys(h, K_FD_PERM, i, me.fd_epoch, k);
+    }
+    uint32_t x = perm(me.fd_cursor++, h->N, k);
+    if (x != i && me.table[x] != SWIM_ABSENT) return x;
+  }
+}
+
+// selectPingReqMembers (FDI:351-363): first k of shuffle(pingMembers \ {target}).
+std::vector<uint32_t> select_ping_req_members(oracle_handle* h, uint32_t i, uint32_t j) {
+  std::vector<uint32_t> out;
+  const int32_t kreq = h->cfg.ping_req_members;
+  if (kreq <= 0) return out;
+  uint32_t k[4];
+  perm_keys(h, K_PROXY_PERM, i, (uint32_t)h->period, k);
+  const Member& me = h->m[i];
+  for (uint32_t pos = 0; pos < h->N && (int32_t)out.size() < kreq; ++pos) {
+    uint32_t x = perm(pos, h->N, k);
+    if (x != i && x != j && me.table[x] != SWIM_ABSENT) out.push_back(x);
+  }
+  return out;
+}
+
+// MembershipProtocolImpl.onFailureDetectorEvent (MPI:376-404).
+void on_fd_event(oracle_handle* h, uint32_t i, uint32_t j, uint32_t status, uint32_t tick) {
+  Member& me = h->m[i];
+  const uint32_t r0 = me.table[j];
+  if (r0 == SWIM_ABSENT) return;          // MPI:378-380
+  if (code_of(r0) == status) return;      // MPI:381-383
+  if (status == SWIM_ALIVE) {             // MPI:385-397: SYNC to the member instead
+    me.sync_fd = j;
+    return;
+  }
+  update_membership(h, i, j, SWIM_PACK(inc_of(r0), status), SWIM_R_FAILURE_DETECTOR_EVENT, 0, 0, tick, me.others,
+                    (int64_t)h->period * h->G);  // MPI:399-402
+}
+
+// doPing (FDI:126-170) + doPingReq (FDI:172-209) + responder handlers onPing (FDI:226-252),
+// onPingReq (FDI:255-277), onTransitPingAck (FDI:283-305), with TransportImpl's cid-only
+// response matching (TransportImpl.java:236-238): all ping-req subscriptions share the cid,
+// so the first transit ack completes every one still pending.
+void do_ping(oracle_handle* h, uint32_t i) {
+  Member& me = h->m[i];
+  if (me.others == 0) return;  // FDI:132-134 pingMembers empty
+  const uint32_t tick = tick_of(h, 0);
+  const uint32_t j = select_ping_member(h, i);
+  h->st.fd_probes++;
+  std::vector<uint32_t> evs;
+  if (delivered(h, K_PING, i, j, 0, tick) && delivered(h, K_ACK, j, i, 0, tick)) {  // FDI:143-150
+    h->st.fd_direct_ok++;
+    evs.push_back(SWIM_ALIVE);
+  } else {
+    const int32_t time_left = h->cfg.ping_interval_ms - h->cfg.ping_timeout_ms;  // FDI:160
+    std::vector<uint32_t> proxies = select_ping_req_members(h, i, j);           // FDI:161
+    if (time_left <= 0 || proxies.empty()) {                                     // FDI:163-165
+      evs.push_back(SWIM_SUSPECT);
+    } else {
+      h->st.fd_ping_req++;
+      uint32_t unsent = 0, sent = 0;
+      bool any_ok = false;
+      for (uint32_t p : proxies) {
+        if (!delivered(h, K_PING_REQ, i, p, j, tick)) {  // emulator send error: immediate SUSPECT
+          ++unsent;
+          continue;
+        }
+        ++sent;
+        if (delivered(h, K_PROXY_PING, p, j, i, tick) && delivered(h, K_PROXY_ACK, j, p, i, tick) &&
+            delivered(h, K_FWD_ACK, p, i, j, tick))
+          any_ok = true;
+      }
+      for (uint32_t u = 0; u < unsent; ++u) evs.push_back(SWIM_SUSPECT);
+      for (uint32_t s = 0; s < sent; ++s) evs.push_back(any_ok ? SWIM_ALIVE : SWIM_SUSPECT);  // FDI:190-207
+    }
+  }
+  for (uint32_t ev : evs) {  // publishPingResult (FDI:365-368) -> MPI:376
+    if (ev == SWIM_ALIVE)
+      h->st.fd_alive_events++;
+    else
+      h->st.fd_suspect_events++;
+    on_fd_event(h, i, j, ev, tick);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// GossipProtocolImpl (GPI).
+// ---------------------------------------------------------------------------------------
+// selectGossipMembers (GPI:253-274): all if size < fanout, else the window [idx, idx+fanout)
+// of a shuffled list, reshuffled when the window would run past the end.
+std::vector<uint32_t> select_gossip_members(oracle_handle* h, uint32_t g) {
+  Member& me = h->m[g];
+  const uint32_t f = (uint32_t)h->cfg.gossip_fanout;
+  std::vector<uint32_t> out;
+  if (me.others < f) {  // GPI:255-256
+    for (uint32_t x = 0; x < h->N; ++x)
+      if (x != g && me.table[x] != SWIM_ABSENT) out.push_back(x);
+    return out;
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    uint32_t k[4];
+    perm_keys(h, K_GOSSIP_PERM, g, me.g_epoch, k);
+    out.clear();
+    uint32_t pos = me.g_cursor;
+    while (pos < h->N && out.size() < f) {
+      uint32_t x = perm(pos++, h->N, k);
+      if (x != g && me.table[x] != SWIM_ABSENT) out.push_back(x);
+    }
+    if (out.size() == f) {
+      me.g_cursor = pos;
+      return out;
+    }
+    me.g_epoch++;  // GPI:259-262 reshuffle
+    me.g_cursor = 0;
+  }
+  return out;  // unreachable when others >= f
+}
+
+// One gossip round r: doSpreadGossip (GPI:139-157) of every member on the
+// start-of-round state, then onGossipReq (GPI:171-183) deliveries, then membership apply
+// (MPI:407-414 via the inbox lattice max).
+void gossip_round(oracle_handle* h, uint32_t q) {
+  const int64_t r = (int64_t)h->period * h->G + q;
+  const uint32_t phase = 1 + q;
+  const uint32_t tick = tick_of(h, phase);
+  const int32_t rm = h->cfg.gossip_repeat_mult;
+  while (h->gbase < h->registry.size() && h->registry[h->gbase].holders == 0) h->gbase++;
+  const uint32_t gend = (uint32_t)h->registry.size();
+  std::vector<uint32_t> window;
+  for (uint32_t s = 0; s < h->N; ++s) {
+    Member& me = h->m[s];
+    if (!me.alive) continue;
+    const int32_t spread = periods_to_spread(rm, (int32_t)me.others + 1);  // GPI:243-244
+    const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);    // GPI:283-284
+    // gossips held at the start of round r: received before it and not swept at r-1.
+    window.clear();
+    bool any = false;
+    for (uint32_t gid = h->gbase; gid < gend; ++gid) {
+      const int64_t inf = gossip_find(h, me, gid);
+      if (inf < 0 || inf > r || r - 1 > inf + sweep) continue;
+      any = true;
+      if (r <= inf + spread) window.push_back(gid);  // GPI:247 infectionPeriod + spread >= period
+    }
+    if (!any) continue;  // GPI:144-146 (no peer selection either)
+    std::vector<uint32_t> peers = select_gossip_members(h, s);  // GPI:150
+    for (uint32_t p : peers) {
+      // GossipState.infected (GPI:248) only prunes sends to members that already hold the
+      // gossip; redundant deliveries are no-ops, so they are not simulated.
+      Member& pm = h->m[p];
+      if (!pm.alive) continue;  // stopped transport: every message to it is lost
+      const int32_t psweep = periods_to_sweep(rm, (int32_t)pm.others + 1);
+      for (uint32_t gid : window) {
+        const int64_t pinf = gossip_find(h, pm, gid);
+        const bool has = pinf >= 0;
+        // counted once per message whose receiver lacked the gossip at the start of the round
+        if (!(has && pinf <= r && r <= pinf + psweep)) h->st.gossip_sends++;
+        if (has && r <= pinf + psweep) continue;  // receiver holds it (maybe since this round)
+        const Gossip& g = h->registry[gid];
+        if (!delivered(h, K_GOSSIP, s, p, g.hash, tick)) continue;
+        gossip_put(h, pm, gid, r + 1);  // GPI:172,176-179: infectionPeriod = receiver's next round
+        h->st.gossip_first_receipts++;
+        auto& slot = h->inbox[p][g.subject];
+        slot = std::max(slot, g.record);
+      }
+    }
+  }
+  // sweepGossips (GPI:281-304), physical removal after every member's sends.
+  for (uint32_t s = 0; s < h->N; ++s) {
+    Member& me = h->m[s];
+    if (!me.alive) continue;
+    const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);
+    for (uint32_t gid = h->gbase; gid < gend; ++gid) {
+      const int64_t inf = gossip_find(h, me, gid);
+      if (inf >= 0 && r > inf + sweep) gossip_erase(h, me, gid);
+    }
+  }
+  // membership apply of the first receipts (MPI:407-414 -> updateMembership MEMBERSHIP_GOSSIP)
+  for (uint32_t p = 0; p < h->N; ++p) {
+    if (h->inbox[p].empty()) continue;
+    const uint32_t snap = h->m[p].others;
+    for (auto& kv : h->inbox[p])
+      update_membership(h, p, kv.first, kv.second, SWIM_R_MEMBERSHIP_GOSSIP, phase, 0, tick, snap, r + 1);
+    h->inbox[p].clear();
+  }
+  finish_phase(h);
+}
+
+// ---------------------------------------------------------------------------------------
+// Suspicion timeouts (MPI:637-647).
+// ---------------------------------------------------------------------------------------
+void suspicion_phase(oracle_handle* h) {
+  const uint32_t phase = h->G + 1;
+  const uint32_t tick = tick_of(h, phase);
+  for (uint32_t i = 0; i < h->N; ++i) {
+    Member& me = h->m[i];
+    if (!me.alive) continue;
+    std::vector<uint32_t> due;
+    for (auto& kv : me.timers)
+      if (kv.second <= h->period) due.push_back(kv.first);
+    const uint32_t snap = me.others;
+    for (uint32_t subj : due) {
+      me.timers.erase(subj);  // MPI:638
+      if (me.table[subj] != SWIM_ABSENT) {  // MPI:639-645: DEAD with the record's incarnation
+        h->st.suspicion_timeouts++;
+        update_membership(h, i, subj, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, phase, 0, tick, snap,
+                          (int64_t)(h->period + 1) * h->G);
+      }
+    }
+  }
+  finish_phase(h);
+}
+
+// ---------------------------------------------------------------------------------------
+// SYNC anti-entropy: doSync (MPI:304-320), selectSyncAddress (MPI:416-427), onSync
+// (MPI:352-373), onSyncAck (MPI:343-349), syncMembership (MPI:463-473).
+// ---------------------------------------------------------------------------------------
+// selectSyncAddress: uniform over seeds U otherMembers (MPI:417-425), by rejection sampling.
+bool select_sync_address(oracle_handle* h, uint32_t i, uint32_t tick, uint32_t* out) {
+  const Member& me = h->m[i];
+  uint64_t count = me.others;
+  for (uint32_t s = 0; s < h->cfg.n_seeds && s < h->N; ++s)
+    if (s != i && me.table[s] == SWIM_ABSENT) ++count;
+  if (count == 0) return false;  // MPI:421-422
+  auto valid = [&](uint32_t x) { return x != i && (me.table[x] != SWIM_ABSENT || x < h->cfg.n_seeds); };
+  uint32_t x = 0;
+  for (uint32_t a = 0; a < 64; ++a) {
+    x = (uint32_t)(((uint64_t)draw(h->seed, K_SYNC_PICK, i, a, 0, tick) * h->N) >> 32);
+    if (valid(x)) {
+      *out = x;
+      return true;
+    }
+  }
+  for (uint32_t d = 1; d <= h->N; ++d) {
+    uint32_t y = (uint32_t)(((uint64_t)x + d) % h->N);
+    if (valid(y)) {
+      *out = y;
+      return true;
+    }
+  }
+  return false;
+}
+
+void sync_phase(oracle_handle* h) {
+  const uint32_t ph_sync = h->G + 2, ph_ack = h->G + 3;
+  const uint32_t tick_s = tick_of(h, ph_sync), tick_a = tick_of(h, ph_ack);
+  const int64_t create_round = (int64_t)(h->period + 1) * h->G;
+  std::vector<SyncReq> reqs;
+  for (uint32_t i = 0; i < h->N; ++i) {
+    Member& me = h->m[i];
+    if (!me.alive) {
+      me.sync_fd = 0xFFFFFFFFu;
+      continue;
+    }
+    uint32_t peer;
+    if ((uint32_t)(h->period % h->S) == i % h->S && select_sync_address(h, i, tick_s, &peer))
+      reqs.push_back({i, peer, 0});
+    if (me.sync_fd != 0xFFFFFFFFu) reqs.push_back({i, me.sync_fd, 1});
+    me.sync_fd = 0xFFFFFFFFu;
+  }
+  h->st.syncs_sent += reqs.size();
+  // prepareSyncDataMsg (MPI:457-461): every SYNC carries its sender's table as of phase start.
+  std::map<uint32_t, std::vector<uint32_t>> snap;
+  for (auto& rq : reqs)
+    if (!snap.count(rq.from)) snap[rq.from] = h->m[rq.from].table;
+  // onSync at each receiver, requests in (receiver, sender, kind) order.
+  std::vector<size_t> order(reqs.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    if (reqs[a].to != reqs[b].to) return reqs[a].to < reqs[b].to;
+    if (reqs[a].from != reqs[b].from) return reqs[a].from < reqs[b].from;
+    return reqs[a].kind < reqs[b].kind;
+  });
+  struct Ack {
+    uint32_t responder, to, kind;
+    std::vector<uint32_t> table;
+  };
+  std::vector<Ack> acks;
+  for (size_t oi : order) {
+    const SyncReq& rq = reqs[oi];
+    if (!delivered(h, K_SYNC, rq.from, rq.to, rq.kind, tick_s)) continue;
+    h->st.syncs_delivered++;
+    Member& me = h->m[rq.to];
+    const uint32_t others_snap = me.others;  // phase-start count (delta deferred)
+    const std::vector<uint32_t>& data = snap[rq.from];
+    const uint32_t attempt = (rq.from << 1) | rq.kind;
+    for (uint32_t c = 0; c < h->N; ++c)  // syncMembership (MPI:468-471), reason SYNC
+      if (data[c] != SWIM_ABSENT)
+        update_membership(h, rq.to, c, data[c], SWIM_R_SYNC, ph_sync, attempt, tick_s, others_snap, create_round);
+    // MPI:357-371: reply SYNC_ACK with the table after the merge
+    if (delivered(h, K_SYNC_ACK, rq.to, rq.from, rq.kind, tick_a)) acks.push_back({rq.to, rq.from, rq.kind, me.table});
+  }
+  finish_phase(h);
+  // onSyncAck at each requester (MPI:343-349), acks in (requester, responder, kind) order.
+  std::sort(acks.begin(), acks.end(), [](const Ack& a, const Ack& b) {
+    if (a.to != b.to) return a.to < b.to;
+    if (a.responder != b.responder) return a.responder < b.responder;
+    return a.kind < b.kind;
+  });
+  for (auto& ak : acks) {
+    h->st.sync_acks_delivered++;
+    Member& me = h->m[ak.to];
+    const uint32_t attempt = (ak.responder << 1) | ak.kind;
+    const uint32_t others_snap = me.others;
+    for (uint32_t c = 0; c < h->N; ++c)
+      if (ak.table[c] != SWIM_ABSENT)
+        update_membership(h, ak.to, c, ak.table[c], SWIM_R_SYNC, ph_ack, attempt, tick_a, others_snap, create_round);
+  }
+  finish_phase(h);
+}
+
+void step_period(oracle_handle* h) {
+  // phase 0: failure detector (FDI:126), one probe per alive member
+  for (uint32_t i = 0; i < h->N; ++i)
+    if (h->m[i].alive) do_ping(h, i);
+  finish_phase(h);
+  // phases 1..G: gossip rounds (GPI:139)
+  for (uint32_t q = 0; q < h->G; ++q) gossip_round(h, q);
+  // phase G+1: suspicion timeouts
+  suspicion_phase(h);
+  // phases G+2, G+3: SYNC / SYNC_ACK
+  sync_phase(h);
+  h->period++;
+  h->st.period = h->period;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_create(const swim_config* cfg, oracle_handle** out) {
+  if (!cfg || !out) return SWIM_EINVAL;
+  if (cfg->n_members < 1 || cfg->n_members > (1u << 24) || cfg->ping_interval_ms <= 0 || cfg->gossip_interval_ms <= 0 ||
+      cfg->gossip_fanout < 1 || cfg->sync_interval_ms <= 0)
+    return SWIM_EINVAL;
+  oracle_handle* h = new (std::nothrow) oracle_handle();
+  if (!h) return SWIM_ENOMEM;
+  h->cfg = *cfg;
+  h->N = cfg->n_members;
+  h->G = (uint32_t)std::max(1, cfg->ping_interval_ms / cfg->gossip_interval_ms);
+  h->S = (uint32_t)std::max(1, cfg->sync_interval_ms / cfg->ping_interval_ms);
+  h->TPP = h->G + 4;
+  h->seed = cfg->seed;
+  h->group.assign(h->N, 0);
+  std::memset(&h->st, 0, sizeof h->st);
+  try {
+    h->m.resize(h->N);
+    for (uint32_t i = 0; i < h->N; ++i) {
+      h->m[i].table.assign(h->N, SWIM_PACK(0, SWIM_ALIVE));  // converged start, all ALIVE inc 0
+      h->m[i].others = h->N - 1;
+      h->m[i].gossips.key.assign(h->rc, EMPTY);
+      h->m[i].gossips.inf.assign(h->rc, 0);
+    }
+    h->inbox.resize(h->N);
+    h->pres.assign(h->N, h->N - 1);
+    h->last_removed.assign(h->N, 0);
+  } catch (...) {
+    delete h;
+    return SWIM_ENOMEM;
+  }
+  *out = h;
+  return SWIM_OK;
+}
+
+int oracle_destroy(oracle_handle* h) {
+  delete h;
+  return SWIM_OK;
+}
+
+int oracle_set_loss(oracle_handle* h, uint32_t loss_bp) {
+  if (!h || loss_bp > 10000) return SWIM_EINVAL;
+  h->loss_bp = loss_bp;
+  return SWIM_OK;
+}
+
+int oracle_set_partition(oracle_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1) {
+  if (!h || !group || n != h->N) return SWIM_EINVAL;
+  h->group.assign(group, group + n);
+  h->part_t0 = t0;
+  h->part_t1 = t1;
+  return SWIM_OK;
+}
+
+int oracle_block_link(oracle_handle* h, uint32_t src, uint32_t dst, int blocked) {
+  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
+  if (h->link.empty()) h->link.assign(((uint64_t)h->N * h->N + 7) / 8, 0);
+  uint64_t bit = (uint64_t)src * h->N + dst;
+  if (blocked)
+    h->link[bit >> 3] |= (uint8_t)(1u << (bit & 7));
+  else
+    h->link[bit >> 3] &= (uint8_t)~(1u << (bit & 7));
+  return SWIM_OK;
+}
+
+int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t c = ids[k];
+    if (c >= h->N) return SWIM_EINVAL;
+    Member& me = h->m[c];
+    if (!me.alive) continue;
+    me.alive = false;
+    me.timers.clear();  // its scheduler is gone
+    for (size_t sl = 0; sl < me.gossips.key.size(); ++sl)
+      if (me.gossips.key[sl] != EMPTY) gossip_erase(h, me, me.gossips.key[sl]);
+    for (uint32_t j = 0; j < h->N; ++j)
+      if (j != c && me.table[j] != SWIM_ABSENT) h->pres[j]--;
+  }
+  return SWIM_OK;
+}
+
+int oracle_step(oracle_handle* h, uint32_t periods) {
+  if (!h) return SWIM_EINVAL;
+  for (uint32_t p = 0; p < periods; ++p) step_period(h);
+  return SWIM_OK;
+}
+
+int oracle_drain_events(oracle_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out) {
+  if (!h || !n_out) return SWIM_EINVAL;
+  std::stable_sort(h->events.begin(), h->events.end(), [](const swim_event& a, const swim_event& b) {
+    if (a.period != b.period) return a.period < b.period;
+    if (a.observer != b.observer) return a.observer < b.observer;
+    if (a.phase != b.phase) return a.phase < b.phase;
+    if (a.subject != b.subject) return a.subject < b.subject;
+    return a.type < b.type;
+  });
+  uint64_t n = std::min<uint64_t>(cap, h->events.size());
+  if (n && buf) std::memcpy(buf, h->events.data(), n * sizeof(swim_event));
+  *n_out = n;
+  int rc = h->events.size() > cap ? SWIM_EOVERFLOW : SWIM_OK;
+  h->events.erase(h->events.begin(), h->events.begin() + (long)n);
+  return rc;
+}
+
+int oracle_read_view(oracle_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
+  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
+  std::memcpy(row, h->m[observer].table.data(), (size_t)n * 4);
+  return SWIM_OK;
+}
+
+int oracle_read_deadlines(oracle_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
+  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
+  std::memset(row, 0, (size_t)n * 4);
+  for (auto& kv : h->m[observer].timers) row[kv.first] = (uint32_t)kv.second + 1u;
+  return SWIM_OK;
+}
+
+int oracle_digest(oracle_handle* h, uint64_t* vd, uint64_t* dd) {
+  if (!h) return SWIM_EINVAL;
+  uint64_t a = 0, b = 0;
+  const uint64_t K = 0x9E3779B97F4A7C15ull;
+  for (uint32_t i = 0; i < h->N; ++i) {
+    const Member& me = h->m[i];
+    for (uint32_t j = 0; j < h->N; ++j)
+      if (me.table[j]) a += fmix64(((uint64_t)i * h->N + j) * K + me.table[j]);
+    for (auto& kv : me.timers) b += fmix64(((uint64_t)i * h->N + kv.first) * K + (uint32_t)(kv.second + 1));
+  }
+  if (vd) *vd = a;
+  if (dd) *dd = b;
+  return SWIM_OK;
+}
+
+int oracle_read_presence(oracle_handle* h, uint32_t* present, uint32_t* last_removed, uint32_t n) {
+  if (!h || n != h->N) return SWIM_EINVAL;
+  if (present) std::memcpy(present, h->pres.data(), (size_t)n * 4);
+  if (last_removed) std::memcpy(last_removed, h->last_removed.data(), (size_t)n * 4);
+  return SWIM_OK;
+}
+
+int oracle_stats_get(oracle_handle* h, swim_stats* out) {
+  if (!h || !out) return SWIM_EINVAL;
+  *out = h->st;
+  out->live_gossip_slots = 0;  // storage detail of the device ring, not modelled here
+  uint64_t nc = 0;
+  for (uint32_t j = 0; j < h->N; ++j)
+    if (!h->m[j].alive) nc += h->pres[j];
+  out->not_converged = nc;
+  return SWIM_OK;
+}
+
+int oracle_is_overrides(uint32_t r1, uint32_t r0) { return is_overrides(r1, r0) ? 1 : 0; }
+
+uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick) {
+  return draw(seed, kind, a, b, c, tick);
+}
+
+int64_t oracle_cluster_math(int which, int32_t mult, int32_t n, int32_t fanout) {
+  switch (which) {
+    case 0:
+      return ceil_log2(n);
+    case 1:
+      return periods_to_spread(mult, n);
+    case 2:
+      return periods_to_sweep(mult, n);
+    case 3:
+      return suspicion_periods(mult, n);
+    case 4:
+      return (int64_t)fanout * mult * ceil_log2(n);  // CM:65-67
+    default:
+      return -1;
+  }
+}
+
+uint32_t oracle_perm(uint32_t x, uint32_t n, const uint32_t* keys4) { return perm(x, n, keys4); }
+
+}  // extern "C"

@@ -1,0 +1,603 @@
+// swim_api.hip — host side of libswimhip.so: the C ABI declared in include/swimhip.h.
+//
+// Owns all device state of one simulated cluster and launches one protocol period as a fixed
+// sequence of kernels on the handle's stream (no host round trips inside a period). This is
+// the replacement for ClusterImpl's per-member wiring of FailureDetectorImpl,
+// GossipProtocolImpl and MembershipProtocolImpl (core/ClusterImpl.java:170-227) for N members.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "swim_kernels.hip"
+
+using namespace swim;
+
+namespace {
+
+constexpr int NCLASS = 8;  // timing classes, see swim_kernel_time
+
+uint32_t pow2ceil(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+}
+
+}  // namespace
+
+struct swim_handle {
+  swim_config cfg{};
+  uint32_t N = 0, G = 1, S = 1, TPP = 5, GC = 0, scap = 0, dcap = 0, ecap = 0;
+  uint64_t period = 0;
+  uint64_t part_t0 = 0, part_t1 = 0;
+  hipStream_t stream = nullptr;
+  KP base{};
+  unsigned long long* d_digest = nullptr;
+  std::vector<void*> allocs;
+  std::string err;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  struct Pending {
+    int cls;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  double acc_ms[NCLASS] = {0};
+  uint64_t acc_n[NCLASS] = {0};
+};
+
+namespace {
+
+int fail(swim_handle* h, int code, const std::string& what) {
+  if (h) h->err = what;
+  return code;
+}
+
+#define HIPC(h, expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return fail((h), SWIM_EHIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename T>
+int dalloc(swim_handle* h, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess)
+    return fail(h, SWIM_ENOMEM, "hipMalloc(" + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
+  h->allocs.push_back(q);
+  *p = (T*)q;
+  return SWIM_OK;
+}
+
+void free_all(swim_handle* h) {
+  for (void* p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  for (auto ev : h->pool) (void)hipEventDestroy(ev);
+  for (auto& pe : h->pending) {
+    (void)hipEventDestroy(pe.a);
+    (void)hipEventDestroy(pe.b);
+  }
+  h->pool.clear();
+  h->pending.clear();
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  h->stream = nullptr;
+}
+
+hipEvent_t take_event(swim_handle* h) {
+  if (!h->pool.empty()) {
+    hipEvent_t e = h->pool.back();
+    h->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void resolve_timing(swim_handle* h) {
+  for (auto& pe : h->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+      h->acc_ms[pe.cls] += ms;
+      h->acc_n[pe.cls] += 1;
+    }
+    h->pool.push_back(pe.a);
+    h->pool.push_back(pe.b);
+  }
+  h->pending.clear();
+}
+
+// launch helper: optional per-launch HIP-event bracketing on the handle's stream
+template <typename F>
+void timed(swim_handle* h, int cls, F&& launch) {
+  if (!h->timing) {
+    launch();
+    return;
+  }
+  hipEvent_t a = take_event(h), b = take_event(h);
+  (void)hipEventRecord(a, h->stream);
+  launch();
+  (void)hipEventRecord(b, h->stream);
+  h->pending.push_back({cls, a, b});
+}
+
+uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)std::max<uint64_t>(1, (n + bs - 1) / bs); }
+
+void memset_ctl_u32(swim_handle* h, size_t offset) {
+  (void)hipMemsetAsync(reinterpret_cast<char*>(h->base.ctl) + offset, 0, 4, h->stream);
+}
+
+// One protocol period.
+int step_one(swim_handle* h) {
+  KP P = h->base;
+  const uint32_t t = (uint32_t)h->period;
+  const uint32_t N = h->N, G = h->G, TPP = h->TPP;
+  P.period = t;
+  P.part_active = (h->period >= h->part_t0 && h->period < h->part_t1) ? 1u : 0u;
+  const uint32_t gN = blocks_for(N, 256);
+  hipStream_t s = h->stream;
+
+  // phase 0: failure detector
+  P.phase = 0;
+  P.tick = t * TPP;
+  P.round = t * G;
+  P.create_round = t * G;
+  timed(h, 0, [&] { hipLaunchKernelGGL(k_fd, dim3(gN), dim3(256), 0, s, P); });
+
+  // phases 1..G: gossip rounds
+  for (uint32_t q = 0; q < G; ++q) {
+    P.phase = 1 + q;
+    P.tick = t * TPP + 1 + q;
+    P.round = t * G + q;
+    P.create_round = t * G + q + 1;
+    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(64), 0, s, P); });
+    timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_send, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
+    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, s, P); });
+    timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
+  }
+
+  // phase G+1: suspicion timeouts
+  P.phase = G + 1;
+  P.tick = t * TPP + G + 1;
+  P.create_round = (t + 1) * G;
+  memset_ctl_u32(h, offsetof(Ctl, due_count));
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_due, dim3(gN), dim3(256), 0, s, P); });
+  timed(h, 3, [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
+
+  // phase G+2: SYNC
+  P.phase = G + 2;
+  P.tick = t * TPP + G + 2;
+  memset_ctl_u32(h, offsetof(Ctl, stage_count));
+  (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_select, dim3(gN), dim3(256), 0, s, P); });
+  timed(h, 6, [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * N, 256)), dim3(256), 0, s, P); });
+  timed(h, 4, [&] { hipLaunchKernelGGL(k_sync_merge, dim3(N), dim3(256), 0, s, P); });
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
+
+  // phase G+3: SYNC_ACK
+  P.phase = G + 3;
+  P.tick = t * TPP + G + 3;
+  timed(h, 5, [&] { hipLaunchKernelGGL(k_sync_ack, dim3(N), dim3(256), 0, s, P); });
+  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
+
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  h->period++;
+  return SWIM_OK;
+}
+
+int check_overflow(swim_handle* h) {
+  uint32_t ov = 0;
+  HIPC(h, hipMemcpyAsync(&ov, &h->base.ctl->overflow, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (ov) {
+    char buf[160];
+    std::snprintf(buf, sizeof buf,
+                  "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 dirty list, "
+                  "16 sync bucket)",
+                  ov);
+    return fail(h, SWIM_EOVERFLOW, buf);
+  }
+  return SWIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int swim_create(const swim_config* cfg, swim_handle** out) {
+  if (!cfg || !out) return SWIM_EINVAL;
+  *out = nullptr;
+  const swim_config& c = *cfg;
+  if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode != 0 || c.ping_interval_ms <= 0 ||
+      c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
+      c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
+    return SWIM_EINVAL;
+  if (c.gossip_capacity && (c.gossip_capacity & (c.gossip_capacity - 1))) return SWIM_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EHIP;
+
+  swim_handle* h = new (std::nothrow) swim_handle();
+  if (!h) return SWIM_ENOMEM;
+  h->cfg = c;
+  const uint32_t N = c.n_members;
+  h->N = N;
+  h->G = (uint32_t)std::max(1, c.ping_interval_ms / c.gossip_interval_ms);
+  h->S = (uint32_t)std::max(1, c.sync_interval_ms / c.ping_interval_ms);
+  h->TPP = h->G + 4;
+  h->GC = c.gossip_capacity ? c.gossip_capacity : std::min<uint32_t>(pow2ceil(std::max<uint64_t>(1024, 2ull * N)), 65536u);
+  h->scap = c.sync_capacity ? c.sync_capacity : std::min<uint32_t>(2u * N, 8192u);
+  h->dcap = c.dirty_capacity ? c.dirty_capacity : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(65536, 64ull * N));
+  h->ecap = c.event_capacity;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return SWIM_EHIP;
+  }
+
+  KP& P = h->base;
+  P.N = N;
+  P.GC = h->GC;
+  P.gmask = h->GC - 1;
+  P.G = h->G;
+  P.S = h->S;
+  P.f = (uint32_t)c.gossip_fanout;
+  P.kreq = (uint32_t)c.ping_req_members;
+  P.rm = (uint32_t)c.gossip_repeat_mult;
+  P.mult = (uint32_t)c.suspicion_mult;
+  P.n_seeds = c.n_seeds;
+  P.time_left_pos = (c.ping_interval_ms - c.ping_timeout_ms) > 0 ? 1u : 0u;
+  P.sweepmax = 2u * (P.rm * bitlen(N) + 1u);
+  P.ecap = h->ecap;
+  P.scap = h->scap;
+  P.dcap = h->dcap;
+  P.seed = c.seed;
+  P.loss_mode = 0;
+  P.loss_thr = 0;
+  P.link = nullptr;
+
+  const size_t NN = (size_t)N * N;
+  int rc = SWIM_OK;
+  uint8_t* group = nullptr;
+#define ALLOC(ptr, count)                       \
+  if (rc == SWIM_OK) rc = dalloc(h, &(ptr), (count));
+  ALLOC(P.view, NN);
+  ALLOC(P.dl, NN);
+  ALLOC(P.inbox, NN);
+  ALLOC(P.hold, (size_t)N * h->GC);
+  ALLOC(P.colmin, N);
+  ALLOC(P.cnt, N);
+  ALLOC(P.cnt_delta, N);
+  ALLOC(P.alive, N);
+  ALLOC(group, N);
+  ALLOC(P.fd_epoch, N);
+  ALLOC(P.fd_cursor, N);
+  ALLOC(P.g_epoch, N);
+  ALLOC(P.g_cursor, N);
+  ALLOC(P.gseq, N);
+  ALLOC(P.sync_fd, N);
+  ALLOC(P.g_subject, h->GC);
+  ALLOC(P.g_record, h->GC);
+  ALLOC(P.g_hash, h->GC);
+  ALLOC(P.g_create, h->GC);
+  ALLOC(P.g_expiry, h->GC);
+  ALLOC(P.dirty, h->dcap);
+  ALLOC(P.due, N);
+  ALLOC(P.events, std::max<uint32_t>(1, h->ecap));
+  ALLOC(P.pres, N);
+  ALLOC(P.last_removed, N);
+  ALLOC(P.req_to, 2ull * N);
+  ALLOC(P.req_stage, 2ull * N);
+  ALLOC(P.stage_req, h->scap);
+  ALLOC(P.stage_sync, (size_t)h->scap * N);
+  ALLOC(P.stage_ack, (size_t)h->scap * N);
+  ALLOC(P.recv_count, N);
+  ALLOC(P.recv_off, N + 1ull);
+  ALLOC(P.recv_fill, N);
+  ALLOC(P.bucket, h->scap);
+  ALLOC(P.ctl, 1);
+  ALLOC(h->d_digest, 2);
+#undef ALLOC
+  P.group = group;
+  if (rc != SWIM_OK) {
+    std::fprintf(stderr, "swim_create: %s\n", h->err.c_str());
+    free_all(h);
+    delete h;
+    return rc;
+  }
+  hipStream_t s = h->stream;
+  const uint32_t fill_blocks = 4096;
+  // converged start: every view holds every member ALIVE incarnation 0 (MPI:139 + initial SYNC)
+  hipLaunchKernelGGL(k_fill_u32, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, SWIM_PACK(0, SWIM_ALIVE));
+  (void)hipMemsetAsync(P.dl, 0, NN * 4, s);
+  (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
+  (void)hipMemsetAsync(P.hold, 0, (size_t)N * h->GC * 4, s);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmin, (size_t)N, NONE);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, N - 1);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, N - 1);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.sync_fd, (size_t)N, NONE);
+  (void)hipMemsetAsync(P.cnt_delta, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.alive, 1, N, s);
+  (void)hipMemsetAsync(group, 0, N, s);
+  (void)hipMemsetAsync(P.fd_epoch, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.fd_cursor, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.g_epoch, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.g_cursor, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.gseq, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.g_expiry, 0, (size_t)h->GC * 4, s);
+  (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
+  (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "swim_create: init failed: %s\n", hipGetErrorString(e));
+    free_all(h);
+    delete h;
+    return SWIM_EHIP;
+  }
+  *out = h;
+  return SWIM_OK;
+}
+
+int swim_destroy(swim_handle* h) {
+  if (!h) return SWIM_EINVAL;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_all(h);
+  delete h;
+  return SWIM_OK;
+}
+
+int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
+  if (!h || loss_bp > 10000) return SWIM_EINVAL;
+  KP& P = h->base;
+  if (loss_bp == 0) {
+    P.loss_mode = 0;
+  } else if (loss_bp >= 10000) {
+    P.loss_mode = 2;
+  } else {
+    P.loss_mode = 1;
+    P.loss_thr = (uint32_t)(((uint64_t)loss_bp << 32) / 10000u);
+  }
+  return SWIM_OK;
+}
+
+int swim_set_partition(swim_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1) {
+  if (!h || !group || n != h->N) return SWIM_EINVAL;
+  HIPC(h, hipMemcpyAsync(const_cast<uint8_t*>(h->base.group), group, n, hipMemcpyHostToDevice, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  h->part_t0 = t0;
+  h->part_t1 = t1;
+  return SWIM_OK;
+}
+
+int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked) {
+  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
+  KP& P = h->base;
+  const size_t bytes = ((size_t)h->N * h->N + 7) / 8;
+  if (!P.link) {
+    uint8_t* l = nullptr;
+    int rc = dalloc(h, &l, bytes);
+    if (rc) return rc;
+    HIPC(h, hipMemsetAsync(l, 0, bytes, h->stream));
+    P.link = l;
+  }
+  const uint64_t bit = (uint64_t)src * h->N + dst;
+  uint8_t byte = 0;
+  uint8_t* dp = const_cast<uint8_t*>(P.link) + (bit >> 3);
+  HIPC(h, hipMemcpyAsync(&byte, dp, 1, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (blocked)
+    byte |= (uint8_t)(1u << (bit & 7));
+  else
+    byte &= (uint8_t) ~(1u << (bit & 7));
+  HIPC(h, hipMemcpyAsync(dp, &byte, 1, hipMemcpyHostToDevice, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  std::vector<uint8_t> alive(h->N);
+  HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, h->N, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t c = ids[k];
+    if (c >= h->N) return SWIM_EINVAL;
+    if (!alive[c]) continue;
+    alive[c] = 0;
+    hipLaunchKernelGGL(k_crash, dim3(blocks_for(h->N, 256)), dim3(256), 0, h->stream, h->base, c);
+  }
+  HIPC(h, hipMemcpyAsync(h->base.alive, alive.data(), h->N, hipMemcpyHostToDevice, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
+int swim_step_async(swim_handle* h, uint32_t periods) {
+  if (!h) return SWIM_EINVAL;
+  for (uint32_t p = 0; p < periods; ++p) {
+    int rc = step_one(h);
+    if (rc) return rc;
+  }
+  return SWIM_OK;
+}
+
+int swim_sync(swim_handle* h) {
+  if (!h) return SWIM_EINVAL;
+  HIPC(h, hipStreamSynchronize(h->stream));
+  resolve_timing(h);
+  return check_overflow(h);
+}
+
+int swim_step(swim_handle* h, uint32_t periods) {
+  int rc = swim_step_async(h, periods);
+  if (rc) return rc;
+  return swim_sync(h);
+}
+
+int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out) {
+  if (!h || !n_out) return SWIM_EINVAL;
+  uint32_t cnt = 0;
+  HIPC(h, hipMemcpyAsync(&cnt, &h->base.ctl->event_count, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  const uint32_t have = std::min(cnt, h->ecap);
+  std::vector<swim_event> ev(have);
+  if (have) HIPC(h, hipMemcpyAsync(ev.data(), h->base.events, (size_t)have * sizeof(swim_event), hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemsetAsync(&h->base.ctl->event_count, 0, 4, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  std::sort(ev.begin(), ev.end(), [](const swim_event& a, const swim_event& b) {
+    if (a.period != b.period) return a.period < b.period;
+    if (a.observer != b.observer) return a.observer < b.observer;
+    if (a.phase != b.phase) return a.phase < b.phase;
+    if (a.subject != b.subject) return a.subject < b.subject;
+    return a.type < b.type;
+  });
+  const uint64_t n = std::min<uint64_t>(cap, ev.size());
+  if (n && buf) std::memcpy(buf, ev.data(), n * sizeof(swim_event));
+  *n_out = n;
+  if (cnt > h->ecap || ev.size() > cap) return fail(h, SWIM_EOVERFLOW, "event buffer overflow");
+  return SWIM_OK;
+}
+
+int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
+  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
+  HIPC(h, hipMemcpyAsync(row, h->base.view + (size_t)observer * h->N, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
+  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
+  // subject-major storage: strided 2D copy of one observer column
+  HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + observer, (size_t)h->N * 4, 4, h->N, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_digest(swim_handle* h, uint64_t* vd, uint64_t* dd) {
+  if (!h) return SWIM_EINVAL;
+  HIPC(h, hipMemsetAsync(h->d_digest, 0, 16, h->stream));
+  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base.view, h->base.dl, h->N, h->d_digest);
+  unsigned long long out[2];
+  HIPC(h, hipMemcpyAsync(out, h->d_digest, 16, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (vd) *vd = out[0];
+  if (dd) *dd = out[1];
+  return SWIM_OK;
+}
+
+int swim_read_presence(swim_handle* h, uint32_t* present, uint32_t* last_removed, uint32_t n) {
+  if (!h || n != h->N) return SWIM_EINVAL;
+  if (present) HIPC(h, hipMemcpyAsync(present, h->base.pres, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (last_removed)
+    HIPC(h, hipMemcpyAsync(last_removed, h->base.last_removed, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_stats_get(swim_handle* h, swim_stats* out) {
+  if (!h || !out) return SWIM_EINVAL;
+  Ctl ctl;
+  HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
+  std::vector<uint32_t> pres(h->N);
+  std::vector<uint8_t> alive(h->N);
+  HIPC(h, hipMemcpyAsync(pres.data(), h->base.pres, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, h->N, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  std::memset(out, 0, sizeof *out);
+  out->period = h->period;
+  out->fd_probes = ctl.stats[ST_FD_PROBES];
+  out->fd_direct_ok = ctl.stats[ST_FD_DIRECT_OK];
+  out->fd_ping_req = ctl.stats[ST_FD_PING_REQ];
+  out->fd_suspect_events = ctl.stats[ST_FD_SUSPECT_EV];
+  out->fd_alive_events = ctl.stats[ST_FD_ALIVE_EV];
+  out->gossips_created = ctl.stats[ST_GOSSIPS_CREATED];
+  out->gossip_first_receipts = ctl.stats[ST_GOSSIP_RECEIPTS];
+  out->gossip_sends = ctl.stats[ST_GOSSIP_SENDS];
+  out->syncs_sent = ctl.stats[ST_SYNCS_SENT];
+  out->syncs_delivered = ctl.stats[ST_SYNCS_DELIVERED];
+  out->sync_acks_delivered = ctl.stats[ST_ACKS_DELIVERED];
+  out->records_accepted = ctl.stats[ST_ACCEPTED];
+  out->events_added = ctl.stats[ST_ADDED];
+  out->events_removed = ctl.stats[ST_REMOVED];
+  out->suspicion_timeouts = ctl.stats[ST_SUSP_TIMEOUTS];
+  out->refutations = ctl.stats[ST_REFUTATIONS];
+  out->overflow = ctl.overflow;
+  out->live_gossip_slots = ctl.gcount - ctl.glo;
+  uint64_t nc = 0;
+  for (uint32_t j = 0; j < h->N; ++j)
+    if (!alive[j]) nc += pres[j];
+  out->not_converged = nc;
+  return SWIM_OK;
+}
+
+const char* swim_last_error(swim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int swim_kat_is_overrides(const uint32_t* r1, const uint32_t* r0, uint8_t* out, uint64_t n) {
+  if (!r1 || !r0 || !out) return SWIM_EINVAL;
+  if (n == 0) return SWIM_OK;
+  uint32_t *d1 = nullptr, *d0 = nullptr;
+  uint8_t* dout = nullptr;
+  if (hipMalloc(&d1, n * 4) != hipSuccess || hipMalloc(&d0, n * 4) != hipSuccess || hipMalloc(&dout, n) != hipSuccess)
+    return SWIM_EHIP;
+  int rc = SWIM_OK;
+  if (hipMemcpy(d1, r1, n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d0, r0, n * 4, hipMemcpyHostToDevice) != hipSuccess)
+    rc = SWIM_EHIP;
+  if (rc == SWIM_OK) {
+    hipLaunchKernelGGL(k_kat_overrides, dim3(blocks_for(n, 256)), dim3(256), 0, 0, d1, d0, dout, n);
+    if (hipMemcpy(out, dout, n, hipMemcpyDeviceToHost) != hipSuccess) rc = SWIM_EHIP;
+  }
+  (void)hipFree(d1);
+  (void)hipFree(d0);
+  (void)hipFree(dout);
+  return rc;
+}
+
+int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out, uint64_t n) {
+  if (!abct || !out) return SWIM_EINVAL;
+  if (n == 0) return SWIM_OK;
+  uint32_t *din = nullptr, *dout = nullptr;
+  if (hipMalloc(&din, n * 16) != hipSuccess || hipMalloc(&dout, n * 4) != hipSuccess) return SWIM_EHIP;
+  int rc = SWIM_OK;
+  if (hipMemcpy(din, abct, n * 16, hipMemcpyHostToDevice) != hipSuccess) rc = SWIM_EHIP;
+  if (rc == SWIM_OK) {
+    hipLaunchKernelGGL(k_kat_philox, dim3(blocks_for(n, 256)), dim3(256), 0, 0, seed, kind, din, dout, n);
+    if (hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = SWIM_EHIP;
+  }
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
+}
+
+int swim_kernel_time(swim_handle* h, uint32_t idx, double* ms, uint64_t* launches) {
+  if (!h || idx >= (uint32_t)NCLASS) return SWIM_EINVAL;
+  if (ms) *ms = h->acc_ms[idx];
+  if (launches) *launches = h->acc_n[idx];
+  return SWIM_OK;
+}
+
+int swim_kernel_time_reset(swim_handle* h, int enable) {
+  if (!h) return SWIM_EINVAL;
+  (void)hipStreamSynchronize(h->stream);
+  resolve_timing(h);
+  for (int i = 0; i < NCLASS; ++i) {
+    h->acc_ms[i] = 0;
+    h->acc_n[i] = 0;
+  }
+  h->timing = enable != 0;
+  return SWIM_OK;
+}
+
+}  // extern "C"

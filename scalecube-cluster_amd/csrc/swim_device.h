@@ -1,0 +1,256 @@
+// swim_device.h — device-side state, kernel parameters and the shared updateMembership.
+//
+// Data layout in HBM (dense mode, N members, GC gossip slots):
+//   view   u32[N][N]  observer-major packed records  (MembershipProtocolImpl.java:87)
+//   dl     u32[N][N]  SUBJECT-major suspicion deadlines (+1, 0 = none) so the timeout sweep
+//                     streams one subject column over all observers (MembershipProtocolImpl.java:101)
+//   inbox  u32[N][N]  observer-major lattice max of the records a gossip round delivered
+//   hold   u32[N][GC] member-major gossip holdings: infectionPeriod + 1, 0 = not held
+//                     (GossipProtocolImpl.java:49, GossipState.java:14)
+// plus per-member vectors (cursors, counts, liveness) and per-slot gossip metadata.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/swimhip.h"
+#include "swim_rng.h"
+
+namespace swim {
+
+// control block counters (device, zeroed at create)
+enum StatIdx : int {
+  ST_FD_PROBES = 0,
+  ST_FD_DIRECT_OK,
+  ST_FD_PING_REQ,
+  ST_FD_SUSPECT_EV,
+  ST_FD_ALIVE_EV,
+  ST_GOSSIPS_CREATED,
+  ST_GOSSIP_RECEIPTS,
+  ST_GOSSIP_SENDS,
+  ST_SYNCS_SENT,
+  ST_SYNCS_DELIVERED,
+  ST_ACKS_DELIVERED,
+  ST_ACCEPTED,
+  ST_ADDED,
+  ST_REMOVED,
+  ST_SUSP_TIMEOUTS,
+  ST_REFUTATIONS,
+  ST_COUNT
+};
+
+enum Overflow : uint32_t {
+  OV_EVENTS = 1u,
+  OV_GOSSIP = 2u,
+  OV_SYNC = 4u,
+  OV_DIRTY = 8u,
+  OV_BUCKET = 16u,
+};
+
+struct Ctl {
+  unsigned long long stats[ST_COUNT];
+  uint32_t gcount;      // gossips ever created (ids); slot = id & (GC-1)
+  uint32_t glo;         // oldest possibly-live gossip id
+  uint32_t scan_lo;     // [scan_lo, scan_hi) ids scanned by the send kernel this round
+  uint32_t scan_hi;
+  uint32_t dirty_count; // (observer, subject) inbox cells touched this round
+  uint32_t event_count;
+  uint32_t stage_count; // staged SYNC requests this period
+  uint32_t due_count;   // subject columns due for the suspicion sweep
+  uint32_t overflow;
+  uint32_t pad[7];
+};
+
+// Everything a kernel needs, passed by value.
+struct KP {
+  // sizes / config
+  uint32_t N, GC, gmask, G, S, f, kreq, rm, mult, n_seeds, time_left_pos;
+  uint32_t sweepmax;
+  uint32_t ecap, scap, dcap;
+  uint64_t seed;
+  // clock
+  uint32_t period, round, phase, tick, create_round;
+  // link model
+  uint32_t loss_thr;  // lost iff draw < loss_thr (when 0 < loss < 100 %)
+  uint32_t loss_mode; // 0 none, 1 probabilistic, 2 all lost
+  uint32_t part_active;
+  const uint8_t* group;
+  const uint8_t* link;  // directed block bitmap or nullptr
+  // state
+  uint32_t* view;
+  uint32_t* dl;
+  uint32_t* colmin;
+  uint32_t* inbox;
+  uint32_t* hold;
+  uint32_t* cnt;
+  int32_t* cnt_delta;
+  uint8_t* alive;
+  uint32_t* fd_epoch;
+  uint32_t* fd_cursor;
+  uint32_t* g_epoch;
+  uint32_t* g_cursor;
+  uint32_t* gseq;
+  uint32_t* sync_fd;
+  uint32_t* g_subject;
+  uint32_t* g_record;
+  uint32_t* g_hash;
+  uint32_t* g_create;
+  uint32_t* g_expiry;
+  unsigned long long* dirty;
+  uint32_t* due;
+  swim_event* events;
+  uint32_t* pres;
+  uint32_t* last_removed;
+  // sync staging
+  uint32_t* req_to;     // [2N] receiver of request 2i+k, or NONE
+  uint32_t* req_stage;  // [2N] staging slot, or NONE
+  uint32_t* stage_req;  // [scap] request index of a staging slot
+  uint32_t* stage_sync; // [scap][N] SYNC payload (sender's table)
+  uint32_t* stage_ack;  // [scap][N] SYNC_ACK payload (receiver's table after the merge)
+  uint32_t* recv_count; // [N]
+  uint32_t* recv_off;   // [N+1]
+  uint32_t* recv_fill;  // [N]
+  uint32_t* bucket;     // [scap]
+  Ctl* ctl;
+};
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool delivered(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
+                                          uint32_t tick) {
+  if (!P.alive[src] || !P.alive[dst]) return false;
+  if (P.part_active && P.group[src] != P.group[dst]) return false;
+  if (P.link) {
+    const uint64_t bit = (uint64_t)src * P.N + dst;
+    if (P.link[bit >> 3] & (1u << (bit & 7))) return false;
+  }
+  if (P.loss_mode == 0) return true;
+  if (P.loss_mode == 2) return false;
+  return draw1(P.seed, kind, src, dst, c, tick) >= P.loss_thr;
+}
+
+__device__ __forceinline__ uint32_t susp_periods(const KP& P, uint32_t others) { return P.mult * bitlen(others + 1u); }
+__device__ __forceinline__ uint32_t spread_rounds(const KP& P, uint32_t others) { return P.rm * bitlen(others + 1u); }
+__device__ __forceinline__ uint32_t sweep_rounds(const KP& P, uint32_t others) {
+  return 2u * (spread_rounds(P, others) + 1u);
+}
+
+__device__ __forceinline__ void push_event(const KP& P, uint32_t obs, uint32_t subj, uint32_t type, uint32_t reason,
+                                           uint32_t record) {
+  if (P.ecap == 0) return;
+  const uint32_t idx = atomicAdd(&P.ctl->event_count, 1u);
+  if (idx >= P.ecap) {
+    atomicOr(&P.ctl->overflow, OV_EVENTS);
+    return;
+  }
+  swim_event e;
+  e.period = P.period;
+  e.observer = obs;
+  e.subject = subj;
+  e.record = record;
+  e.type = (uint8_t)type;
+  e.reason = (uint8_t)reason;
+  e.phase = (uint8_t)P.phase;
+  e.pad = 0;
+  P.events[idx] = e;
+}
+
+struct Tally {
+  uint32_t accepted = 0, refut = 0, added = 0, removed = 0;
+};
+
+// GossipProtocolImpl.spread -> createAndPutGossip (GossipProtocolImpl.java:124-128,163-169):
+// allocate a ring slot, publish the record, the origin holds it from `create_round`.
+__device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32_t subject, uint32_t record,
+                                            uint32_t seq) {
+  const uint32_t id = atomicAdd(&P.ctl->gcount, 1u);
+  const uint32_t s = id & P.gmask;
+  if (id >= P.GC && P.g_expiry[s] >= P.create_round) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  P.g_subject[s] = subject;
+  P.g_record[s] = record;
+  P.g_hash[s] = gossip_hash(origin, seq);
+  P.g_create[s] = P.create_round;
+  P.g_expiry[s] = P.create_round + P.sweepmax;
+  P.hold[(size_t)origin * P.GC + s] = P.create_round + 1u;
+}
+
+// MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip.
+__device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t subj, uint32_t attempt) {
+  return delivered(P, K_MREQ, obs, subj, attempt, P.tick) && delivered(P, K_MRESP, subj, obs, attempt, P.tick);
+}
+
+// MembershipProtocolImpl.updateMembership (MembershipProtocolImpl.java:481-547) and callees
+// (onSelfMemberDetected :549-569, onDeadMemberDetected :571-587, onAliveMemberDetected
+// :589-610, schedule/cancelSuspicionTimeoutTask :612-635, spreadMembershipGossipUnlessGossiped
+// :649-656). Returns the record to gossip (0 = none); the caller assigns the gossip sequence
+// number so that every origin's ids are canonical.
+__device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint32_t subj, uint32_t r1,
+                                                 uint32_t reason, uint32_t attempt, uint32_t others_snap, Tally& T) {
+  uint32_t* cellp = P.view + (size_t)obs * P.N + subj;
+  const uint32_t r0 = *cellp;
+  if (!is_overrides(r1, r0)) return 0u;
+  const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;
+  if (subj == obs) {
+    const uint32_t inc1 = (r1 == SWIM_DEAD) ? rec_inc(r0) : rec_inc(r1);
+    const uint32_t inc0 = rec_inc(r0);
+    const uint32_t r2 = SWIM_PACK((inc0 > inc1 ? inc0 : inc1) + 1u, rec_code(r0));
+    *cellp = r2;
+    T.accepted++;
+    T.refut++;
+    return r2;
+  }
+  uint32_t* dlp = P.dl + (size_t)subj * P.N + obs;
+  if (r1 == SWIM_DEAD) {
+    *dlp = 0u;
+    *cellp = SWIM_ABSENT;
+    atomicSub(&P.cnt_delta[obs], 1);
+    atomicSub(&P.pres[subj], 1u);
+    atomicMax(&P.last_removed[subj], P.period + 1u);
+    T.accepted++;
+    T.removed++;
+    push_event(P, obs, subj, SWIM_EV_REMOVED, reason, r0);
+    return 0u;
+  }
+  if (rec_code(r1) == SWIM_SUSPECT) {
+    *cellp = r1;
+    T.accepted++;
+    if (*dlp == 0u) {
+      const uint32_t dl = P.period + susp_periods(P, others_snap);
+      *dlp = dl + 1u;
+      atomicMin(&P.colmin[subj], dl);
+    }
+    return spread ? r1 : 0u;
+  }
+  if (!fetch_ok(P, obs, subj, attempt)) return 0u;
+  *dlp = 0u;
+  *cellp = r1;
+  T.accepted++;
+  if (r0 == SWIM_ABSENT) {
+    atomicAdd(&P.cnt_delta[obs], 1);
+    atomicAdd(&P.pres[subj], 1u);
+    T.added++;
+    push_event(P, obs, subj, SWIM_EV_ADDED, reason, r1);
+  }
+  return spread ? r1 : 0u;
+}
+
+// ---- wave / block reductions (wave64) -------------------------------------------------
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&P.ctl->stats[idx], (unsigned long long)v);
+}
+
+__device__ __forceinline__ void flush_tally(const KP& P, const Tally& T) {
+  add_stat(P, ST_ACCEPTED, T.accepted);
+  add_stat(P, ST_REFUTATIONS, T.refut);
+  add_stat(P, ST_ADDED, T.added);
+  add_stat(P, ST_REMOVED, T.removed);
+}
+
+}  // namespace swim

@@ -1,0 +1,174 @@
+"""ctypes mirror of include/swimhip.h and the loader for libswimhip.so.
+
+The product path is the HIP library only: `load_swimhip()` raises if the in-tree
+libswimhip.so is missing or cannot be loaded — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)  # scalecube-cluster_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(HERE, "libswimhip.so")
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "swimhip.h")
+
+SWIM_OK = 0
+SWIM_EINVAL = -22
+SWIM_ENOMEM = -12
+SWIM_EHIP = -5
+SWIM_ERCCL = -6
+SWIM_EOVERFLOW = -75
+
+ABSENT, ALIVE, SUSPECT, DEAD = 0, 1, 2, 0xFFFFFFFF
+
+EV_ADDED, EV_REMOVED, EV_UPDATED = 1, 2, 3
+R_FAILURE_DETECTOR_EVENT, R_MEMBERSHIP_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_SUSPICION_TIMEOUT = 0, 1, 2, 3, 4
+
+
+def pack(inc: int, code: int) -> int:
+    return ((inc << 2) | code) & 0xFFFFFFFF
+
+
+class SwimConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_members", ctypes.c_uint32),
+        ("mode", ctypes.c_uint32),
+        ("seed", ctypes.c_uint64),
+        ("ping_interval_ms", ctypes.c_int32),
+        ("ping_timeout_ms", ctypes.c_int32),
+        ("ping_req_members", ctypes.c_int32),
+        ("gossip_fanout", ctypes.c_int32),
+        ("gossip_interval_ms", ctypes.c_int32),
+        ("gossip_repeat_mult", ctypes.c_int32),
+        ("sync_interval_ms", ctypes.c_int32),
+        ("sync_timeout_ms", ctypes.c_int32),
+        ("suspicion_mult", ctypes.c_int32),
+        ("metadata_timeout_ms", ctypes.c_int32),
+        ("n_seeds", ctypes.c_uint32),
+        ("gossip_capacity", ctypes.c_uint32),
+        ("event_capacity", ctypes.c_uint32),
+        ("sync_capacity", ctypes.c_uint32),
+        ("dirty_capacity", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+class SwimEvent(ctypes.Structure):
+    _fields_ = [
+        ("period", ctypes.c_uint64),
+        ("observer", ctypes.c_uint32),
+        ("subject", ctypes.c_uint32),
+        ("record", ctypes.c_uint32),
+        ("type", ctypes.c_uint8),
+        ("reason", ctypes.c_uint8),
+        ("phase", ctypes.c_uint8),
+        ("pad", ctypes.c_uint8),
+    ]
+
+
+STAT_FIELDS = [
+    "period",
+    "fd_probes",
+    "fd_direct_ok",
+    "fd_ping_req",
+    "fd_suspect_events",
+    "fd_alive_events",
+    "gossips_created",
+    "gossip_first_receipts",
+    "gossip_sends",
+    "syncs_sent",
+    "syncs_delivered",
+    "sync_acks_delivered",
+    "records_accepted",
+    "events_added",
+    "events_removed",
+    "suspicion_timeouts",
+    "refutations",
+    "overflow",
+    "live_gossip_slots",
+    "not_converged",
+]
+
+
+class SwimStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in STAT_FIELDS]
+
+
+# (name, restype, argtypes) for every entry point of include/swimhip.h
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_pU32 = ctypes.POINTER(ctypes.c_uint32)
+_pU64 = ctypes.POINTER(ctypes.c_uint64)
+_pU8 = ctypes.POINTER(ctypes.c_uint8)
+
+
+def api_table(prefix: str):
+    """Signature table shared by libswimhip (prefix 'swim_') and the oracle ('oracle_')."""
+    return [
+        (prefix + "create", _I, [ctypes.POINTER(SwimConfig), ctypes.POINTER(_P)]),
+        (prefix + "destroy", _I, [_P]),
+        (prefix + "set_loss", _I, [_P, _U32]),
+        (prefix + "set_partition", _I, [_P, _pU8, _U32, _U64, _U64]),
+        (prefix + "block_link", _I, [_P, _U32, _U32, _I]),
+        (prefix + "crash", _I, [_P, _pU32, _U32]),
+        (prefix + "step", _I, [_P, _U32]),
+        (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
+        (prefix + "read_view", _I, [_P, _U32, _pU32, _U32]),
+        (prefix + "read_deadlines", _I, [_P, _U32, _pU32, _U32]),
+        (prefix + "digest", _I, [_P, _pU64, _pU64]),
+        (prefix + "read_presence", _I, [_P, _pU32, _pU32, _U32]),
+        (prefix + "stats_get", _I, [_P, ctypes.POINTER(SwimStats)]),
+    ]
+
+
+SWIM_ONLY = [
+    ("swim_step_async", _I, [_P, _U32]),
+    ("swim_sync", _I, [_P]),
+    ("swim_last_error", ctypes.c_char_p, [_P]),
+    ("swim_kat_is_overrides", _I, [_pU32, _pU32, _pU8, _U64]),
+    ("swim_kat_philox", _I, [_U64, _U32, _pU32, _pU32, _U64]),
+    ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),
+    ("swim_kernel_time_reset", _I, [_P, _I]),
+]
+
+
+def bind(lib, table):
+    for name, res, args in table:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/swimhip.h."""
+    import re
+
+    txt = open(path).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(swim_\w+)\s*\(", txt, re.M)))
+
+
+_LIB = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def load_swimhip():
+    """Load the in-tree HIP library. Fails loudly: no CPU fallback exists."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise NativeMissing(
+            f"libswimhip.so not built at {LIB_PATH}; run __graft_entry__.build() (hipcc --offload-arch=gfx950)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    bind(lib, api_table("swim_") + SWIM_ONLY)
+    _LIB = lib
+    return lib

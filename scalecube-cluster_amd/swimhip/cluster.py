@@ -1,0 +1,217 @@
+"""SwimCluster — N simulated scalecube members stepped in bulk through the C ABI.
+
+The facade mirrors what a user of the reference sees per member:
+  MembershipProtocol.members()/otherMembers()/listen()   (core/membership/MembershipProtocol.java:14-65)
+  MembershipEvent{ADDED, REMOVED, UPDATED}               (api/membership/MembershipEvent.java:11-117)
+  NetworkEmulator loss / block / partition               (cluster-testlib/.../utils/NetworkEmulator.java:58-297)
+  transport.stop() as crash                               (MembershipProtocolTest.java:991-1000)
+
+`SwimCluster(...)` always drives libswimhip.so (HIP, gfx950). The class is also used by the test
+suite with the oracle's function table to compare both implementations call-for-call.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as nat
+from .config import ClusterConfig, to_swim_config
+
+
+class SwimError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with status {code}")
+        self.code = code
+
+
+@dataclass(frozen=True)
+class MembershipEvent:
+    """api/membership/MembershipEvent.java:13-67, plus the simulated observer and period."""
+
+    type: int
+    member: int
+    observer: int
+    period: int
+    record: int
+    reason: int
+    phase: int
+
+    ADDED = nat.EV_ADDED
+    REMOVED = nat.EV_REMOVED
+    UPDATED = nat.EV_UPDATED
+
+    def isAdded(self):
+        return self.type == nat.EV_ADDED
+
+    def isRemoved(self):
+        return self.type == nat.EV_REMOVED
+
+    def isUpdated(self):
+        return self.type == nat.EV_UPDATED
+
+    def key(self):
+        return (self.period, self.observer, self.phase, self.member, self.type, self.reason, self.record)
+
+
+@dataclass(frozen=True)
+class MembershipRecord:
+    """core/membership/MembershipRecord.java:12-109 decoded from a packed cell."""
+
+    member: int
+    status: str
+    incarnation: int
+
+    @staticmethod
+    def decode(member: int, cell: int):
+        if cell == nat.ABSENT:
+            return None
+        if cell == nat.DEAD:
+            return MembershipRecord(member, "DEAD", -1)
+        return MembershipRecord(member, {1: "ALIVE", 2: "SUSPECT"}.get(cell & 3, "?"), cell >> 2)
+
+
+class SwimCluster:
+    def __init__(self, config: ClusterConfig, n_members: int, seed: int = 0, *, event_capacity: int = 0,
+                 gossip_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, _lib=None,
+                 _prefix: str = "swim_"):
+        self._lib = _lib if _lib is not None else nat.load_swimhip()
+        self._p = _prefix
+        self.config = config
+        self.n = int(n_members)
+        self.seed = int(seed)
+        self._cfg = to_swim_config(config, self.n, seed, gossip_capacity=gossip_capacity,
+                                   event_capacity=event_capacity, sync_capacity=sync_capacity,
+                                   dirty_capacity=dirty_capacity)
+        h = ctypes.c_void_p()
+        self._h = None
+        self._call("create", ctypes.byref(self._cfg), ctypes.byref(h))
+        self._h = h
+        self._alive = np.ones(self.n, dtype=bool)
+
+    # -- plumbing -------------------------------------------------------------------------
+    def _fn(self, name):
+        return getattr(self._lib, self._p + name)
+
+    def _call(self, name, *args):
+        rc = self._fn(name)(*args)
+        if rc != nat.SWIM_OK:
+            msg = name
+            if self._p == "swim_" and self._h is not None:
+                err = self._lib.swim_last_error(self._h)
+                if err:
+                    msg += ": " + err.decode(errors="replace")
+            raise SwimError(rc, msg)
+        return rc
+
+    def close(self):
+        if self._h is not None:
+            self._fn("destroy")(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- fault injection (NetworkEmulator) ------------------------------------------------
+    def set_loss(self, percent: float):
+        """setDefaultOutboundSettings(lossPercent, 0) on every member (NetworkEmulator.java:81-84)."""
+        self._call("set_loss", self._h, int(round(percent * 100)))
+
+    def partition(self, groups, t0: int, t1: int):
+        g = np.ascontiguousarray(np.asarray(groups, dtype=np.uint8))
+        assert g.shape == (self.n,)
+        self._call("set_partition", self._h, g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), self.n, t0, t1)
+
+    def block_outbound(self, src: int, dsts, blocked: bool = True):
+        """NetworkEmulator.blockOutbound(Address...) (NetworkEmulator.java:105-119)."""
+        for d in dsts:
+            self._call("block_link", self._h, int(src), int(d), 1 if blocked else 0)
+
+    def unblock_outbound(self, src: int, dsts):
+        self.block_outbound(src, dsts, blocked=False)
+
+    def block_inbound(self, dst: int, srcs, blocked: bool = True):
+        """NetworkEmulator.blockInbound (NetworkEmulator.java:255-269): drops by sender."""
+        for s in srcs:
+            self._call("block_link", self._h, int(s), int(dst), 1 if blocked else 0)
+
+    def crash(self, ids):
+        ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
+        self._call("crash", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+        self._alive[ids] = False
+
+    # -- stepping -------------------------------------------------------------------------
+    def step(self, periods: int = 1):
+        self._call("step", self._h, int(periods))
+
+    # -- observation ----------------------------------------------------------------------
+    def view(self, observer: int) -> np.ndarray:
+        row = np.zeros(self.n, dtype=np.uint32)
+        self._call("read_view", self._h, int(observer), row.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), self.n)
+        return row
+
+    def views(self) -> np.ndarray:
+        return np.stack([self.view(i) for i in range(self.n)])
+
+    def deadlines(self, observer: int) -> np.ndarray:
+        row = np.zeros(self.n, dtype=np.uint32)
+        self._call("read_deadlines", self._h, int(observer), row.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                   self.n)
+        return row
+
+    def digest(self):
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._call("digest", self._h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def presence(self):
+        pres = np.zeros(self.n, dtype=np.uint32)
+        last = np.zeros(self.n, dtype=np.uint32)
+        self._call("read_presence", self._h, pres.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                   last.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), self.n)
+        return pres, last
+
+    def stats(self) -> dict:
+        s = nat.SwimStats()
+        self._call("stats_get", self._h, ctypes.byref(s))
+        return {f: getattr(s, f) for f in nat.STAT_FIELDS}
+
+    def events(self, cap: int = 1 << 20):
+        buf = (nat.SwimEvent * cap)()
+        n = ctypes.c_uint64()
+        self._call("drain_events", self._h, buf, cap, ctypes.byref(n))
+        return [
+            MembershipEvent(e.type, e.subject, e.observer, e.period, e.record, e.reason, e.phase)
+            for e in buf[: n.value]
+        ]
+
+    # -- MembershipProtocol-shaped accessors (MembershipProtocol.java:14-65) ----------------
+    def members(self, observer: int):
+        row = self.view(observer)
+        return [int(j) for j in np.nonzero(row)[0]]
+
+    def otherMembers(self, observer: int):
+        return [j for j in self.members(observer) if j != observer]
+
+    def membershipRecords(self, observer: int):
+        """getMembershipRecords (MembershipProtocolImpl.java:716-718)."""
+        row = self.view(observer)
+        return [MembershipRecord.decode(int(j), int(row[j])) for j in np.nonzero(row)[0]]
+
+    def alive(self, observer: int):
+        row = self.view(observer)
+        return [int(j) for j in np.nonzero((row & 3) == 1)[0] if j != observer]
+
+    def suspected(self, observer: int):
+        row = self.view(observer)
+        return [int(j) for j in np.nonzero((row != 0) & ((row & 3) == 2))[0]]

@@ -1,0 +1,121 @@
+"""Scenario scripts shared by the parity tests, the golden-fixture generator and smoke checks.
+
+Each scenario drives a cluster object (SwimCluster on the GPU or OracleCluster on the CPU)
+through the same calls. They restate the reference's test shapes on the discrete replay:
+FailureDetectorTest, MembershipProtocolTest, GossipProtocolTest and the BASELINE configs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from swimhip import ClusterConfig, FailureDetectorConfig, GossipConfig, MembershipConfig
+
+PARITY_KEYS = [
+    "period", "fd_probes", "fd_direct_ok", "fd_ping_req", "fd_suspect_events", "fd_alive_events",
+    "gossips_created", "gossip_first_receipts", "gossip_sends", "syncs_sent", "syncs_delivered",
+    "sync_acks_delivered", "records_accepted", "events_added", "events_removed", "suspicion_timeouts",
+    "refutations", "not_converged",
+]
+
+
+def crash_ids(n, k, seed):
+    rng = np.random.default_rng(seed)
+    return sorted(int(x) for x in rng.choice(n, size=k, replace=False))
+
+
+def test_membership_config():
+    """MembershipProtocolTest.java:920-928 (sync 500 ms, ping 200/100 ms, suspicion local)."""
+    return (
+        ClusterConfig.defaultLocalConfig()
+        .membership(lambda o: o.syncInterval(1000).syncTimeout(200))
+        .failureDetector(lambda o: o.pingInterval(200).pingTimeout(100))
+        .gossip(lambda o: o.gossipInterval(20))
+    )
+
+
+# name -> (config, n, seed, script) ; script(cluster) yields after each step so callers can compare
+def _c1(c):
+    c.step(10)
+    yield
+    c.crash(crash_ids(c.n, 1, 1))
+    for _ in range(30):
+        c.step(1)
+        yield
+
+
+def _lan_loss(c, n_crash, periods, loss, t0=5):
+    c.set_loss(loss)
+    c.step(t0)
+    yield
+    c.crash(crash_ids(c.n, n_crash, c.seed))
+    for _ in range(periods):
+        c.step(1)
+        yield
+
+
+def _partition_heal(c, t_part, length, after):
+    g = (np.arange(c.n) % 2).astype(np.uint8)
+    c.partition(g, t_part, t_part + length)
+    for _ in range(t_part + length + after):
+        c.step(1)
+        yield
+
+
+def _links(c):
+    # FailureDetectorTest.testTrustedDespiteBadNetwork (:116-146) + MembershipProtocolTest
+    # testMemberLostNetworkDueNoOutboundThenRecover (:140-193) shapes, scaled up
+    c.block_outbound(0, [1])
+    c.block_outbound(2, range(3, 12))
+    for _ in range(6):
+        c.step(1)
+        yield
+    c.unblock_outbound(2, range(3, 12))
+    for _ in range(8):
+        c.step(1)
+        yield
+
+
+SCENARIOS = {
+    "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
+    "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
+    "local100_loss20": (ClusterConfig.defaultLocalConfig(), 100, 3, lambda c: _lan_loss(c, 2, 30, 20.0)),
+    "local128_partition_heal": (
+        ClusterConfig.defaultLocalConfig().membership(lambda o: o.syncInterval(3000)),
+        128, 4, lambda c: _partition_heal(c, 3, 8, 12)),
+    "test64_long_partition_rejoin": (
+        test_membership_config().membership(lambda o: o.seedMembers(0, 1, 2, 3)),
+        64, 5, lambda c: _partition_heal(c, 2, 30, 25)),
+    "local48_links": (ClusterConfig.defaultLocalConfig(), 48, 6, _links),
+    "lan1024_loss5_crash10": (ClusterConfig.defaultLanConfig(), 1024, 7, lambda c: _lan_loss(c, 10, 30, 5.0)),
+}
+
+
+def run_pair(name, make_a, make_b, compare_every=1, full_tables=True, event_capacity=1 << 20):
+    """Drive two implementations through scenario `name`, asserting equality as it goes."""
+    cfg, n, seed, script = SCENARIOS[name]
+    a = make_a(cfg, n, seed, event_capacity=event_capacity)
+    b = make_b(cfg, n, seed, event_capacity=event_capacity)
+    ga, gb = script(a), script(b)
+    step = 0
+    for _ in ga:
+        next(gb)
+        step += 1
+        if step % compare_every:
+            continue
+        ea = [e.key() for e in a.events()]
+        eb = [e.key() for e in b.events()]
+        if ea != eb:
+            first = next((i for i, (x, y) in enumerate(zip(ea, eb)) if x != y), min(len(ea), len(eb)))
+            raise AssertionError(f"{name}: events differ at step {step}, index {first}: "
+                                 f"{ea[first:first + 3]} vs {eb[first:first + 3]} (len {len(ea)} vs {len(eb)})")
+        sa, sb = a.stats(), b.stats()
+        bad = {k: (sa[k], sb[k]) for k in PARITY_KEYS if sa[k] != sb[k]}
+        assert not bad, f"{name}: stats differ at step {step}: {bad}"
+        assert a.digest() == b.digest(), f"{name}: digests differ at step {step}"
+    if full_tables:
+        for i in range(n):
+            assert np.array_equal(a.view(i), b.view(i)), f"{name}: view row {i} differs"
+            assert np.array_equal(a.deadlines(i), b.deadlines(i)), f"{name}: deadline row {i} differs"
+        pa, pb = a.presence(), b.presence()
+        assert np.array_equal(pa[0], pb[0]) and np.array_equal(pa[1], pb[1])
+    return a, b

@@ -1,0 +1,52 @@
+"""The drop-in boundary: libswimhip.so loads here (no GPU needed) and exports exactly the entry
+points include/swimhip.h declares; the oracle mirrors every stateful entry point."""
+import ctypes
+import os
+
+from swimhip import _native as nat
+
+
+def test_header_declares_expected_surface():
+    syms = nat.header_symbols()
+    for s in ("swim_create", "swim_destroy", "swim_step", "swim_drain_events", "swim_read_view", "swim_crash",
+              "swim_set_loss", "swim_set_partition", "swim_stats_get", "swim_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    assert os.path.exists(nat.LIB_PATH), "build() must produce the in-tree libswimhip.so"
+    lib = ctypes.CDLL(nat.LIB_PATH)
+    missing = [s for s in nat.header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header():
+    bound = {name for name, _, _ in nat.api_table("swim_") + nat.SWIM_ONLY}
+    assert set(nat.header_symbols()) == bound
+
+
+def test_oracle_mirrors_stateful_api():
+    import oracle_py
+
+    lib = oracle_py.load_oracle()
+    for name, _, _ in nat.api_table("oracle_"):
+        assert hasattr(lib, name)
+
+
+def test_struct_sizes_match_c_layout():
+    assert ctypes.sizeof(nat.SwimEvent) == 24
+    assert ctypes.sizeof(nat.SwimStats) == 8 * len(nat.STAT_FIELDS)
+    assert ctypes.sizeof(nat.SwimConfig) == 80
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+
+    if torch.cuda.is_available():
+        return
+    lib = nat.load_swimhip()
+    from swimhip import ClusterConfig, to_swim_config
+
+    cfg = to_swim_config(ClusterConfig.defaultLocalConfig(), 8)
+    h = ctypes.c_void_p()
+    assert lib.swim_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.SWIM_EHIP

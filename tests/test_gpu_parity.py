@@ -1,0 +1,62 @@
+"""Parity proper: libswimhip.so (gfx950) vs the CPU oracle, bit-exact on every membership table,
+suspicion-deadline table, MembershipEvent sequence and protocol counter, period by period."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_py
+import scenarios
+from oracle_py import OracleCluster
+from swimhip import ClusterConfig, SwimCluster
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", list(scenarios.SCENARIOS))
+def test_scenario_parity(name):
+    scenarios.run_pair(name, SwimCluster, OracleCluster)
+
+
+def test_philox_device_matches_oracle():
+    from swimhip import native
+
+    lib = native.load_swimhip()
+    rng = np.random.default_rng(0)
+    abct = rng.integers(0, 2**32, size=(4096, 4), dtype=np.uint64).astype(np.uint32)
+    for kind in (1, 7, 19):
+        out = np.zeros(len(abct), dtype=np.uint32)
+        P = ctypes.POINTER(ctypes.c_uint32)
+        seed = 0x1234_5678_9ABC_DEF0
+        assert lib.swim_kat_philox(seed, kind, abct.ctypes.data_as(P), out.ctypes.data_as(P), len(abct)) == 0
+        ref = [oracle_py.philox(seed, kind, *map(int, r)) for r in abct[:256]]
+        assert out[:256].tolist() == ref
+
+
+def test_c2_shape_4096_digest_parity():
+    """BASELINE config 2 shape (4,096 dense, 5 % loss, fanout 3, 1 % crash), 12 periods."""
+    cfg = ClusterConfig.defaultLanConfig()
+    n = 4096
+    a, b = SwimCluster(cfg, n, seed=2024), OracleCluster(cfg, n, seed=2024)
+    crashed = scenarios.crash_ids(n, 41, 2024)
+    for c in (a, b):
+        c.set_loss(5.0)
+        c.step(2)
+        c.crash(crashed)
+    for _ in range(3):
+        for c in (a, b):
+            c.step(4)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+
+
+def test_crash_converges_and_gossip_capacity_reports_overflow():
+    """A too-small gossip ring must fail loudly (SWIM_EOVERFLOW), never silently diverge."""
+    from swimhip import SwimError
+
+    cfg = ClusterConfig.defaultLanConfig()
+    c = SwimCluster(cfg, 2048, seed=3, gossip_capacity=16)
+    c.crash(scenarios.crash_ids(2048, 200, 3))
+    with pytest.raises(SwimError):
+        c.step(4)
