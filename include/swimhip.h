@@ -175,6 +175,10 @@ int swim_kat_is_overrides(const uint32_t* r1, const uint32_t* r0, uint8_t* out, 
 /* Device Philox4x32-10 draws (counter = {a,b,c,tick}, key = seed ^ kind) for RNG parity. */
 int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint32_t* out, uint64_t n);
 
+/* Debug: the gossips a member holds, as (gossip hash, infection round) pairs. */
+int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
+                        uint32_t* n_out);
+
 /* Kernel timing for the bench: the last step's per-kernel-class device time (ms, HIP events
  * on the handle's stream). idx: 0 fd, 1 gossip_send, 2 gossip_apply, 3 suspicion, 4 sync_merge,
  * 5 sync_ack. Returns accumulated time since the last reset. */

@@ -871,6 +871,23 @@ int oracle_stats_get(oracle_handle* h, swim_stats* out) {
   return SWIM_OK;
 }
 
+int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
+                          uint32_t* n_out) {
+  if (!h || member >= h->N || !n_out) return SWIM_EINVAL;
+  uint32_t n = 0;
+  for (uint32_t gid = h->gbase; gid < h->registry.size(); ++gid) {
+    const int64_t inf = gossip_find(h, h->m[member], gid);
+    if (inf < 0) continue;
+    if (n < cap) {
+      out_hash[n] = h->registry[gid].hash;
+      out_inf[n] = (uint32_t)inf;
+    }
+    ++n;
+  }
+  *n_out = n;
+  return SWIM_OK;
+}
+
 int oracle_is_overrides(uint32_t r1, uint32_t r0) { return is_overrides(r1, r0) ? 1 : 0; }
 
 uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick) {

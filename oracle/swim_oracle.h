@@ -41,6 +41,9 @@ int oracle_digest(oracle_handle* h, uint64_t* view_digest, uint64_t* deadline_di
 int oracle_read_presence(oracle_handle* h, uint32_t* present, uint32_t* last_removed, uint32_t n);
 int oracle_stats_get(oracle_handle* h, swim_stats* out);
 
+int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
+                          uint32_t* n_out);
+
 /* Pure helpers (known-answer tests). */
 int oracle_is_overrides(uint32_t r1, uint32_t r0);
 uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick);

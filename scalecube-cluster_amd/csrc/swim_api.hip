@@ -236,9 +236,11 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   h->G = (uint32_t)std::max(1, c.ping_interval_ms / c.gossip_interval_ms);
   h->S = (uint32_t)std::max(1, c.sync_interval_ms / c.ping_interval_ms);
   h->TPP = h->G + 4;
-  h->GC = c.gossip_capacity ? c.gossip_capacity : std::min<uint32_t>(pow2ceil(std::max<uint64_t>(1024, 2ull * N)), 65536u);
+  h->GC = c.gossip_capacity ? c.gossip_capacity
+                            : std::min<uint32_t>(pow2ceil(std::max<uint64_t>(8192, 32ull * N)), 65536u);
   h->scap = c.sync_capacity ? c.sync_capacity : std::min<uint32_t>(2u * N, 8192u);
-  h->dcap = c.dirty_capacity ? c.dirty_capacity : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(65536, 64ull * N));
+  h->dcap = c.dirty_capacity ? c.dirty_capacity
+                            : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(1ull << 20, 64ull * N));
   h->ecap = c.event_capacity;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
@@ -579,6 +581,32 @@ int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t
   (void)hipFree(din);
   (void)hipFree(dout);
   return rc;
+}
+
+int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
+                        uint32_t* n_out) {
+  if (!h || member >= h->N || !n_out) return SWIM_EINVAL;
+  Ctl ctl;
+  HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  const uint32_t GC = h->GC;
+  std::vector<uint32_t> row(GC), cr(GC), hs(GC);
+  HIPC(h, hipMemcpy(row.data(), h->base.hold + (size_t)member * GC, (size_t)GC * 4, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(cr.data(), h->base.g_create, (size_t)GC * 4, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(hs.data(), h->base.g_hash, (size_t)GC * 4, hipMemcpyDeviceToHost));
+  uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;
+  if (hi - lo > GC) lo = hi - GC;
+  for (uint32_t id = lo; id < hi; ++id) {
+    const uint32_t s = id & (GC - 1), e = row[s];
+    if (e == 0 || e - 1 < cr[s]) continue;
+    if (n < cap) {
+      out_hash[n] = hs[s];
+      out_inf[n] = e - 1;
+    }
+    ++n;
+  }
+  *n_out = n;
+  return SWIM_OK;
 }
 
 int swim_kernel_time(swim_handle* h, uint32_t idx, double* ms, uint64_t* launches) {

@@ -45,6 +45,7 @@ enum Overflow : uint32_t {
   OV_SYNC = 4u,
   OV_DIRTY = 8u,
   OV_BUCKET = 16u,
+  OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
 };
 
 struct Ctl {

@@ -62,8 +62,8 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
     // selectPingMember (FailureDetectorImpl.java:340-349)
     uint32_t ep = P.fd_epoch[i], cur = P.fd_cursor[i];
     PermKey key = perm_key(P.seed, K_FD_PERM, i, ep);
-    uint32_t j = 0;
-    for (;;) {
+    uint32_t j = NONE;
+    for (uint32_t guard = 0; guard < 2u * N + 2u; ++guard) {
       if (cur >= N) {
         cur = 0;
         ++ep;
@@ -77,6 +77,10 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
     }
     P.fd_epoch[i] = ep;
     P.fd_cursor[i] = cur;
+    if (j == NONE) {  // member count says >0 but the row holds nobody: invariant broken
+      atomicOr(&P.ctl->overflow, OV_BUG);
+      j = (i + 1) % N;
+    }
     probes = 1;
     // outcome as (nA SUSPECT events, then nB events of status stB) — DESIGN.md §3.3
     uint32_t nA = 0, nB = 0, stB = SWIM_SUSPECT;
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
           if (!held_start) ++sends;
         }
         bool dl_known = false, dl_ok = false;
-        for (;;) {
+        for (uint32_t guard = 0; guard < 64u; ++guard) {
           const bool held_now = v != 0u && v - 1u >= create && r <= v - 1u + psweep;
           if (held_now) break;
           if (!dl_known) {

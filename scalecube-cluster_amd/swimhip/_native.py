@@ -131,6 +131,7 @@ SWIM_ONLY = [
     ("swim_last_error", ctypes.c_char_p, [_P]),
     ("swim_kat_is_overrides", _I, [_pU32, _pU32, _pU8, _U64]),
     ("swim_kat_philox", _I, [_U64, _U32, _pU32, _pU32, _U64]),
+    ("swim_debug_holdings", _I, [_P, _U32, _pU32, _pU32, _U32, _pU32]),
     ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),
     ("swim_kernel_time_reset", _I, [_P, _I]),
 ]

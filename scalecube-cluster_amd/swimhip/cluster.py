@@ -215,3 +215,14 @@ class SwimCluster:
     def suspected(self, observer: int):
         row = self.view(observer)
         return [int(j) for j in np.nonzero((row != 0) & ((row & 3) == 2))[0]]
+
+    def debug_holdings(self, member: int, cap: int = 1 << 20):
+        """(gossip hash, infection round) pairs the member's GossipProtocol holds (debug)."""
+        hs = np.zeros(cap, dtype=np.uint32)
+        inf = np.zeros(cap, dtype=np.uint32)
+        n = ctypes.c_uint32()
+        P = ctypes.POINTER(ctypes.c_uint32)
+        self._call("debug_holdings", self._h, int(member), hs.ctypes.data_as(P), inf.ctypes.data_as(P), cap,
+                   ctypes.byref(n))
+        k = min(n.value, cap)
+        return sorted(zip(hs[:k].tolist(), inf[:k].tolist()))
