@@ -1,0 +1,221 @@
+#!/usr/bin/env python
+"""bench.py — whole-node member-periods/s of the SWIM protocol-period step on MI355X.
+
+Metric (BASELINE.json): member-periods/sec at 65k/262k members; periods to DEAD convergence.
+A "step" is one protocol period for every simulated member: FD probe, G gossip
+rounds, suspicion timeouts, SYNC/SYNC_ACK. Inputs are synthetic (a converged cluster, a
+Philox-chosen crash set) and resident in HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3s]
+
+N > 1 runs under torch.distributed.run, one rank per GPU (RANK/LOCAL_RANK/WORLD_SIZE from the
+env); each rank steps its own independent cluster replica (the row-sharded RCCL
+path is not built yet), barrier + max-over-ranks timing, value = all ranks' member-periods / time.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# name -> (description, n, preset, loss %, crash fraction, gossip ring slots)
+WORKLOADS = {
+    "c3s": ("C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash "
+            "after warmup", 65536, "lan", 0.0, 0.001, 1 << 16),
+    "c3": ("C3: 65,536 members, dense, LAN defaults, 10% simultaneous crash after warmup", 65536, "lan", 0.0,
+           0.10, 1 << 16),
+    "c2": ("C2: 4,096 members, dense, LAN defaults, 5% uniform loss, 1% crash after warmup", 4096, "lan", 5.0,
+           0.01, 1 << 18),
+    "steady65k": ("65,536 members, dense, LAN defaults, fault-free steady state", 65536, "lan", 0.0, 0.0, 1 << 14),
+}
+
+
+def kernel_bytes(name, d, n):
+    """Algorithmic HBM bytes of one kernel class over the timed region.
+    d = stats deltas over the timed region."""
+    if name == "k_sync_merge":  # read SYNC payload row + read table row + write SYNC_ACK payload
+        return 12 * d["merge_cells"]
+    if name == "k_sync_ack":  # read SYNC_ACK payload row + read table row
+        return 8 * d["ack_cells"]
+    if name == "k_sync_snapshot":  # copy the sender's row into the SYNC payload
+        return 8 * d["merge_cells"]
+    if name == "k_gossip_select":  # own holding row
+        return 4 * d["gossip_scanned"] // 2
+    if name == "k_gossip_send":  # own holding row + receiver entries + receipt CAS/inbox
+        return 4 * d["gossip_scanned"] // 2 + 4 * d["gossip_probes"] + 12 * d["gossip_first_receipts"]
+    if name == "k_susp_sweep":  # stream a deadline column
+        return 4 * d["sweep_cells"]
+    if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
+        return 24 * d["fd_probes"]
+    return 0
+
+
+def make_cluster(workload, device, seed, event_capacity=0):
+    from swimhip import ClusterConfig, SwimCluster
+
+    _, n, preset, loss, _, gcap = WORKLOADS[workload]
+    cfg = {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
+    c = SwimCluster(cfg, n, seed=seed, gossip_capacity=gcap, device=device, event_capacity=event_capacity)
+    if loss:
+        c.set_loss(loss)
+    return c
+
+
+def crash_set(n, frac, seed):
+    k = int(round(n * frac))
+    if k == 0:
+        return []
+    rng = np.random.default_rng(seed)
+    return sorted(int(x) for x in rng.choice(n, size=k, replace=False))
+
+
+def cpu_baseline(workload, warmup, budget_s=15.0, seed=1):
+    """The oracle (oracle/, single-threaded C++) on the same workload: `warmup` untimed periods,
+    the crash, then periods timed one by one until ~budget_s of CPU work (bounded sample)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle_py import OracleCluster
+    from swimhip import ClusterConfig
+
+    _, n, preset, loss, frac, _ = WORKLOADS[workload]
+    cfg = {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
+    c = OracleCluster(cfg, n, seed=seed)
+    if loss:
+        c.set_loss(loss)
+    c.step(warmup)
+    c.crash(crash_set(n, frac, seed))
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and done < 64:
+        c.step(1)
+        done += 1
+    dt = time.perf_counter() - t0
+    c.close()
+    return {"value": n * done / dt, "unit": "member-periods/s", "cores": 1, "kind": "port",
+            "sample": f"oracle (single-threaded C++ restatement) on {n} members: {warmup} untimed periods, the "
+                      f"crash, then {done} timed periods ({dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3s", choices=sorted(WORKLOADS))
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--converge", type=int, default=120,
+                    help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    desc, n, preset, loss, frac, gcap = WORKLOADS[args.workload]
+    c = make_cluster(args.workload, local, args.seed)
+    c.step(args.warmup)
+    crashed = crash_set(n, frac, args.seed)
+    if crashed:
+        c.crash(crashed)
+    crash_period = args.warmup
+    s0 = c.stats()
+    c.kernel_timing(True)
+    barrier()
+    c.sync()
+    t0 = time.perf_counter()
+    c.step_async(args.steps)
+    c.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    s1 = c.stats()
+    ktimes = c.kernel_times()
+    c.kernel_timing(False)
+    d = {k: s1[k] - s0[k] for k in s1}
+
+    # dominant kernel + roofline over the timed region
+    dom = max((k for k in ktimes if k != "bookkeeping"), key=lambda k: ktimes[k][0])
+    ms, launches = ktimes[dom]
+    byts = kernel_bytes(dom, d, n)
+    avg_s = ms / 1e3 / max(1, launches)
+    per_launch = byts / max(1, launches)
+    achieved = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+
+    # periods to DEAD convergence (untimed): every alive observer removed every crashed member
+    periods_to_dead = None
+    if crashed and args.converge:
+        extra = 0
+        while extra < args.converge:
+            st = c.stats()
+            if st["not_converged"] == 0:
+                break
+            c.step(5)
+            extra += 5
+        pres, last = c.presence()
+        if c.stats()["not_converged"] == 0:
+            periods_to_dead = int(max(last[crashed])) - 1 - crash_period
+
+    value = world * n * args.steps / elapsed
+    out = {
+        "metric": "member-periods/sec (whole node)",
+        "value": value,
+        "unit": "member-periods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (converged start, Philox-chosen crash set, seeded)",
+        "config": {"workload": desc, "members": n, "members_per_gpu": n, "parallelism": f"replicas x{world}",
+                   "crashed": len(crashed), "loss_pct": loss, "gossip_ring_slots": gcap},
+        "periods_to_dead": periods_to_dead,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3, "launches": launches},
+        "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
+        "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
+                                   "merge_cells", "gossip_scanned", "gossip_probes", "events_removed")},
+    }
+    c.close()
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload, args.warmup, args.cpu_budget, args.seed)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,7 @@ typedef struct swim_config {
   uint32_t sync_capacity;   /* SYNC requests per period (0 = default)                     */
   uint32_t dirty_capacity;  /* gossip (observer, subject) inbox cells per round (0 = default) */
   uint32_t flags;           /* reserved, 0                                                */
+  int32_t device;           /* HIP device ordinal the handle lives on                     */
 } swim_config;
 
 typedef struct swim_stats {
@@ -127,6 +128,12 @@ typedef struct swim_stats {
   uint64_t overflow;          /* bit mask of overflowed buffers (0 = none)                */
   uint64_t live_gossip_slots; /* gossip slots currently in use                            */
   uint64_t not_converged;     /* (alive observer, crashed subject) cells still present    */
+  /* work counters for the bench's algorithmic-byte model; 0 in the oracle */
+  uint64_t gossip_scanned;    /* holding-row slots scanned by k_gossip_select + k_gossip_send */
+  uint64_t gossip_probes;     /* receiver holding entries read by k_gossip_send           */
+  uint64_t sweep_cells;       /* deadline cells streamed by k_susp_sweep                  */
+  uint64_t merge_cells;       /* table cells merged by k_sync_merge                       */
+  uint64_t ack_cells;         /* table cells merged by k_sync_ack                         */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -178,6 +185,10 @@ int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint
 /* Debug: the gossips a member holds, as (gossip hash, infection round) pairs. */
 int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
                         uint32_t* n_out);
+
+/* Debug: per-member protocol cursors, 6 arrays of n: FD epoch, FD cursor, gossip epoch,
+ * gossip cursor, gossip counter, member count (others). */
+int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n);
 
 /* Kernel timing for the bench: the last step's per-kernel-class device time (ms, HIP events
  * on the handle's stream). idx: 0 fd, 1 gossip_send, 2 gossip_apply, 3 suspicion, 4 sync_merge,

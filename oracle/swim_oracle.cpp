@@ -520,22 +520,29 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   const int32_t rm = h->cfg.gossip_repeat_mult;
   while (h->gbase < h->registry.size() && h->registry[h->gbase].holders == 0) h->gbase++;
   const uint32_t gend = (uint32_t)h->registry.size();
+  // GPI:144-146 "gossips.isEmpty()" is decided on the start-of-round state of every member:
+  // a gossip swept at the end of round r (r-1 <= inf + sweep < r) still counts, even if a
+  // delivery later in round r re-infects the member with it.
+  std::vector<uint8_t> nonempty(h->N, 0);
+  for (uint32_t s = 0; s < h->N; ++s) {
+    const Member& me = h->m[s];
+    if (!me.alive) continue;
+    const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);  // GPI:283-284
+    for (uint32_t gid = h->gbase; gid < gend && !nonempty[s]; ++gid) {
+      const int64_t inf = gossip_find(h, me, gid);
+      if (inf >= 0 && inf <= r && r - 1 <= inf + sweep) nonempty[s] = 1;
+    }
+  }
   std::vector<uint32_t> window;
   for (uint32_t s = 0; s < h->N; ++s) {
     Member& me = h->m[s];
-    if (!me.alive) continue;
+    if (!me.alive || !nonempty[s]) continue;  // GPI:144-146 (no peer selection either)
     const int32_t spread = periods_to_spread(rm, (int32_t)me.others + 1);  // GPI:243-244
-    const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);    // GPI:283-284
-    // gossips held at the start of round r: received before it and not swept at r-1.
     window.clear();
-    bool any = false;
     for (uint32_t gid = h->gbase; gid < gend; ++gid) {
       const int64_t inf = gossip_find(h, me, gid);
-      if (inf < 0 || inf > r || r - 1 > inf + sweep) continue;
-      any = true;
-      if (r <= inf + spread) window.push_back(gid);  // GPI:247 infectionPeriod + spread >= period
+      if (inf >= 0 && inf <= r && r <= inf + spread) window.push_back(gid);  // GPI:247
     }
-    if (!any) continue;  // GPI:144-146 (no peer selection either)
     std::vector<uint32_t> peers = select_gossip_members(h, s);  // GPI:150
     for (uint32_t p : peers) {
       // GossipState.infected (GPI:248) only prunes sends to members that already hold the
@@ -885,6 +892,20 @@ int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash,
     ++n;
   }
   *n_out = n;
+  return SWIM_OK;
+}
+
+int oracle_debug_member_state(oracle_handle* h, uint32_t* out6n, uint32_t n) {
+  if (!h || !out6n || n != h->N) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    const Member& me = h->m[i];
+    out6n[0 * (size_t)n + i] = me.fd_epoch;
+    out6n[1 * (size_t)n + i] = me.fd_cursor;
+    out6n[2 * (size_t)n + i] = me.g_epoch;
+    out6n[3 * (size_t)n + i] = me.g_cursor;
+    out6n[4 * (size_t)n + i] = me.gossip_seq;
+    out6n[5 * (size_t)n + i] = me.others;
+  }
   return SWIM_OK;
 }
 

@@ -44,6 +44,8 @@ int oracle_stats_get(oracle_handle* h, swim_stats* out);
 int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
                           uint32_t* n_out);
 
+int oracle_debug_member_state(oracle_handle* h, uint32_t* out6n, uint32_t n);
+
 /* Pure helpers (known-answer tests). */
 int oracle_is_overrides(uint32_t r1, uint32_t r0);
 uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick);

@@ -19,7 +19,7 @@ using namespace swim;
 
 namespace {
 
-constexpr int NCLASS = 8;  // timing classes, see swim_kernel_time
+constexpr int NCLASS = 9;  // timing classes, see swim_kernel_time
 
 uint32_t pow2ceil(uint64_t v) {
   uint64_t p = 1;
@@ -158,6 +158,7 @@ int step_one(swim_handle* h) {
     P.round = t * G + q;
     P.create_round = t * G + q + 1;
     timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(64), 0, s, P); });
+    timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
     timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_send, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
     timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, s, P); });
     timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
@@ -227,6 +228,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (c.gossip_capacity && (c.gossip_capacity & (c.gossip_capacity - 1))) return SWIM_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EHIP;
+  if (c.device < 0 || c.device >= ndev) return SWIM_EINVAL;
+  if (hipSetDevice(c.device) != hipSuccess) return SWIM_EHIP;
 
   swim_handle* h = new (std::nothrow) swim_handle();
   if (!h) return SWIM_ENOMEM;
@@ -236,11 +239,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   h->G = (uint32_t)std::max(1, c.ping_interval_ms / c.gossip_interval_ms);
   h->S = (uint32_t)std::max(1, c.sync_interval_ms / c.ping_interval_ms);
   h->TPP = h->G + 4;
+  // default gossip ring: ~4 GiB of holdings (N x GC x 4 B), between 8 Ki and 256 Ki slots
   h->GC = c.gossip_capacity ? c.gossip_capacity
-                            : std::min<uint32_t>(pow2ceil(std::max<uint64_t>(8192, 32ull * N)), 65536u);
+                            : std::max<uint32_t>(8192u, std::min<uint32_t>(262144u, pow2ceil((1ull << 30) / N + 1) / 2));
   h->scap = c.sync_capacity ? c.sync_capacity : std::min<uint32_t>(2u * N, 8192u);
   h->dcap = c.dirty_capacity ? c.dirty_capacity
-                            : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(1ull << 20, 64ull * N));
+                            : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(1ull << 22, 256ull * N));
   h->ecap = c.event_capacity;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
@@ -259,7 +263,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.mult = (uint32_t)c.suspicion_mult;
   P.n_seeds = c.n_seeds;
   P.time_left_pos = (c.ping_interval_ms - c.ping_timeout_ms) > 0 ? 1u : 0u;
-  P.sweepmax = 2u * (P.rm * bitlen(N) + 1u);
+  // a holder with infection round inf still counts the gossip as held at the start of round
+  // inf + sweep + 1 (sweepGossips runs after that round's sends, GossipProtocolImpl.java:150-153),
+  // and sweep <= 2 * (rm * bitlen(N) + 1); expiry = inf + sweepmax bounds every holder.
+  P.sweepmax = 2u * (P.rm * bitlen(N) + 1u) + 1u;
   P.ecap = h->ecap;
   P.scap = h->scap;
   P.dcap = h->dcap;
@@ -288,6 +295,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_cursor, N);
   ALLOC(P.gseq, N);
   ALLOC(P.sync_fd, N);
+  ALLOC(P.peers, (size_t)N * c.gossip_fanout);
+  ALLOC(P.npeers, N);
   ALLOC(P.g_subject, h->GC);
   ALLOC(P.g_record, h->GC);
   ALLOC(P.g_hash, h->GC);
@@ -536,6 +545,11 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->suspicion_timeouts = ctl.stats[ST_SUSP_TIMEOUTS];
   out->refutations = ctl.stats[ST_REFUTATIONS];
   out->overflow = ctl.overflow;
+  out->gossip_scanned = ctl.stats[ST_G_SCANNED];
+  out->gossip_probes = ctl.stats[ST_G_PROBES];
+  out->sweep_cells = ctl.stats[ST_SWEEP_CELLS];
+  out->merge_cells = ctl.stats[ST_MERGE_CELLS];
+  out->ack_cells = ctl.stats[ST_ACK_CELLS];
   out->live_gossip_slots = ctl.gcount - ctl.glo;
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
@@ -606,6 +620,16 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
     ++n;
   }
   *n_out = n;
+  return SWIM_OK;
+}
+
+int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n) {
+  if (!h || !out6n || n != h->N) return SWIM_EINVAL;
+  uint32_t* src[6] = {h->base.fd_epoch, h->base.fd_cursor, h->base.g_epoch, h->base.g_cursor, h->base.gseq,
+                      h->base.cnt};
+  for (int k = 0; k < 6; ++k)
+    HIPC(h, hipMemcpyAsync(out6n + (size_t)k * n, src[k], (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
 }
 

@@ -36,6 +36,11 @@ enum StatIdx : int {
   ST_REMOVED,
   ST_SUSP_TIMEOUTS,
   ST_REFUTATIONS,
+  ST_G_SCANNED,
+  ST_G_PROBES,
+  ST_SWEEP_CELLS,
+  ST_MERGE_CELLS,
+  ST_ACK_CELLS,
   ST_COUNT
 };
 
@@ -66,7 +71,7 @@ struct Ctl {
 struct KP {
   // sizes / config
   uint32_t N, GC, gmask, G, S, f, kreq, rm, mult, n_seeds, time_left_pos;
-  uint32_t sweepmax;
+  uint32_t sweepmax;  // max gossipPeriodsToSweep + 1: last round a holder may still count a gossip
   uint32_t ecap, scap, dcap;
   uint64_t seed;
   // clock
@@ -92,6 +97,8 @@ struct KP {
   uint32_t* g_cursor;
   uint32_t* gseq;
   uint32_t* sync_fd;
+  uint32_t* peers;   // [N][f] gossip peers chosen this round
+  uint32_t* npeers;  // [N]
   uint32_t* g_subject;
   uint32_t* g_record;
   uint32_t* g_hash;

@@ -3,7 +3,7 @@
 // Phase order per period, all on one HIP stream, no host round trips:
 //   k_fd             FailureDetectorImpl.doPing/doPingReq (FailureDetectorImpl.java:126-209)
 //                    + onFailureDetectorEvent (MembershipProtocolImpl.java:376-404)
-//   G x { k_gossip_prep, k_gossip_send, k_gossip_apply, k_finalize }
+//   G x { k_gossip_prep, k_gossip_select, k_gossip_send, k_gossip_apply, k_finalize }
 //                    GossipProtocolImpl.doSpreadGossip/onGossipReq/sweepGossips
 //                    (GossipProtocolImpl.java:139-304) + onMembershipGossip (MPI:407-414)
 //   k_due, k_susp_sweep, k_finalize
@@ -164,14 +164,12 @@ __global__ void k_gossip_prep(KP P) {
   c->dirty_count = 0u;
 }
 
-// One wave per sender m. doSpreadGossip (GossipProtocolImpl.java:139-157):
-//   held   = gossips present at the start of round r (received before r, not swept at r-1)
-//   window = held with r <= infectionPeriod + periodsToSpread          (:242-251)
-//   peers  = selectGossipMembers                                        (:253-274)
-//   send each window gossip to each peer; the receiver adopts it iff it does not hold it
-//   (onGossipReq :171-183), first receipt -> inbox atomicMax for the membership apply.
-//   sweepGossips (:281-304): the owner clears entries with r > infectionPeriod + sweep.
-__global__ void __launch_bounds__(256) k_gossip_send(KP P) {
+// One wave per member m, on the start-of-round state (before any delivery of round r):
+// doSpreadGossip's "gossips non-empty" test (GossipProtocolImpl.java:144-146), the peer
+// choice selectGossipMembers (:253-274) and the previous round's sweepGossips (:281-304;
+// entries with r > infectionPeriod + sweep are cleared so round-r receivers see them absent).
+// A gossip swept at the end of round r still counts as held at its start (r-1 <= inf+sweep).
+__global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
@@ -179,16 +177,13 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
-  uint32_t sends = 0, receipts = 0;
   const bool active = (m < N) && P.alive[m] && lo < hi;
-  uint32_t others = 0, spread = 0, sweep = 0;
+  uint32_t others = 0;
   bool any_l = false;
-  uint32_t* hrow = nullptr;
   if (active) {
     others = P.cnt[m];
-    spread = spread_rounds(P, others);
-    sweep = sweep_rounds(P, others);
-    hrow = P.hold + (size_t)m * P.GC;
+    const uint32_t sweep = sweep_rounds(P, others);
+    uint32_t* hrow = P.hold + (size_t)m * P.GC;
     for (uint32_t id = lo + lane; id < hi; id += 64u) {
       const uint32_t s = id & P.gmask;
       const uint32_t e = hrow[s];
@@ -196,7 +191,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
       const uint32_t inf = e - 1u;
       if (inf < P.g_create[s]) continue;  // stale entry of a recycled slot
       if (inf <= r && r <= inf + sweep + 1u) any_l = true;
-      if (r > inf + sweep) atomicCAS(&hrow[s], e, 0u);  // sweepGossips
+      if (r > inf + sweep) hrow[s] = 0u;  // sweepGossips (swept by the end of round r-1)
     }
   }
   const bool any = __any(any_l);
@@ -236,8 +231,7 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
           const uint32_t need = P.f - np;
           const uint32_t have = (uint32_t)__popcll(b);
           if (have >= need) {
-            // position of the need-th set bit
-            unsigned long long bb = b;
+            unsigned long long bb = b;  // position of the need-th set bit
             for (uint32_t t = 1; t < need; ++t) bb &= bb - 1ull;
             const uint32_t last = (uint32_t)__builtin_ctzll(bb);
             if (ok && lane <= last) s_peers[w][np + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = x;
@@ -263,6 +257,34 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < np) P.peers[(size_t)m * P.f + lane] = s_peers[w][lane];
+  }
+  if (m < N && lane == 0) P.npeers[m] = np;
+  add_stat(P, ST_G_SCANNED, (active && lane == 0) ? hi - lo : 0u);
+}
+
+// One wave per sender m: spreadGossipsTo (GossipProtocolImpl.java:215-251) for the peers chosen
+// by k_gossip_select. window = gossips with inf <= r <= inf + periodsToSpread; each goes to each
+// peer; the receiver adopts it iff it does not hold it (onGossipReq :171-183), and the first
+// receipt does an inbox atomicMax for the membership apply.
+__global__ void __launch_bounds__(256) k_gossip_send(KP P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t m = blockIdx.x * 4u + w;
+  const uint32_t N = P.N;
+  const uint32_t r = P.round;
+  const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  uint32_t sends = 0, receipts = 0, probes = 0;
+  const uint32_t np = m < N ? P.npeers[m] : 0u;
+  if (np > 0u) {
+    uint32_t peers[MAXF];
+    uint32_t psweep[MAXF];
+    for (uint32_t k = 0; k < np; ++k) {
+      peers[k] = P.peers[(size_t)m * P.f + k];
+      psweep[k] = P.alive[peers[k]] ? sweep_rounds(P, P.cnt[peers[k]]) : NONE;
+    }
+    const uint32_t spread = spread_rounds(P, P.cnt[m]);
+    const uint32_t* hrow = P.hold + (size_t)m * P.GC;
     for (uint32_t id = lo + lane; id < hi; id += 64u) {
       const uint32_t s = id & P.gmask;
       const uint32_t e = hrow[s];
@@ -272,19 +294,18 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
       if (inf < create || inf > r || r > inf + spread) continue;
       const uint32_t gh = P.g_hash[s];
       for (uint32_t k = 0; k < np; ++k) {
-        const uint32_t p = s_peers[w][k];
-        if (!P.alive[p]) continue;  // stopped transport: every message to it is lost
+        if (psweep[k] == NONE) continue;  // stopped transport: every message to it is lost
+        const uint32_t p = peers[k];
         uint32_t* hp = P.hold + (size_t)p * P.GC + s;
-        const uint32_t psweep = sweep_rounds(P, P.cnt[p]);
         uint32_t v = *hp;
+        ++probes;
         {
-          const bool valid = v != 0u && v - 1u >= create;
-          const bool held_start = valid && v - 1u <= r && r <= v - 1u + psweep;
+          const bool held_start = v != 0u && v - 1u >= create && v - 1u <= r && r <= v - 1u + psweep[k];
           if (!held_start) ++sends;
         }
         bool dl_known = false, dl_ok = false;
         for (uint32_t guard = 0; guard < 64u; ++guard) {
-          const bool held_now = v != 0u && v - 1u >= create && r <= v - 1u + psweep;
+          const bool held_now = v != 0u && v - 1u >= create && r <= v - 1u + psweep[k];
           if (held_now) break;
           if (!dl_known) {
             dl_ok = delivered(P, K_GOSSIP, m, p, gh, P.tick);
@@ -313,6 +334,8 @@ __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
   }
   add_stat(P, ST_GOSSIP_SENDS, sends);
   add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
+  add_stat(P, ST_G_PROBES, probes);
+  add_stat(P, ST_G_SCANNED, (np > 0u && lane == 0) ? hi - lo : 0u);
 }
 
 // Membership apply of a round's first receipts: onMembershipGossip (MPI:407-414) with the
@@ -395,6 +418,7 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     __syncthreads();
   }
   add_stat(P, ST_SUSP_TIMEOUTS, fired);
+  add_stat(P, ST_SWEEP_CELLS, threadIdx.x == 0 ? ((n + gridDim.x - 1u - blockIdx.x) / gridDim.x) * P.N : 0u);
   flush_tally(P, T);
 }
 
@@ -595,6 +619,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
               s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
+  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * P.N : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -634,6 +659,7 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
+  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * P.N : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }

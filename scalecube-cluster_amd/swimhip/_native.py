@@ -52,6 +52,7 @@ class SwimConfig(ctypes.Structure):
         ("sync_capacity", ctypes.c_uint32),
         ("dirty_capacity", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
     ]
 
 
@@ -89,6 +90,11 @@ STAT_FIELDS = [
     "overflow",
     "live_gossip_slots",
     "not_converged",
+    "gossip_scanned",
+    "gossip_probes",
+    "sweep_cells",
+    "merge_cells",
+    "ack_cells",
 ]
 
 
@@ -132,6 +138,7 @@ SWIM_ONLY = [
     ("swim_kat_is_overrides", _I, [_pU32, _pU32, _pU8, _U64]),
     ("swim_kat_philox", _I, [_U64, _U32, _pU32, _pU32, _U64]),
     ("swim_debug_holdings", _I, [_P, _U32, _pU32, _pU32, _U32, _pU32]),
+    ("swim_debug_member_state", _I, [_P, _pU32, _U32]),
     ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),
     ("swim_kernel_time_reset", _I, [_P, _I]),
 ]

@@ -74,8 +74,8 @@ class MembershipRecord:
 
 class SwimCluster:
     def __init__(self, config: ClusterConfig, n_members: int, seed: int = 0, *, event_capacity: int = 0,
-                 gossip_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, _lib=None,
-                 _prefix: str = "swim_"):
+                 gossip_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0,
+                 _lib=None, _prefix: str = "swim_"):
         self._lib = _lib if _lib is not None else nat.load_swimhip()
         self._p = _prefix
         self.config = config
@@ -83,7 +83,7 @@ class SwimCluster:
         self.seed = int(seed)
         self._cfg = to_swim_config(config, self.n, seed, gossip_capacity=gossip_capacity,
                                    event_capacity=event_capacity, sync_capacity=sync_capacity,
-                                   dirty_capacity=dirty_capacity)
+                                   dirty_capacity=dirty_capacity, device=device)
         h = ctypes.c_void_p()
         self._h = None
         self._call("create", ctypes.byref(self._cfg), ctypes.byref(h))
@@ -226,3 +226,32 @@ class SwimCluster:
                    ctypes.byref(n))
         k = min(n.value, cap)
         return sorted(zip(hs[:k].tolist(), inf[:k].tolist()))
+
+    def debug_member_state(self):
+        """Per-member protocol cursors (debug): dict of arrays."""
+        out = np.zeros(6 * self.n, dtype=np.uint32)
+        self._call("debug_member_state", self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), self.n)
+        names = ["fd_epoch", "fd_cursor", "g_epoch", "g_cursor", "gossip_seq", "others"]
+        return {k: out[i * self.n:(i + 1) * self.n] for i, k in enumerate(names)}
+
+    # -- bench helpers (HIP library only) ---------------------------------------------------
+    KERNEL_CLASSES = ["k_fd", "k_gossip_send", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
+                      "k_sync_snapshot", "bookkeeping", "k_gossip_select"]
+
+    def step_async(self, periods: int = 1):
+        self._call("step_async", self._h, int(periods))
+
+    def sync(self):
+        self._call("sync", self._h)
+
+    def kernel_timing(self, enable: bool):
+        self._call("kernel_time_reset", self._h, 1 if enable else 0)
+
+    def kernel_times(self) -> dict:
+        """{kernel class: (total device ms, launches)} since the last kernel_timing() reset."""
+        out = {}
+        for i, name in enumerate(self.KERNEL_CLASSES):
+            ms, n = ctypes.c_double(), ctypes.c_uint64()
+            self._call("kernel_time", self._h, i, ctypes.byref(ms), ctypes.byref(n))
+            out[name] = (ms.value, n.value)
+        return out

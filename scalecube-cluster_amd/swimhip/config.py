@@ -232,7 +232,7 @@ class ClusterConfig(_Cfg):
 
 
 def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_capacity: int = 0,
-                   event_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0):
+                   event_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0):
     """Marshal a ClusterConfig into the C struct of include/swimhip.h."""
     from ._native import SwimConfig
 
@@ -260,4 +260,5 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
     c.sync_capacity = sync_capacity
     c.dirty_capacity = dirty_capacity
     c.flags = 0
+    c.device = device
     return c

@@ -36,7 +36,7 @@ def test_oracle_mirrors_stateful_api():
 def test_struct_sizes_match_c_layout():
     assert ctypes.sizeof(nat.SwimEvent) == 24
     assert ctypes.sizeof(nat.SwimStats) == 8 * len(nat.STAT_FIELDS)
-    assert ctypes.sizeof(nat.SwimConfig) == 80
+    assert ctypes.sizeof(nat.SwimConfig) == 88
 
 
 def test_create_without_gpu_fails_cleanly():
