@@ -49,10 +49,10 @@ def kernel_bytes(name, d, n):
         return 8 * d["ack_cells"]
     if name == "k_sync_snapshot":  # copy the sender's row into the SYNC payload
         return 8 * d["merge_cells"]
-    if name == "k_gossip_select":  # own holding row
-        return 4 * d["gossip_scanned"] // 2
-    if name == "k_gossip_send":  # own holding row + receiver entries + receipt CAS/inbox
-        return 4 * d["gossip_scanned"] // 2 + 4 * d["gossip_probes"] + 12 * d["gossip_first_receipts"]
+    if name == "k_gossip_select":  # own hd row (2 B/slot) + hb read/write + wb write (1 bit/slot each)
+        return (2 * d["gossip_scanned"] + 3 * d["gossip_scanned"] // 8) // 2
+    if name == "k_gossip_send":  # own window bits + receiver bitmap words + receipt (bit, hd, inbox)
+        return d["gossip_scanned"] // 2 // 8 + 4 * d["gossip_probes"] + 14 * d["gossip_first_receipts"]
     if name == "k_susp_sweep":  # stream a deadline column
         return 4 * d["sweep_cells"]
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)

@@ -116,7 +116,7 @@ typedef struct swim_stats {
   uint64_t fd_alive_events;   /* FailureDetectorEvent(ALIVE) published                    */
   uint64_t gossips_created;   /* GossipProtocol.spread() calls                            */
   uint64_t gossip_first_receipts; /* onGossipReq with a new gossip id                     */
-  uint64_t gossip_sends;      /* GossipRequest messages whose receiver lacked the gossip  */
+  uint64_t gossip_sends;      /* GossipRequest messages to alive peers (window x peers)    */
   uint64_t syncs_sent;        /* SYNC messages (periodic + FD-triggered)                  */
   uint64_t syncs_delivered;
   uint64_t sync_acks_delivered;
@@ -130,7 +130,7 @@ typedef struct swim_stats {
   uint64_t not_converged;     /* (alive observer, crashed subject) cells still present    */
   /* work counters for the bench's algorithmic-byte model; 0 in the oracle */
   uint64_t gossip_scanned;    /* holding-row slots scanned by k_gossip_select + k_gossip_send */
-  uint64_t gossip_probes;     /* receiver holding entries read by k_gossip_send           */
+  uint64_t gossip_probes;     /* receiver holds-now bitmap words read by k_gossip_send     */
   uint64_t sweep_cells;       /* deadline cells streamed by k_susp_sweep                  */
   uint64_t merge_cells;       /* table cells merged by k_sync_merge                       */
   uint64_t ack_cells;         /* table cells merged by k_sync_ack                         */

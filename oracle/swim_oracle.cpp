@@ -553,8 +553,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       for (uint32_t gid : window) {
         const int64_t pinf = gossip_find(h, pm, gid);
         const bool has = pinf >= 0;
-        // counted once per message whose receiver lacked the gossip at the start of the round
-        if (!(has && pinf <= r && r <= pinf + psweep)) h->st.gossip_sends++;
+        h->st.gossip_sends++;  // one GossipRequest message per gossip and peer (GPI:225-239)
         if (has && r <= pinf + psweep) continue;  // receiver holds it (maybe since this round)
         const Gossip& g = h->registry[gid];
         if (!delivered(h, K_GOSSIP, s, p, g.hash, tick)) continue;

@@ -31,7 +31,7 @@ uint32_t pow2ceil(uint64_t v) {
 
 struct swim_handle {
   swim_config cfg{};
-  uint32_t N = 0, G = 1, S = 1, TPP = 5, GC = 0, scap = 0, dcap = 0, ecap = 0;
+  uint32_t N = 0, G = 1, S = 1, TPP = 5, GC = 0, scap = 0, ecap = 0;
   uint64_t period = 0;
   uint64_t part_t0 = 0, part_t1 = 0;
   hipStream_t stream = nullptr;
@@ -160,7 +160,7 @@ int step_one(swim_handle* h) {
     timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(64), 0, s, P); });
     timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
     timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_send, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
-    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(1024), dim3(256), 0, s, P); });
+    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
     timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
   }
 
@@ -225,7 +225,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
       c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
     return SWIM_EINVAL;
-  if (c.gossip_capacity && (c.gossip_capacity & (c.gossip_capacity - 1))) return SWIM_EINVAL;
+  // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
+  if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
+    return SWIM_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EHIP;
   if (c.device < 0 || c.device >= ndev) return SWIM_EINVAL;
@@ -243,8 +245,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   h->GC = c.gossip_capacity ? c.gossip_capacity
                             : std::max<uint32_t>(8192u, std::min<uint32_t>(262144u, pow2ceil((1ull << 30) / N + 1) / 2));
   h->scap = c.sync_capacity ? c.sync_capacity : std::min<uint32_t>(2u * N, 8192u);
-  h->dcap = c.dirty_capacity ? c.dirty_capacity
-                            : (uint32_t)std::min<uint64_t>((uint64_t)N * N, std::max<uint64_t>(1ull << 22, 256ull * N));
   h->ecap = c.event_capacity;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
@@ -269,7 +269,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.sweepmax = 2u * (P.rm * bitlen(N) + 1u) + 1u;
   P.ecap = h->ecap;
   P.scap = h->scap;
-  P.dcap = h->dcap;
   P.seed = c.seed;
   P.loss_mode = 0;
   P.loss_thr = 0;
@@ -283,7 +282,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.view, NN);
   ALLOC(P.dl, NN);
   ALLOC(P.inbox, NN);
-  ALLOC(P.hold, (size_t)N * h->GC);
+  ALLOC(P.hb, (size_t)N * (h->GC / 32));
+  ALLOC(P.wb, (size_t)N * (h->GC / 32));
+  ALLOC(P.hd, (size_t)N * h->GC);
   ALLOC(P.colmin, N);
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
@@ -301,8 +302,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_record, h->GC);
   ALLOC(P.g_hash, h->GC);
   ALLOC(P.g_create, h->GC);
-  ALLOC(P.g_expiry, h->GC);
-  ALLOC(P.dirty, h->dcap);
+  ALLOC(P.g_last, h->GC);
+  ALLOC(P.hs, (size_t)N * (h->GC / 32));
   ALLOC(P.due, N);
   ALLOC(P.events, std::max<uint32_t>(1, h->ecap));
   ALLOC(P.pres, N);
@@ -317,6 +318,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, h->scap);
   ALLOC(P.ctl, 1);
+  ALLOC(P.stat_shards, (size_t)STAT_SHARDS * STAT_STRIDE);
   ALLOC(h->d_digest, 2);
 #undef ALLOC
   P.group = group;
@@ -332,7 +334,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, SWIM_PACK(0, SWIM_ALIVE));
   (void)hipMemsetAsync(P.dl, 0, NN * 4, s);
   (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
-  (void)hipMemsetAsync(P.hold, 0, (size_t)N * h->GC * 4, s);
+  (void)hipMemsetAsync(P.hb, 0, (size_t)N * (h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.wb, 0, (size_t)N * (h->GC / 32) * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmin, (size_t)N, NONE);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, N - 1);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, N - 1);
@@ -345,10 +348,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.g_epoch, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.g_cursor, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.gseq, 0, (size_t)N * 4, s);
-  (void)hipMemsetAsync(P.g_expiry, 0, (size_t)h->GC * 4, s);
+  (void)hipMemsetAsync(P.g_last, 0, (size_t)h->GC * 4, s);
+  (void)hipMemsetAsync(P.hs, 0, (size_t)N * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
+  (void)hipMemsetAsync(P.stat_shards, 0, (size_t)STAT_SHARDS * STAT_STRIDE * 8, s);
   hipError_t e = hipStreamSynchronize(s);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) {
@@ -525,31 +530,36 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   std::vector<uint8_t> alive(h->N);
   HIPC(h, hipMemcpyAsync(pres.data(), h->base.pres, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, h->N, hipMemcpyDeviceToHost, h->stream));
+  std::vector<unsigned long long> shards((size_t)STAT_SHARDS * STAT_STRIDE);
+  HIPC(h, hipMemcpyAsync(shards.data(), h->base.stat_shards, shards.size() * 8, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  unsigned long long stats[ST_COUNT] = {0};
+  for (uint32_t sh = 0; sh < STAT_SHARDS; ++sh)
+    for (int i = 0; i < ST_COUNT; ++i) stats[i] += shards[(size_t)sh * STAT_STRIDE + i];
   std::memset(out, 0, sizeof *out);
   out->period = h->period;
-  out->fd_probes = ctl.stats[ST_FD_PROBES];
-  out->fd_direct_ok = ctl.stats[ST_FD_DIRECT_OK];
-  out->fd_ping_req = ctl.stats[ST_FD_PING_REQ];
-  out->fd_suspect_events = ctl.stats[ST_FD_SUSPECT_EV];
-  out->fd_alive_events = ctl.stats[ST_FD_ALIVE_EV];
-  out->gossips_created = ctl.stats[ST_GOSSIPS_CREATED];
-  out->gossip_first_receipts = ctl.stats[ST_GOSSIP_RECEIPTS];
-  out->gossip_sends = ctl.stats[ST_GOSSIP_SENDS];
-  out->syncs_sent = ctl.stats[ST_SYNCS_SENT];
-  out->syncs_delivered = ctl.stats[ST_SYNCS_DELIVERED];
-  out->sync_acks_delivered = ctl.stats[ST_ACKS_DELIVERED];
-  out->records_accepted = ctl.stats[ST_ACCEPTED];
-  out->events_added = ctl.stats[ST_ADDED];
-  out->events_removed = ctl.stats[ST_REMOVED];
-  out->suspicion_timeouts = ctl.stats[ST_SUSP_TIMEOUTS];
-  out->refutations = ctl.stats[ST_REFUTATIONS];
+  out->fd_probes = stats[ST_FD_PROBES];
+  out->fd_direct_ok = stats[ST_FD_DIRECT_OK];
+  out->fd_ping_req = stats[ST_FD_PING_REQ];
+  out->fd_suspect_events = stats[ST_FD_SUSPECT_EV];
+  out->fd_alive_events = stats[ST_FD_ALIVE_EV];
+  out->gossips_created = stats[ST_GOSSIPS_CREATED];
+  out->gossip_first_receipts = stats[ST_GOSSIP_RECEIPTS];
+  out->gossip_sends = stats[ST_GOSSIP_SENDS];
+  out->syncs_sent = stats[ST_SYNCS_SENT];
+  out->syncs_delivered = stats[ST_SYNCS_DELIVERED];
+  out->sync_acks_delivered = stats[ST_ACKS_DELIVERED];
+  out->records_accepted = stats[ST_ACCEPTED];
+  out->events_added = stats[ST_ADDED];
+  out->events_removed = stats[ST_REMOVED];
+  out->suspicion_timeouts = stats[ST_SUSP_TIMEOUTS];
+  out->refutations = stats[ST_REFUTATIONS];
   out->overflow = ctl.overflow;
-  out->gossip_scanned = ctl.stats[ST_G_SCANNED];
-  out->gossip_probes = ctl.stats[ST_G_PROBES];
-  out->sweep_cells = ctl.stats[ST_SWEEP_CELLS];
-  out->merge_cells = ctl.stats[ST_MERGE_CELLS];
-  out->ack_cells = ctl.stats[ST_ACK_CELLS];
+  out->gossip_scanned = stats[ST_G_SCANNED];
+  out->gossip_probes = stats[ST_G_PROBES];
+  out->sweep_cells = stats[ST_SWEEP_CELLS];
+  out->merge_cells = stats[ST_MERGE_CELLS];
+  out->ack_cells = stats[ST_ACK_CELLS];
   out->live_gossip_slots = ctl.gcount - ctl.glo;
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
@@ -604,18 +614,20 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
   HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   const uint32_t GC = h->GC;
-  std::vector<uint32_t> row(GC), cr(GC), hs(GC);
-  HIPC(h, hipMemcpy(row.data(), h->base.hold + (size_t)member * GC, (size_t)GC * 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> bits(GC / 32), cr(GC), hs(GC);
+  std::vector<uint16_t> d(GC);
+  HIPC(h, hipMemcpy(bits.data(), h->base.hb + (size_t)member * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(d.data(), h->base.hd + (size_t)member * GC, (size_t)GC * 2, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(cr.data(), h->base.g_create, (size_t)GC * 4, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(hs.data(), h->base.g_hash, (size_t)GC * 4, hipMemcpyDeviceToHost));
   uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;
   if (hi - lo > GC) lo = hi - GC;
   for (uint32_t id = lo; id < hi; ++id) {
-    const uint32_t s = id & (GC - 1), e = row[s];
-    if (e == 0 || e - 1 < cr[s]) continue;
+    const uint32_t s = id & (GC - 1);
+    if (!((bits[s >> 5] >> (s & 31)) & 1u)) continue;
     if (n < cap) {
       out_hash[n] = hs[s];
-      out_inf[n] = e - 1;
+      out_inf[n] = cr[s] + (uint16_t)(d[s] - (uint16_t)cr[s]);  // hd = infection round mod 2^16
     }
     ++n;
   }

@@ -5,7 +5,10 @@
 //   dl     u32[N][N]  SUBJECT-major suspicion deadlines (+1, 0 = none) so the timeout sweep
 //                     streams one subject column over all observers (MembershipProtocolImpl.java:101)
 //   inbox  u32[N][N]  observer-major lattice max of the records a gossip round delivered
-//   hold   u32[N][GC] member-major gossip holdings: infectionPeriod + 1, 0 = not held
+//   hb     u32[N][GC/32] member-major "holds gossip slot s now" bitmap
+//   hd     u16[N][GC]    infectionPeriod - creation round of each held gossip
+//   wb     u32[N][GC/32] the member's start-of-round send window (written by k_gossip_select)
+//                     (GossipProtocolImpl.java:49, GossipState.java:14)
 //                     (GossipProtocolImpl.java:49, GossipState.java:14)
 // plus per-member vectors (cursors, counts, liveness) and per-slot gossip metadata.
 #pragma once
@@ -51,15 +54,20 @@ enum Overflow : uint32_t {
   OV_DIRTY = 8u,
   OV_BUCKET = 16u,
   OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
+  OV_HOLD_RANGE = 64u,  // a gossip was received more than 65534 rounds after its creation
 };
 
+constexpr uint32_t STAT_SHARDS = 64;  // power of two
+constexpr uint32_t STAT_STRIDE = 32;  // u64 per shard (256 B), >= ST_COUNT
+static_assert(ST_COUNT <= (int)STAT_STRIDE, "stat shard too small");
+
 struct Ctl {
-  unsigned long long stats[ST_COUNT];
+  unsigned long long rsv_stats[ST_COUNT];
   uint32_t gcount;      // gossips ever created (ids); slot = id & (GC-1)
   uint32_t glo;         // oldest possibly-live gossip id
   uint32_t scan_lo;     // [scan_lo, scan_hi) ids scanned by the send kernel this round
   uint32_t scan_hi;
-  uint32_t dirty_count; // (observer, subject) inbox cells touched this round
+  uint32_t rsv0;
   uint32_t event_count;
   uint32_t stage_count; // staged SYNC requests this period
   uint32_t due_count;   // subject columns due for the suspicion sweep
@@ -72,7 +80,7 @@ struct KP {
   // sizes / config
   uint32_t N, GC, gmask, G, S, f, kreq, rm, mult, n_seeds, time_left_pos;
   uint32_t sweepmax;  // max gossipPeriodsToSweep + 1: last round a holder may still count a gossip
-  uint32_t ecap, scap, dcap;
+  uint32_t ecap, scap;
   uint64_t seed;
   // clock
   uint32_t period, round, phase, tick, create_round;
@@ -87,7 +95,10 @@ struct KP {
   uint32_t* dl;
   uint32_t* colmin;
   uint32_t* inbox;
-  uint32_t* hold;
+  uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
+  uint16_t* hd;  // [N][GC] infection round mod 2^16, valid where the hb bit is set (exact: a
+                 // held entry is at most sweep+1 rounds old, far below 2^16)
+  uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select
   uint32_t* cnt;
   int32_t* cnt_delta;
   uint8_t* alive;
@@ -103,8 +114,8 @@ struct KP {
   uint32_t* g_record;
   uint32_t* g_hash;
   uint32_t* g_create;
-  uint32_t* g_expiry;
-  unsigned long long* dirty;
+  uint32_t* g_last;   // latest infection round of any holder (plain idempotent stores)
+  uint32_t* hs;       // [N][GC/32] holds bitmap at the start of the round's deliveries
   uint32_t* due;
   swim_event* events;
   uint32_t* pres;
@@ -120,9 +131,20 @@ struct KP {
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
   Ctl* ctl;
+  unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// partition cut and directed link blocks only (no liveness, no loss draw)
+__device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t dst) {
+  if (P.part_active && P.group[src] != P.group[dst]) return false;
+  if (P.link) {
+    const uint64_t bit = (uint64_t)src * P.N + dst;
+    if (P.link[bit >> 3] & (1u << (bit & 7))) return false;
+  }
+  return true;
+}
 
 __device__ __forceinline__ bool delivered(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
                                           uint32_t tick) {
@@ -173,13 +195,17 @@ __device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32
                                             uint32_t seq) {
   const uint32_t id = atomicAdd(&P.ctl->gcount, 1u);
   const uint32_t s = id & P.gmask;
-  if (id >= P.GC && P.g_expiry[s] >= P.create_round) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  // the live id range must stay below GC - 64 slots so 64-slot chunks never alias across the
+  // ring wrap, and the slot's previous gossip must be dead everywhere
+  if (id - P.ctl->glo >= P.GC - 64u || (id >= P.GC && P.g_last[s] + P.sweepmax >= P.create_round))
+    atomicOr(&P.ctl->overflow, OV_GOSSIP);
   P.g_subject[s] = subject;
   P.g_record[s] = record;
   P.g_hash[s] = gossip_hash(origin, seq);
   P.g_create[s] = P.create_round;
-  P.g_expiry[s] = P.create_round + P.sweepmax;
-  P.hold[(size_t)origin * P.GC + s] = P.create_round + 1u;
+  P.g_last[s] = P.create_round;
+  P.hd[(size_t)origin * P.GC + s] = (uint16_t)P.create_round;  // origin's infectionPeriod
+  atomicOr(&P.hb[(size_t)origin * (P.GC >> 5) + (s >> 5)], 1u << (s & 31u));
 }
 
 // MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip.
@@ -249,9 +275,27 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+// exclusive prefix sum over the 64 lanes; *total = sum over the wave (all lanes must call)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {
   v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&P.ctl->stats[idx], (unsigned long long)v);
+  // 64 counter shards on separate 256-B lines: one same-address atomic per wave would
+  // serialize a 65,536-wave launch at the L2 (the host sums the shards)
+  if ((threadIdx.x & 63) == 0 && v) {
+    const uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (STAT_SHARDS - 1u);
+    atomicAdd(&P.stat_shards[shard * STAT_STRIDE + idx], (unsigned long long)v);
+  }
 }
 
 __device__ __forceinline__ void flush_tally(const KP& P, const Tally& T) {

@@ -157,18 +157,29 @@ __global__ void k_gossip_prep(KP P) {
   Ctl* c = P.ctl;
   const uint32_t hi = c->gcount;
   uint32_t lo = c->glo;
-  while (lo < hi && (hi - lo > P.GC || P.g_expiry[lo & P.gmask] < P.round)) ++lo;
+  // a gossip is dead once every holder has swept it: the last holder got it at g_last
+  while (lo < hi && (hi - lo > P.GC || P.g_last[lo & P.gmask] + P.sweepmax < P.round)) ++lo;
   c->glo = lo;
   c->scan_lo = lo;
   c->scan_hi = hi;
-  c->dirty_count = 0u;
 }
 
 // One wave per member m, on the start-of-round state (before any delivery of round r):
 // doSpreadGossip's "gossips non-empty" test (GossipProtocolImpl.java:144-146), the peer
-// choice selectGossipMembers (:253-274) and the previous round's sweepGossips (:281-304;
-// entries with r > infectionPeriod + sweep are cleared so round-r receivers see them absent).
-// A gossip swept at the end of round r still counts as held at its start (r-1 <= inf+sweep).
+// choice selectGossipMembers (:253-274), the send window (:242-251) written to wb, and the
+// sweep sweepGossips (:281-304) of entries with r > infectionPeriod + sweep, cleared before
+// round-r deliveries so receivers see them absent. A gossip swept in round r still counts as
+// held at its start (r-1 <= inf + sweep). Lane = one 32-slot bitmap word: a wave covers 2,048
+// slots per step; the 32 infection offsets (64 B) and creation rounds (128 B) of a word are
+// vector loads, so every lane has its loads in flight at once.
+__device__ __forceinline__ uint32_t range_mask(uint32_t id0, uint32_t lo, uint32_t hi) {
+  // bits b of the word whose id id0 + b lies in [lo, hi)
+  uint32_t m = 0xFFFFFFFFu;
+  if (lo > id0) m = lo - id0 >= 32u ? 0u : m << (lo - id0);
+  if (hi < id0 + 32u) m &= hi <= id0 ? 0u : (0xFFFFFFFFu >> (32u - (hi - id0)));
+  return m;
+}
+
 __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
@@ -178,20 +189,41 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const bool active = (m < N) && P.alive[m] && lo < hi;
+  const uint32_t W32 = P.GC >> 5;
   uint32_t others = 0;
   bool any_l = false;
   if (active) {
     others = P.cnt[m];
     const uint32_t sweep = sweep_rounds(P, others);
-    uint32_t* hrow = P.hold + (size_t)m * P.GC;
-    for (uint32_t id = lo + lane; id < hi; id += 64u) {
-      const uint32_t s = id & P.gmask;
-      const uint32_t e = hrow[s];
-      if (e == 0u) continue;
-      const uint32_t inf = e - 1u;
-      if (inf < P.g_create[s]) continue;  // stale entry of a recycled slot
-      if (inf <= r && r <= inf + sweep + 1u) any_l = true;
-      if (r > inf + sweep) hrow[s] = 0u;  // sweepGossips (swept by the end of round r-1)
+    const uint32_t spread = spread_rounds(P, others);
+    uint32_t* hbr = P.hb + (size_t)m * W32;
+    uint32_t* wbr = P.wb + (size_t)m * W32;
+    const uint16_t* hdr = P.hd + (size_t)m * P.GC;
+    const uint32_t w_end = ((hi + 63u) & ~63u) >> 5;
+    for (uint32_t wi = ((lo & ~63u) >> 5) + lane; wi < w_end; wi += 64u) {
+      const uint32_t ws = wi & (W32 - 1u);
+      const uint32_t word = hbr[ws];
+      const uint32_t held = word & range_mask(wi << 5, lo, hi);
+      uint32_t clear = 0, win = 0;
+      if (held) {
+        any_l = true;
+        // age = r - infectionPeriod, exact mod 2^16 (every held entry received before round r)
+        uint4 dv[4];
+        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[k] = dp[k];
+        const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dv);
+#pragma unroll
+        for (uint32_t b = 0; b < 32u; ++b) {
+          const uint32_t age = (r - (d32[b >> 1] >> ((b & 1u) * 16u))) & 0xFFFFu;
+          const uint32_t hbit = (held >> b) & 1u;
+          clear |= (hbit & (age > sweep ? 1u : 0u)) << b;  // sweepGossips
+          win |= (hbit & (age <= spread ? 1u : 0u)) << b;
+        }
+        if (clear) hbr[ws] = word & ~clear;
+      }
+      wbr[ws] = win;
+      P.hs[(size_t)m * W32 + ws] = word & ~clear;  // holds at the start of this round's deliveries
     }
   }
   const bool any = __any(any_l);
@@ -264,104 +296,167 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
 }
 
 // One wave per sender m: spreadGossipsTo (GossipProtocolImpl.java:215-251) for the peers chosen
-// by k_gossip_select. window = gossips with inf <= r <= inf + periodsToSpread; each goes to each
-// peer; the receiver adopts it iff it does not hold it (onGossipReq :171-183), and the first
-// receipt does an inbox atomicMax for the membership apply.
+// by k_gossip_select over its start-of-round window wb. Each window gossip goes to each alive
+// peer (one GossipRequest per gossip, :225-239); the receiver adopts it iff its holds-now bit
+// is clear (onGossipReq :171-183). Lane = one 32-slot word: the probe of a peer is one bitmap
+// word, and all of that word's deliveries to the peer are ONE fire-and-forget atomicOr. Every
+// copy delivered in a round has the same effect, so no winner is needed; k_gossip_apply finds
+// the round's first receipts as hb & ~hs.
 __global__ void __launch_bounds__(256) k_gossip_send(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t w = threadIdx.x >> 6;
-  const uint32_t m = blockIdx.x * 4u + w;
-  const uint32_t N = P.N;
-  const uint32_t r = P.round;
+  const uint32_t m = blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
-  uint32_t sends = 0, receipts = 0, probes = 0;
-  const uint32_t np = m < N ? P.npeers[m] : 0u;
+  const uint32_t W32 = P.GC >> 5;
+  uint32_t sends = 0, probes = 0;
+  const uint32_t np = m < P.N ? P.npeers[m] : 0u;
   if (np > 0u) {
-    uint32_t peers[MAXF];
-    uint32_t psweep[MAXF];
-    for (uint32_t k = 0; k < np; ++k) {
-      peers[k] = P.peers[(size_t)m * P.f + k];
-      psweep[k] = P.alive[peers[k]] ? sweep_rounds(P, P.cnt[peers[k]]) : NONE;
-    }
-    const uint32_t spread = spread_rounds(P, P.cnt[m]);
-    const uint32_t* hrow = P.hold + (size_t)m * P.GC;
-    for (uint32_t id = lo + lane; id < hi; id += 64u) {
-      const uint32_t s = id & P.gmask;
-      const uint32_t e = hrow[s];
-      if (e == 0u) continue;
-      const uint32_t inf = e - 1u;
-      const uint32_t create = P.g_create[s];
-      if (inf < create || inf > r || r > inf + spread) continue;
-      const uint32_t gh = P.g_hash[s];
-      for (uint32_t k = 0; k < np; ++k) {
-        if (psweep[k] == NONE) continue;  // stopped transport: every message to it is lost
-        const uint32_t p = peers[k];
-        uint32_t* hp = P.hold + (size_t)p * P.GC + s;
-        uint32_t v = *hp;
+    // the words k_gossip_select rewrote this round: [lo & ~63, hi rounded up to 64)
+    const uint32_t* wbr = P.wb + (size_t)m * W32;
+    const uint32_t w_beg = (lo & ~63u) >> 5, w_end = ((hi + 63u) & ~63u) >> 5;
+    for (uint32_t k = 0; k < np; ++k) {  // peers are wave-uniform
+      const uint32_t p = __builtin_amdgcn_readfirstlane(P.peers[(size_t)m * P.f + k]);
+      if (!P.alive[p]) continue;  // a stopped transport loses every message
+      const bool reach = link_open(P, m, p) && P.loss_mode != 2u;
+      uint32_t* hbp = P.hb + (size_t)p * W32;
+      for (uint32_t wi = w_beg + lane; wi < w_end; wi += 64u) {
+        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t win = wbr[ws];
+        if (!win) continue;
+        const uint32_t hw = hbp[ws];
         ++probes;
-        {
-          const bool held_start = v != 0u && v - 1u >= create && v - 1u <= r && r <= v - 1u + psweep[k];
-          if (!held_start) ++sends;
-        }
-        bool dl_known = false, dl_ok = false;
-        for (uint32_t guard = 0; guard < 64u; ++guard) {
-          const bool held_now = v != 0u && v - 1u >= create && r <= v - 1u + psweep[k];
-          if (held_now) break;
-          if (!dl_known) {
-            dl_ok = delivered(P, K_GOSSIP, m, p, gh, P.tick);
-            dl_known = true;
+        sends += (uint32_t)__popc(win);
+        uint32_t mask = reach ? (win & ~hw) : 0u;  // receiver lacks it (at load time)
+        if (mask && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+          uint32_t need = mask;
+          mask = 0u;
+          while (need) {
+            const uint32_t b = (uint32_t)__builtin_ctz(need);
+            need &= need - 1u;
+            if (draw1(P.seed, K_GOSSIP, m, p, P.g_hash[ws * 32u + b], P.tick) >= P.loss_thr) mask |= 1u << b;
           }
-          if (!dl_ok) break;
-          const uint32_t old = atomicCAS(hp, v, r + 2u);
-          if (old == v) {
-            ++receipts;
-            const uint32_t subj = P.g_subject[s];
-            const uint32_t prev = atomicMax(&P.inbox[(size_t)p * N + subj], P.g_record[s]);
-            if (prev == 0u) {
-              const uint32_t d = atomicAdd(&P.ctl->dirty_count, 1u);
-              if (d < P.dcap)
-                P.dirty[d] = ((unsigned long long)p << 32) | subj;
-              else
-                atomicOr(&P.ctl->overflow, OV_DIRTY);
-            }
-            atomicMax(&P.g_expiry[s], r + 1u + P.sweepmax);
-            break;
-          }
-          v = old;
         }
+        if (mask) atomicOr(&hbp[ws], mask);
       }
     }
   }
   add_stat(P, ST_GOSSIP_SENDS, sends);
-  add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
   add_stat(P, ST_G_PROBES, probes);
   add_stat(P, ST_G_SCANNED, (np > 0u && lane == 0) ? hi - lo : 0u);
 }
 
-// Membership apply of a round's first receipts: onMembershipGossip (MPI:407-414) with the
-// lattice max of the records that reached the cell this round.
+constexpr uint32_t HCAP = 512;  // per-wave LDS hash slots (power of two)
+
+// Hands the set bits of the lanes' receipt words to the whole wave, two words per step: lanes
+// 0-31 take bit (lane) of one word, lanes 32-63 bit (lane-32) of the next. fn(slot) runs once per
+// set bit. All lanes must call it (wave-uniform control flow).
+template <typename F>
+__device__ __forceinline__ void wave_for_bits(uint32_t ws, uint32_t bits, F&& fn) {
+  const uint32_t lane = threadIdx.x & 63u;
+  unsigned long long bal = __ballot(bits != 0u);
+  while (bal) {
+    const uint32_t la = (uint32_t)__builtin_ctzll(bal);
+    bal &= bal - 1ull;
+    uint32_t lb = 64u;
+    if (bal) {
+      lb = (uint32_t)__builtin_ctzll(bal);
+      bal &= bal - 1ull;
+    }
+    const uint32_t src = lane < 32u ? la : lb;
+    const uint32_t my_ws = __shfl(ws, (int)(src & 63u), 64);
+    const uint32_t my_bits = __shfl(bits, (int)(src & 63u), 64);
+    const uint32_t b = lane & 31u;
+    if (src < 64u && ((my_bits >> b) & 1u)) fn(my_ws * 32u + b);
+  }
+}
+
+// Membership apply of a round's first receipts: onGossipReq's new-gossip branch
+// (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
+// the records that reached a cell this round. One wave per receiver p: the
+// first receipts are exactly hb & ~hs. They get infectionPeriod r+1; their records are
+// max-reduced per subject in a per-wave LDS hash table (the global inbox is the fallback when a
+// receiver gets more than HCAP/2 new gossips in one round), then applied once per subject.
 __global__ void __launch_bounds__(256) k_gossip_apply(KP P) {
+  __shared__ uint32_t s_key[4][HCAP];
+  __shared__ uint32_t s_val[4][HCAP];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t p = blockIdx.x * 4u + w;
+  const uint32_t r = P.round;
+  const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t W32 = P.GC >> 5;
   Tally T;
-  uint32_t created = 0;
-  uint32_t n = P.ctl->dirty_count;
-  if (n > P.dcap) n = P.dcap;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t n_pad = (n + 63u) & ~63u;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_pad; k += stride) {
-    if (k < n) {
-      const unsigned long long d = P.dirty[k];
-      const uint32_t p = (uint32_t)(d >> 32), subj = (uint32_t)d;
-      uint32_t* ip = P.inbox + (size_t)p * P.N + subj;
-      const uint32_t r1 = *ip;
-      *ip = 0u;
-      const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, P.cnt[p], T);
+  uint32_t created = 0, receipts = 0;
+  const bool act = p < P.N && P.alive[p] && lo < hi;
+  const uint32_t* hbr = P.hb + (size_t)p * W32;
+  const uint32_t* hsr = P.hs + (size_t)p * W32;
+  const uint32_t w_beg = (lo & ~63u) >> 5, w_end = ((hi + 63u) & ~63u) >> 5;
+  // receipts = hb & ~hs; ids >= hi are gossips this kernel itself creates (refutations)
+  auto new_bits = [&](uint32_t wi) -> uint32_t {
+    const uint32_t ws = wi & (W32 - 1u);
+    return wi < w_end ? (hbr[ws] & ~hsr[ws] & range_mask(wi << 5, lo, hi)) : 0u;
+  };
+  if (act)
+    for (uint32_t wi = w_beg + lane; wi < w_end; wi += 64u) receipts += (uint32_t)__popc(new_bits(wi));
+  const uint32_t total = wave_sum(receipts);
+  if (act && total) {
+    const bool lds = total <= HCAP / 2u;
+    uint32_t* hk = s_key[w];
+    uint32_t* hv = s_val[w];
+    if (lds) {
+      for (uint32_t t = lane; t < HCAP; t += 64u) {
+        hk[t] = NONE;
+        hv[t] = 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    // infection round, gossip liveness, and the lattice max per subject
+    for (uint32_t wb0 = w_beg; wb0 < w_end; wb0 += 64u) {
+      const uint32_t wi = wb0 + lane;
+      wave_for_bits(wi & (W32 - 1u), new_bits(wi), [&](uint32_t s) {
+        P.hd[(size_t)p * P.GC + s] = (uint16_t)(r + 1u);
+        if (P.g_last[s] != r + 1u) P.g_last[s] = r + 1u;
+        const uint32_t subj = P.g_subject[s], rec = P.g_record[s];
+        if (lds) {
+          uint32_t h = (subj * 0x9E3779B1u) >> (32u - 9u);  // HCAP = 2^9
+          for (;;) {  // linear probing; at most HCAP/2 keys, so a slot is always found
+            const uint32_t prev = atomicCAS(&hk[h], NONE, subj);
+            if (prev == NONE || prev == subj) break;
+            h = (h + 1u) & (HCAP - 1u);
+          }
+          atomicMax(&hv[h], rec);
+        } else {
+          atomicMax(&P.inbox[(size_t)p * P.N + subj], rec);
+        }
+      });
+    }
+    const uint32_t snap = P.cnt[p];
+    auto apply = [&](uint32_t subj, uint32_t r1) {
+      const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, snap, T);
       if (rec) {  // only onSelfMemberDetected spreads here (reason MEMBERSHIP_GOSSIP)
         emit_gossip(P, p, subj, rec, P.gseq[p]++);
         ++created;
       }
+    };
+    if (lds) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (uint32_t t = lane; t < HCAP; t += 64u)  // one updateMembership per subject
+        if (hk[t] != NONE) apply(hk[t], hv[t]);
+    } else {
+      __threadfence();
+      for (uint32_t wb0 = w_beg; wb0 < w_end; wb0 += 64u) {
+        const uint32_t wi = wb0 + lane;
+        wave_for_bits(wi & (W32 - 1u), new_bits(wi), [&](uint32_t s) {
+          const uint32_t subj = P.g_subject[s];
+          const uint32_t r1 = atomicExch(&P.inbox[(size_t)p * P.N + subj], 0u);
+          if (r1) apply(subj, r1);  // several new gossips about one subject: applied once
+        });
+      }
     }
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
+  add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
   flush_tally(P, T);
 }
 
@@ -560,21 +655,45 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
                                           uint32_t* lds4) {
   const uint32_t N = P.N;
   uint32_t* row = P.view + (size_t)obs * N;
-  for (uint32_t c0 = 0; c0 < N; c0 += 256u) {
-    const uint32_t c = c0 + threadIdx.x;
-    uint32_t rec = 0;
+  // 4 cells per thread (16-B loads) when rows are 16-B aligned, else 1; cells that the
+  // incoming record does not override (the common case) never enter updateMembership.
+  const uint32_t per = (N & 3u) == 0u ? 4u : 1u;
+  for (uint32_t c0 = 0; c0 < N; c0 += 256u * per) {
+    const uint32_t c = c0 + per * threadIdx.x;
+    uint32_t recs[4], cells[4], nrec = 0;
     if (c < N) {
-      const uint32_t r1 = src[c];
-      if (r1 != 0u) rec = apply_record(P, obs, c, r1, SWIM_R_SYNC, attempt, snap, T);
-      if (ack_out) ack_out[c] = row[c];
-    }
-    if (__syncthreads_or(rec != 0u)) {
-      uint32_t total;
-      const uint32_t off = block_excl_scan256(rec != 0u ? 1u : 0u, &total, lds4);
-      if (rec) {
-        emit_gossip(P, obs, c, rec, seq + off);
-        ++created;
+      uint32_t sv[4], vv[4];
+      if (per == 4u) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(src + c);
+        const uint4 v4 = *reinterpret_cast<const uint4*>(row + c);
+        sv[0] = s4.x, sv[1] = s4.y, sv[2] = s4.z, sv[3] = s4.w;
+        vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+      } else {
+        sv[0] = src[c];
+        vv[0] = row[c];
       }
+      for (uint32_t k = 0; k < per; ++k) {
+        if (sv[k] == 0u || !is_overrides(sv[k], vv[k])) continue;
+        const uint32_t rec = apply_record(P, obs, c + k, sv[k], SWIM_R_SYNC, attempt, snap, T);
+        vv[k] = row[c + k];
+        if (rec) {
+          recs[nrec] = rec;
+          cells[nrec] = c + k;
+          ++nrec;
+        }
+      }
+      if (ack_out) {
+        if (per == 4u)
+          *reinterpret_cast<uint4*>(ack_out + c) = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+        else
+          ack_out[c] = vv[0];
+      }
+    }
+    if (__syncthreads_or(nrec != 0u)) {  // gossip sequence numbers in cell order
+      uint32_t total;
+      const uint32_t off = block_excl_scan256(nrec, &total, lds4);
+      for (uint32_t k = 0; k < nrec; ++k) emit_gossip(P, obs, cells[k], recs[k], seq + off + k);
+      created += nrec;
       seq += total;
     }
   }

@@ -56,7 +56,10 @@ def test_crash_converges_and_gossip_capacity_reports_overflow():
     from swimhip import SwimError
 
     cfg = ClusterConfig.defaultLanConfig()
-    c = SwimCluster(cfg, 2048, seed=3, gossip_capacity=16)
-    c.crash(scenarios.crash_ids(2048, 200, 3))
     with pytest.raises(SwimError):
-        c.step(4)
+        SwimCluster(cfg, 2048, seed=3, gossip_capacity=16)  # below the 1024-slot minimum
+    c = SwimCluster(cfg, 2048, seed=3, gossip_capacity=1024)
+    c.crash(scenarios.crash_ids(2048, 400, 3))
+    with pytest.raises(SwimError) as ei:
+        c.step(12)
+    assert ei.value.code == -75  # SWIM_EOVERFLOW
