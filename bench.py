@@ -28,15 +28,22 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
-# name -> (description, n, preset, loss %, crash fraction, gossip ring slots)
+# name -> workload spec. The default ("c3") is BASELINE.json configs[2], the 65,536-member config
+# the metric is quoted on that fits one GPU: 10 % simultaneous crash plus a 2-way partition
+# (member-id parity) from t0 to t0+40 periods (< the 85-period suspicion timeout, so it heals by
+# refutation and SYNC), LAN defaults, no loss. t0 = the end of the warmup.
 WORKLOADS = {
-    "c3s": ("C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash "
-            "after warmup", 65536, "lan", 0.0, 0.001, 1 << 16),
-    "c3": ("C3: 65,536 members, dense, LAN defaults, 10% simultaneous crash after warmup", 65536, "lan", 0.0,
-           0.10, 1 << 16),
-    "c2": ("C2: 4,096 members, dense, LAN defaults, 5% uniform loss, 1% crash after warmup", 4096, "lan", 5.0,
-           0.01, 1 << 18),
-    "steady65k": ("65,536 members, dense, LAN defaults, fault-free steady state", 65536, "lan", 0.0, 0.0, 1 << 14),
+    "c3": dict(desc="C3: 65,536 members, dense N x N views, LAN defaults, 10% simultaneous crash + 2-way "
+                    "partition (id parity) for 40 periods healed via SYNC",
+               n=65536, preset="lan", loss=0.0, crash=0.10, part=40, gcap=1 << 18),
+    "c3s": dict(desc="C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash",
+                n=65536, preset="lan", loss=0.0, crash=0.001, part=0, gcap=1 << 16),
+    "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",
+                    n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17),
+    "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
+               n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 16),
+    "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
+                      n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }
 
 
@@ -53,6 +60,8 @@ def kernel_bytes(name, d, n):
         return (2 * d["gossip_scanned"] + 3 * d["gossip_scanned"] // 8) // 2
     if name == "k_gossip_send":  # own window bits + receiver bitmap words + receipt (bit, hd, inbox)
         return d["gossip_scanned"] // 2 // 8 + 4 * d["gossip_probes"] + 14 * d["gossip_first_receipts"]
+    if name == "k_gossip_apply":  # hb + hs words over the live range + per receipt (hd, g_last, subject, record)
+        return d["gossip_scanned"] // 2 // 4 + 14 * d["gossip_first_receipts"]
     if name == "k_susp_sweep":  # stream a deadline column
         return 4 * d["sweep_cells"]
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
@@ -60,15 +69,37 @@ def kernel_bytes(name, d, n):
     return 0
 
 
-def make_cluster(workload, device, seed, event_capacity=0):
-    from swimhip import ClusterConfig, SwimCluster
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
-    _, n, preset, loss, _, gcap = WORKLOADS[workload]
-    cfg = {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
-    c = SwimCluster(cfg, n, seed=seed, gossip_capacity=gcap, device=device, event_capacity=event_capacity)
-    if loss:
-        c.set_loss(loss)
+
+def preset_config(preset):
+    from swimhip import ClusterConfig
+
+    return {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
+
+
+def make_cluster(workload, device, seed, event_capacity=0):
+    from swimhip import SwimCluster
+
+    w = WORKLOADS[workload]
+    c = SwimCluster(preset_config(w["preset"]), w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
+                    event_capacity=event_capacity)
+    if w["loss"]:
+        c.set_loss(w["loss"])
     return c
+
+
+def inject_faults(c, workload, t0, seed, n=None):
+    """The workload's fault schedule at period t0: crash set, then the partition window."""
+    w = WORKLOADS[workload]
+    n = n or w["n"]
+    crashed = crash_set(n, w["crash"], seed)
+    if crashed:
+        c.crash(crashed)
+    if w["part"]:
+        c.partition((np.arange(n) % 2).astype(np.uint8), t0, t0 + w["part"])
+    return crashed
 
 
 def crash_set(n, frac, seed):
@@ -79,20 +110,26 @@ def crash_set(n, frac, seed):
     return sorted(int(x) for x in rng.choice(n, size=k, replace=False))
 
 
+# The oracle keeps one direct-mapped gossip table per member that grows for every member at once,
+# so the full-size C3 gossip storm (~1e5 live gossips x 65,536 members) does not fit host RAM; its
+# CPU sample runs the same schedule at this many members.
+CPU_SAMPLE_N = 8192
+
+
 def cpu_baseline(workload, warmup, budget_s=15.0, seed=1):
-    """The oracle (oracle/, single-threaded C++) on the same workload: `warmup` untimed periods,
-    the crash, then periods timed one by one until ~budget_s of CPU work (bounded sample)."""
+    """The oracle (oracle/, single-threaded C++) on the same schedule: `warmup` untimed periods, the
+    faults, then periods timed one by one until ~budget_s of CPU work (a bounded sample of the
+    timed region's first periods), at min(N, CPU_SAMPLE_N) members."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle_py import OracleCluster
-    from swimhip import ClusterConfig
 
-    _, n, preset, loss, frac, _ = WORKLOADS[workload]
-    cfg = {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
-    c = OracleCluster(cfg, n, seed=seed)
-    if loss:
-        c.set_loss(loss)
+    w = WORKLOADS[workload]
+    n = min(w["n"], CPU_SAMPLE_N)
+    c = OracleCluster(preset_config(w["preset"]), n, seed=seed)
+    if w["loss"]:
+        c.set_loss(w["loss"])
     c.step(warmup)
-    c.crash(crash_set(n, frac, seed))
+    inject_faults(c, workload, warmup, seed, n=n)
     done, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s and done < 64:
         c.step(1)
@@ -100,16 +137,16 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1):
     dt = time.perf_counter() - t0
     c.close()
     return {"value": n * done / dt, "unit": "member-periods/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (single-threaded C++ restatement) on {n} members: {warmup} untimed periods, the "
-                      f"crash, then {done} timed periods ({dt:.1f} s)"}
+            "sample": f"oracle (single-threaded C++ restatement), same schedule at {n} of {w['n']} members: "
+                      f"{warmup} untimed periods, the faults, then the first {done} timed periods ({dt:.1f} s)"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3s", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--converge", type=int, default=120,
                     help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
@@ -133,20 +170,29 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    desc, n, preset, loss, frac, gcap = WORKLOADS[args.workload]
+    w = WORKLOADS[args.workload]
+    n = w["n"]
     c = make_cluster(args.workload, local, args.seed)
+    log(f"created {args.workload}: N={n}")
     c.step(args.warmup)
-    crashed = crash_set(n, frac, args.seed)
-    if crashed:
-        c.crash(crashed)
+    log(f"warmup {args.warmup} periods done")
+    crashed = inject_faults(c, args.workload, args.warmup, args.seed)
     crash_period = args.warmup
     s0 = c.stats()
     c.kernel_timing(True)
     barrier()
     c.sync()
     t0 = time.perf_counter()
-    c.step_async(args.steps)
-    c.sync()
+    done, last_print = 0, t0
+    while done < args.steps:  # chunks of 5 periods: a host sync per chunk, progress on stderr
+        k = min(5, args.steps - done)
+        c.step_async(k)
+        c.sync()
+        done += k
+        now = time.perf_counter()
+        if now - last_print > 20.0:
+            log(f"timed: {done}/{args.steps} periods, {now - t0:.1f} s")
+            last_print = now
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -179,6 +225,7 @@ def main():
                 break
             c.step(5)
             extra += 5
+            log(f"converge: +{extra} periods, not_converged={st['not_converged']}")
         pres, last = c.presence()
         if c.stats()["not_converged"] == 0:
             periods_to_dead = int(max(last[crashed])) - 1 - crash_period
@@ -197,8 +244,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (converged start, Philox-chosen crash set, seeded)",
-        "config": {"workload": desc, "members": n, "members_per_gpu": n, "parallelism": f"replicas x{world}",
-                   "crashed": len(crashed), "loss_pct": loss, "gossip_ring_slots": gcap},
+        "config": {"workload": w["desc"], "members": n, "members_per_gpu": n, "parallelism": f"replicas x{world}",
+                   "crashed": len(crashed), "loss_pct": w["loss"], "partition_periods": w["part"],
+                   "gossip_ring_slots": w["gcap"]},
         "periods_to_dead": periods_to_dead,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

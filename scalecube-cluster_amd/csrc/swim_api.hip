@@ -244,7 +244,19 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // default gossip ring: ~4 GiB of holdings (N x GC x 4 B), between 8 Ki and 256 Ki slots
   h->GC = c.gossip_capacity ? c.gossip_capacity
                             : std::max<uint32_t>(8192u, std::min<uint32_t>(262144u, pow2ceil((1ull << 30) / N + 1) / 2));
-  h->scap = c.sync_capacity ? c.sync_capacity : std::min<uint32_t>(2u * N, 8192u);
+  // SYNC staging rows: at most one periodic doSync per member every S periods (staggered) plus
+  // one FD-triggered SYNC per member per period (MPI:385-397), so N + ceil(N/S) never
+  // overflows; the default takes that bound unless the two payload slabs (8 B per cell) would
+  // exceed ~30 % of the device's free memory.
+  if (c.sync_capacity) {
+    h->scap = c.sync_capacity;
+  } else {
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const uint64_t bound = (uint64_t)N + (N + h->S - 1) / h->S;
+    const uint64_t fit = (uint64_t)(free_b * 0.30) / (8ull * N);
+    h->scap = (uint32_t)std::max<uint64_t>(64, std::min(bound, fit));
+  }
   h->ecap = c.event_capacity;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;

@@ -1,0 +1,259 @@
+"""Behavioural restatements of the reference's FD / membership tests on the discrete replay.
+
+Each function takes a cluster factory `make(config, n, seed)` (OracleCluster on the CPU,
+SwimCluster on the GPU) and asserts what the reference test asserts, with its wall-clock waits
+converted to protocol periods (period = pingInterval). Member a, b, c, d = ids
+0, 1, 2, 3. The reference tests wire every member with all addresses as seeds
+(MembershipProtocolTest.java:920-928), so the configs here use seedMembers(0..n-1).
+"""
+from __future__ import annotations
+
+from swimhip import ClusterConfig, FailureDetectorConfig
+from swimhip import cluster_math
+
+# MembershipProtocolTest.java:44-45
+TEST_SYNC_INTERVAL = 500
+PING_INTERVAL = 200
+
+
+def membership_test_config(n):
+    """MembershipProtocolTest.testConfig (:920-928): LAN defaults, sync 500 ms / timeout 100 ms,
+    ping 200 / 100 ms, metadataTimeout 100 ms, every member a seed."""
+    return (
+        ClusterConfig()
+        .membership(lambda o: o.seedMembers(list(range(n))).syncInterval(TEST_SYNC_INTERVAL).syncTimeout(100))
+        .failureDetector(lambda o: o.pingInterval(PING_INTERVAL).pingTimeout(100))
+        .metadataTimeout(100)
+    )
+
+
+def fd_test_config(n):
+    """FailureDetectorTest.createFd (:400-407): local preset, timeout 100 / interval 200, pingReq 2."""
+    return ClusterConfig.defaultLocalConfig().failureDetector(
+        lambda o: FailureDetectorConfig.defaultLocalConfig().pingTimeout(100).pingInterval(200).pingReqMembers(2)
+    ).membership(lambda o: o.seedMembers(list(range(n))))
+
+
+def seconds(s):
+    """awaitSeconds(s) (BaseTest.java:33-39) in periods of PING_INTERVAL."""
+    return int(s * 1000 // PING_INTERVAL)
+
+
+def await_suspicion(cluster_size):
+    """BaseTest.awaitSuspicion (:41-47): suspicionTimeout(5, size, 200 ms) + 2 s, in periods."""
+    ms = cluster_math.suspicionTimeout(5, cluster_size, PING_INTERVAL)
+    return seconds(ms // 1000 + 2)
+
+
+# -- assertion helpers (MembershipProtocolTest.java:1007-1078) ------------------------------
+def assert_trusted(c, obs, *expected):
+    """ALIVE records = expected + the local member (assertTrusted :1014-1032)."""
+    got = sorted(r.member for r in c.membershipRecords(obs) if r.status == "ALIVE")
+    assert got == sorted(set(expected) | {obs}), f"member {obs} trusts {got}, expected {sorted(expected)} + self"
+
+
+def assert_suspected(c, obs, *expected):
+    got = sorted(r.member for r in c.membershipRecords(obs) if r.status == "SUSPECT")
+    assert got == sorted(expected), f"member {obs} suspects {got}, expected {sorted(expected)}"
+
+
+def block_outbound(c, src, dsts):
+    c.block_outbound(src, [d for d in dsts if d != src])
+
+
+def unblock_all_outbound(c, src):
+    c.unblock_outbound(src, [d for d in range(c.n) if d != src])
+
+
+A, B, C, D = 0, 1, 2, 3
+
+
+# -- FailureDetectorTest ------------------------------------------------------------------
+def fd_trusted(make):
+    """testTrusted (:50-77): clean network, every member keeps the others ALIVE."""
+    c = make(fd_test_config(3), 3, 11)
+    c.step(6)
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def fd_suspected(make):
+    """testSuspected (:79-114): all outbound blocked, every member suspects the others."""
+    c = make(fd_test_config(3), 3, 12)
+    for m in (A, B, C):
+        block_outbound(c, m, (A, B, C))
+    c.step(4)
+    for m in (A, B, C):
+        assert_trusted(c, m)
+        assert_suspected(c, m, *[x for x in (A, B, C) if x != m])
+
+
+def fd_trusted_despite_bad_network(make):
+    """testTrustedDespiteBadNetwork (:116-146): A -> B blocked; ping-req through C keeps B ALIVE."""
+    c = make(fd_test_config(3), 3, 13)
+    block_outbound(c, A, (B,))
+    for _ in range(10):
+        c.step(1)
+        for m in (A, B, C):
+            assert_suspected(c, m)
+
+
+# -- MembershipProtocolTest ---------------------------------------------------------------
+def mp_initial_phase_ok(make):
+    """testInitialPhaseOk (:68-91)."""
+    c = make(membership_test_config(3), 3, 21)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_partition_no_outbound_then_recover(make):
+    """testNetworkPartitionDueNoOutboundThenRecover (:93-137): everyone isolated until removed,
+    then unblocked: SYNC to the seeds brings everyone back."""
+    c = make(membership_test_config(3), 3, 22)
+    c.step(seconds(3))
+    for m in (A, B, C):
+        block_outbound(c, m, (A, B, C))
+    c.step(await_suspicion(3))
+    for m in (A, B, C):
+        assert_trusted(c, m)  # assertSelfTrusted
+        assert_suspected(c, m)
+    removed = {(e.observer, e.member) for e in c.events() if e.isRemoved()}
+    assert removed == {(o, s) for o in (A, B, C) for s in (A, B, C) if o != s}
+    for m in (A, B, C):
+        unblock_all_outbound(c, m)
+    c.step(seconds(TEST_SYNC_INTERVAL * 2 / 1000))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_member_lost_network_then_recover(make):
+    """testMemberLostNetworkDueNoOutboundThenRecover (:139-193)."""
+    c = make(membership_test_config(3), 3, 23)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+    block_outbound(c, B, (A, C))
+    block_outbound(c, A, (B,))
+    block_outbound(c, C, (B,))
+    c.step(seconds(1))
+    assert_trusted(c, A, C)
+    assert_suspected(c, A, B)
+    assert_trusted(c, B)
+    assert_suspected(c, B, A, C)
+    assert_trusted(c, C, A)
+    assert_suspected(c, C, B)
+    for m in (A, B, C):
+        unblock_all_outbound(c, m)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_partition_twice_then_recover(make):
+    """testNetworkPartitionTwiceDueNoOutboundThenRecover (:195-263)."""
+    c = make(membership_test_config(3), 3, 24)
+    c.step(seconds(1))
+    block_outbound(c, B, (A, C))
+    block_outbound(c, A, (B,))
+    block_outbound(c, C, (B,))
+    c.step(seconds(1))
+    assert_trusted(c, A, C)
+    assert_suspected(c, A, B)
+    assert_trusted(c, B)
+    assert_suspected(c, B, A, C)
+    block_outbound(c, A, (C,))
+    block_outbound(c, C, (A,))
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m)
+        assert_suspected(c, m, *[x for x in (A, B, C) if x != m])
+    for m in (A, B, C):
+        unblock_all_outbound(c, m)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_network_lost_on_all_nodes_then_recover(make):
+    """testNetworkLostOnAllNodesDueNoOutboundThenRecover (:265-318)."""
+    c = make(membership_test_config(3), 3, 25)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        block_outbound(c, m, (A, B, C))
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m)
+        assert_suspected(c, m, *[x for x in (A, B, C) if x != m])
+    for m in (A, B, C):
+        unblock_all_outbound(c, m)
+    c.step(seconds(1))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_long_partition_then_removed(make):
+    """testLongNetworkPartitionDueNoOutboundThenRemoved (:320-371): {a,b} | {c,d} until the
+    suspicion timeout removes the other side."""
+    c = make(membership_test_config(4), 4, 26)
+    c.step(seconds(1))
+    for m in (A, B, C, D):
+        assert_trusted(c, m, *[x for x in (A, B, C, D) if x != m])
+    block_outbound(c, A, (C, D))
+    block_outbound(c, B, (C, D))
+    block_outbound(c, C, (A, B))
+    block_outbound(c, D, (A, B))
+    c.step(seconds(2))
+    assert_trusted(c, A, B)
+    assert_suspected(c, A, C, D)
+    assert_trusted(c, B, A)
+    assert_suspected(c, B, C, D)
+    assert_trusted(c, C, D)
+    assert_suspected(c, C, A, B)
+    assert_trusted(c, D, C)
+    assert_suspected(c, D, A, B)
+    c.step(await_suspicion(4))
+    assert_trusted(c, A, B)
+    assert_suspected(c, A)
+    assert_trusted(c, B, A)
+    assert_suspected(c, B)
+    assert_trusted(c, C, D)
+    assert_suspected(c, C)
+    assert_trusted(c, D, C)
+    assert_suspected(c, D)
+
+
+def gossip_dissemination_bound(make):
+    """GossipProtocolTest (:48-64, :154-161) restated on membership gossip: the SUSPECT gossip
+    about a crashed member reaches every alive member within gossipTimeoutToSweep rounds, with
+    loss 0..50 %; every member then removes it within the suspicion timeout + sweep bound."""
+    for n, loss in ((10, 0.0), (50, 10.0), (50, 25.0), (50, 50.0)):
+        cfg = ClusterConfig.defaultLocalConfig()
+        c = make(cfg, n, 100 + n + int(loss))
+        c.set_loss(loss)
+        c.step(2)
+        c.crash([n - 1])
+        g = cfg.gossipConfig()
+        rounds_per_period = cfg.failureDetectorConfig().pingInterval() // g.gossipInterval()
+        sweep_rounds = cluster_math.gossipPeriodsToSweep(g.gossipRepeatMult(), n)
+        susp = cluster_math.suspicionTimeout(cfg.membershipConfig().suspicionMult(), n, 1)
+        bound = susp + sweep_rounds // rounds_per_period + 10
+        for _ in range(bound):
+            c.step(1)
+            if all(c.view(o)[n - 1] == 0 for o in range(n - 1)):
+                break
+        assert all(c.view(o)[n - 1] == 0 for o in range(n - 1)), (n, loss)
+
+
+ALL = [
+    fd_trusted, fd_suspected, fd_trusted_despite_bad_network,
+    mp_initial_phase_ok, mp_partition_no_outbound_then_recover, mp_member_lost_network_then_recover,
+    mp_partition_twice_then_recover, mp_network_lost_on_all_nodes_then_recover, mp_long_partition_then_removed,
+    gossip_dissemination_bound,
+]
