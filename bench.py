@@ -29,22 +29,33 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # name -> workload spec. The default ("c3") is BASELINE.json configs[2], the 65,536-member config
-# the metric is quoted on that fits one GPU: 10 % simultaneous crash plus a 2-way partition
-# (member-id parity) from t0 to t0+40 periods (< the 85-period suspicion timeout, so it heals by
-# refutation and SYNC), LAN defaults, no loss. t0 = the end of the warmup.
+# the metric is quoted on that fits one GPU: a 10 % simultaneous crash plus a 2-way partition from
+# t0 to t0+40 periods (< the 85-period suspicion timeout, so it heals by refutation and SYNC), LAN
+# defaults, no loss; t0 = the end of the warmup. The partition cuts a 16-member group (ids that are
+# multiples of N/16) from the rest. A half/half cut is not simulable under the reference's rules at
+# this N by any implementation: on heal every SYNC/SYNC_ACK re-spreads each accepted SUSPECT record
+# as a new gossip (MembershipProtocolImpl.java:649-656), ~0.47 N^2 gossips (oracle: 25.7k / 112k /
+# 491k at N = 256 / 512 / 1,024), i.e. ~2e9 gossips held by 65,536 members each.
 WORKLOADS = {
     "c3": dict(desc="C3: 65,536 members, dense N x N views, LAN defaults, 10% simultaneous crash + 2-way "
-                    "partition (id parity) for 40 periods healed via SYNC",
-               n=65536, preset="lan", loss=0.0, crash=0.10, part=40, gcap=1 << 18),
+                    "partition (16-member group) for 40 periods healed via SYNC",
+               n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16, gcap=1 << 20, scap=8192),
     "c3s": dict(desc="C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash",
                 n=65536, preset="lan", loss=0.0, crash=0.001, part=0, gcap=1 << 16),
     "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",
-                    n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17),
+                    n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 20, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 16),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }
+
+
+def partition_groups(n, group_size):
+    """Group 1 = `group_size` members spread evenly over the id space (ids k * n // group_size)."""
+    g = np.zeros(n, dtype=np.uint8)
+    g[(np.arange(group_size, dtype=np.int64) * n) // group_size] = 1
+    return g
 
 
 def kernel_bytes(name, d, n):
@@ -84,7 +95,7 @@ def make_cluster(workload, device, seed, event_capacity=0):
 
     w = WORKLOADS[workload]
     c = SwimCluster(preset_config(w["preset"]), w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
-                    event_capacity=event_capacity)
+                    event_capacity=event_capacity, sync_capacity=w.get("scap", 0))
     if w["loss"]:
         c.set_loss(w["loss"])
     return c
@@ -98,7 +109,7 @@ def inject_faults(c, workload, t0, seed, n=None):
     if crashed:
         c.crash(crashed)
     if w["part"]:
-        c.partition((np.arange(n) % 2).astype(np.uint8), t0, t0 + w["part"])
+        c.partition(partition_groups(n, w["part_group"]), t0, t0 + w["part"])
     return crashed
 
 
