@@ -59,7 +59,7 @@ def partition_groups(n, group_size):
 
 
 def kernel_bytes(name, d, n):
-    """Algorithmic HBM bytes of one kernel class over the timed region (DESIGN.md §4).
+    """Algorithmic HBM bytes of one kernel class over the timed region (DESIGN.md §5).
     d = stats deltas over the timed region."""
     if name == "k_sync_merge":  # read SYNC payload row + read table row + write SYNC_ACK payload
         return 12 * d["merge_cells"]
@@ -67,12 +67,12 @@ def kernel_bytes(name, d, n):
         return 8 * d["ack_cells"]
     if name == "k_sync_snapshot":  # copy the sender's row into the SYNC payload
         return 8 * d["merge_cells"]
-    if name == "k_gossip_select":  # own hd row (2 B/slot) + hb read/write + wb write (1 bit/slot each)
-        return (2 * d["gossip_scanned"] + 3 * d["gossip_scanned"] // 8) // 2
-    if name == "k_gossip_send":  # own window bits + receiver bitmap words + receipt (bit, hd, inbox)
-        return d["gossip_scanned"] // 2 // 8 + 4 * d["gossip_probes"] + 14 * d["gossip_first_receipts"]
-    if name == "k_gossip_apply":  # hb + hs words over the live range + per receipt (hd, g_last, subject, record)
-        return d["gossip_scanned"] // 2 // 4 + 14 * d["gossip_first_receipts"]
+    if name == "k_gossip_select":  # holds word per active word, 64 B of infection rounds per MIXED word,
+        return 4 * d["gossip_scanned"] + 64 * d["gossip_hd_words"] + 4 * d["gossip_window_words"]  # + window
+    if name == "k_gossip_pull":  # receiver holds word r/w + receipts word per active window word, one
+        return 12 * d["gossip_pull_words"] + 4 * d["gossip_probes"]  # sender window word per probe
+    if name == "k_gossip_apply":  # per receipt: infection round (2 B) + ring record (8 B)
+        return 10 * d["gossip_first_receipts"]
     if name == "k_susp_sweep":  # stream a deadline column
         return 4 * d["sweep_cells"]
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
@@ -264,7 +264,8 @@ def main():
                      "bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3, "launches": launches},
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
-                                   "merge_cells", "gossip_scanned", "gossip_probes", "events_removed")},
+                                   "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
+                                   "gossip_pull_words", "gossip_probes", "events_removed")},
     }
     c.close()
     if rank == 0 and not args.no_cpu_baseline:

@@ -129,11 +129,14 @@ typedef struct swim_stats {
   uint64_t live_gossip_slots; /* gossip slots currently in use                            */
   uint64_t not_converged;     /* (alive observer, crashed subject) cells still present    */
   /* work counters for the bench's algorithmic-byte model; 0 in the oracle */
-  uint64_t gossip_scanned;    /* holding-row slots scanned by k_gossip_select + k_gossip_send */
+  uint64_t gossip_scanned;    /* active bitmap words scanned by k_gossip_select (x members) */
   uint64_t gossip_probes;     /* receiver holds-now bitmap words read by k_gossip_send     */
   uint64_t sweep_cells;       /* deadline cells streamed by k_susp_sweep                  */
   uint64_t merge_cells;       /* table cells merged by k_sync_merge                       */
   uint64_t ack_cells;         /* table cells merged by k_sync_ack                         */
+  uint64_t gossip_hd_words;   /* active words whose infection rounds k_gossip_select read  */
+  uint64_t gossip_window_words; /* window words written by k_gossip_select (x members)    */
+  uint64_t gossip_pull_words; /* active window words examined by k_gossip_pull (x receivers) */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;

@@ -157,10 +157,10 @@ int step_one(swim_handle* h) {
     P.tick = t * TPP + 1 + q;
     P.round = t * G + q;
     P.create_round = t * G + q + 1;
-    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(64), 0, s, P); });
+    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
     timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
-    timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_send, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
-    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
+    timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
+    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
     timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
   }
 
@@ -279,6 +279,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // inf + sweep + 1 (sweepGossips runs after that round's sends, GossipProtocolImpl.java:150-153),
   // and sweep <= 2 * (rm * bitlen(N) + 1); expiry = inf + sweepmax bounds every holder.
   P.sweepmax = 2u * (P.rm * bitlen(N) + 1u) + 1u;
+  if (P.sweepmax + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
+    std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u rounds > 254)\n", P.rm, N,
+                 P.sweepmax);
+    free_all(h);
+    delete h;
+    return SWIM_EINVAL;
+  }
   P.ecap = h->ecap;
   P.scap = h->scap;
   P.seed = c.seed;
@@ -310,12 +317,17 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.sync_fd, N);
   ALLOC(P.peers, (size_t)N * c.gossip_fanout);
   ALLOC(P.npeers, N);
-  ALLOC(P.g_subject, h->GC);
-  ALLOC(P.g_record, h->GC);
+  ALLOC(P.g_sr, h->GC);
   ALLOC(P.g_hash, h->GC);
   ALLOC(P.g_create, h->GC);
-  ALLOC(P.g_last, h->GC);
-  ALLOC(P.hs, (size_t)N * (h->GC / 32));
+  ALLOC(P.nb, (size_t)N * (h->GC / 32));
+  ALLOC(P.wlast, h->GC / 32);
+  ALLOC(P.in_cnt, N);
+  ALLOC(P.in_list, (size_t)N * INCAP);
+  ALLOC(P.in_ov, 2ull * N * c.gossip_fanout);
+  ALLOC(P.alist, N);
+  ALLOC(P.act, h->GC / 32);
+  ALLOC(P.held, N);
   ALLOC(P.due, N);
   ALLOC(P.events, std::max<uint32_t>(1, h->ecap));
   ALLOC(P.pres, N);
@@ -360,11 +372,18 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.g_epoch, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.g_cursor, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.gseq, 0, (size_t)N * 4, s);
-  (void)hipMemsetAsync(P.g_last, 0, (size_t)h->GC * 4, s);
-  (void)hipMemsetAsync(P.hs, 0, (size_t)N * (h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.in_cnt, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.nb, 0, (size_t)N * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
+  (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
+  {  // every member starts with others = N - 1
+    const uint32_t all = N;
+    (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);
+    (void)hipStreamSynchronize(s);
+  }
   (void)hipMemsetAsync(P.stat_shards, 0, (size_t)STAT_SHARDS * STAT_STRIDE * 8, s);
   hipError_t e = hipStreamSynchronize(s);
   if (e == hipSuccess) e = hipGetLastError();
@@ -573,6 +592,9 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->merge_cells = stats[ST_MERGE_CELLS];
   out->ack_cells = stats[ST_ACK_CELLS];
   out->live_gossip_slots = ctl.gcount - ctl.glo;
+  out->gossip_hd_words = stats[ST_G_HDREAD];
+  out->gossip_window_words = stats[ST_G_WINW];
+  out->gossip_pull_words = stats[ST_G_PULLW];
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];
@@ -627,19 +649,20 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
   HIPC(h, hipStreamSynchronize(h->stream));
   const uint32_t GC = h->GC;
   std::vector<uint32_t> bits(GC / 32), cr(GC), hs(GC);
-  std::vector<uint16_t> d(GC);
+  std::vector<uint8_t> d(GC);
   HIPC(h, hipMemcpy(bits.data(), h->base.hb + (size_t)member * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
-  HIPC(h, hipMemcpy(d.data(), h->base.hd + (size_t)member * GC, (size_t)GC * 2, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(d.data(), h->base.hd + (size_t)member * GC, (size_t)GC, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(cr.data(), h->base.g_create, (size_t)GC * 4, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(hs.data(), h->base.g_hash, (size_t)GC * 4, hipMemcpyDeviceToHost));
   uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;
+  const uint32_t rnow = (uint32_t)(h->period * h->G);  // next round to run
   if (hi - lo > GC) lo = hi - GC;
   for (uint32_t id = lo; id < hi; ++id) {
     const uint32_t s = id & (GC - 1);
     if (!((bits[s >> 5] >> (s & 31)) & 1u)) continue;
     if (n < cap) {
       out_hash[n] = hs[s];
-      out_inf[n] = cr[s] + (uint16_t)(d[s] - (uint16_t)cr[s]);  // hd = infection round mod 2^16
+      out_inf[n] = rnow - (uint8_t)(rnow - d[s]);  // hd = infection round mod 2^8, age < 2^8
     }
     ++n;
   }

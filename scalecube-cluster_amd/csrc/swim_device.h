@@ -6,10 +6,12 @@
 //                     streams one subject column over all observers (MembershipProtocolImpl.java:101)
 //   inbox  u32[N][N]  observer-major lattice max of the records a gossip round delivered
 //   hb     u32[N][GC/32] member-major "holds gossip slot s now" bitmap
-//   hd     u16[N][GC]    infectionPeriod - creation round of each held gossip
-//   wb     u32[N][GC/32] the member's start-of-round send window (written by k_gossip_select)
+//   hd     u8[N][GC]     infection round (mod 2^8) of each held gossip
 //                     (GossipProtocolImpl.java:49, GossipState.java:14)
-//                     (GossipProtocolImpl.java:49, GossipState.java:14)
+//   act    u32[GC/32]    this round's active bitmap words (k_gossip_prep): the words where some
+//                     holder's send window or sweep can change; every other word is skipped
+//   wb, nb u32[N][GC/32] per member, indexed by position in `act`: start-of-round send window and
+//                     the round's first receipts (k_gossip_pull)
 // plus per-member vectors (cursors, counts, liveness) and per-slot gossip metadata.
 #pragma once
 
@@ -44,6 +46,9 @@ enum StatIdx : int {
   ST_SWEEP_CELLS,
   ST_MERGE_CELLS,
   ST_ACK_CELLS,
+  ST_G_HDREAD,
+  ST_G_WINW,
+  ST_G_PULLW,
   ST_COUNT
 };
 
@@ -72,8 +77,17 @@ struct Ctl {
   uint32_t stage_count; // staged SYNC requests this period
   uint32_t due_count;   // subject columns due for the suspicion sweep
   uint32_t overflow;
-  uint32_t pad[7];
+  uint32_t n_act;       // active bitmap words this round (k_gossip_prep)
+  uint32_t w_beg;       // unwrapped index of the live range's first bitmap word this round
+  uint32_t n_alist;     // receivers with first receipts this round (k_gossip_pull)
+  uint32_t n_inov;      // entries of in_ov this round
+  uint32_t pad[3];
+  uint32_t bl_hist[32]; // alive members per bit_length(others + 1) (spread/sweep bounds)
 };
+
+// act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
+constexpr uint32_t ACT_OFF_MASK = (1u << 26) - 1u;
+enum WordClass : uint32_t { WC_NONE = 0, WC_MIXED = 1, WC_ALL = 2 };
 
 // Everything a kernel needs, passed by value.
 struct KP {
@@ -96,9 +110,10 @@ struct KP {
   uint32_t* colmin;
   uint32_t* inbox;
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
-  uint16_t* hd;  // [N][GC] infection round mod 2^16, valid where the hb bit is set (exact: a
-                 // held entry is at most sweep+1 rounds old, far below 2^16)
-  uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select
+  uint8_t* hd;   // [N][GC] infection round mod 2^8, valid where the hb bit is set (exact: an
+                 // alive member's held entry is at most sweep+1 <= sweepmax rounds old, < 2^8)
+  uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select (act-indexed)
+  uint32_t* nb;  // [N][GC/32] first receipts of the round found by k_gossip_pull (act-indexed)
   uint32_t* cnt;
   int32_t* cnt_delta;
   uint8_t* alive;
@@ -110,12 +125,16 @@ struct KP {
   uint32_t* sync_fd;
   uint32_t* peers;   // [N][f] gossip peers chosen this round
   uint32_t* npeers;  // [N]
-  uint32_t* g_subject;
-  uint32_t* g_record;
+  uint2* g_sr;        // [GC] (subject, packed record) of each gossip
   uint32_t* g_hash;
   uint32_t* g_create;
-  uint32_t* g_last;   // latest infection round of any holder (plain idempotent stores)
-  uint32_t* hs;       // [N][GC/32] holds bitmap at the start of the round's deliveries
+  uint32_t* wlast;    // [GC/32] max infection round of any holder over the word's slots
+  uint32_t* in_cnt;   // [N] senders that picked member p this round (k_gossip_select)
+  uint32_t* in_list;  // [N][INCAP] the first INCAP of them
+  uint32_t* in_ov;    // [N*f][2] (receiver, sender) pairs beyond INCAP
+  uint32_t* alist;    // [N] receivers with first receipts this round
+  uint32_t* act;      // [GC/32] active words of this round (k_gossip_prep)
+  uint32_t* held;     // [N] live gossips each member holds (GossipProtocolImpl.gossips.size())
   uint32_t* due;
   swim_event* events;
   uint32_t* pres;
@@ -135,6 +154,7 @@ struct KP {
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
 
 // partition cut and directed link blocks only (no liveness, no loss draw)
 __device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t dst) {
@@ -195,17 +215,17 @@ __device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32
                                             uint32_t seq) {
   const uint32_t id = atomicAdd(&P.ctl->gcount, 1u);
   const uint32_t s = id & P.gmask;
-  // the live id range must stay below GC - 64 slots so 64-slot chunks never alias across the
-  // ring wrap, and the slot's previous gossip must be dead everywhere
-  if (id - P.ctl->glo >= P.GC - 64u || (id >= P.GC && P.g_last[s] + P.sweepmax >= P.create_round))
-    atomicOr(&P.ctl->overflow, OV_GOSSIP);
-  P.g_subject[s] = subject;
-  P.g_record[s] = record;
+  // the live id range must stay below GC - 64 slots so bitmap words never alias across the
+  // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
+  if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  P.g_sr[s] = make_uint2(subject, record);
   P.g_hash[s] = gossip_hash(origin, seq);
   P.g_create[s] = P.create_round;
-  P.g_last[s] = P.create_round;
-  P.hd[(size_t)origin * P.GC + s] = (uint16_t)P.create_round;  // origin's infectionPeriod
-  atomicOr(&P.hb[(size_t)origin * (P.GC >> 5) + (s >> 5)], 1u << (s & 31u));
+  P.hd[(size_t)origin * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
+  const uint32_t old = atomicOr(&P.hb[(size_t)origin * (P.GC >> 5) + (s >> 5)], 1u << (s & 31u));
+  if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
+  // a reused word's stale maximum is older than any live creation round, so max() resets it
+  if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
 }
 
 // MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip.

@@ -34,14 +34,21 @@ __global__ void k_finalize(KP P) {
   if (i < P.N) {
     const int32_t d = P.cnt_delta[i];
     if (d) {
-      P.cnt[i] = (uint32_t)((int32_t)P.cnt[i] + d);
+      const uint32_t old = P.cnt[i], now = (uint32_t)((int32_t)old + d);
+      P.cnt[i] = now;
       P.cnt_delta[i] = 0;
+      const uint32_t b0 = bitlen(old + 1u), b1 = bitlen(now + 1u);
+      if (b0 != b1 && P.alive[i]) {
+        atomicSub(&P.ctl->bl_hist[b0], 1u);
+        atomicAdd(&P.ctl->bl_hist[b1], 1u);
+      }
     }
   }
 }
 
 // swim_crash: transport.stop() — presence no longer counted, timers dropped.
 __global__ void k_crash(KP P, uint32_t c) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < P.N; j += gridDim.x * blockDim.x) {
     if (j != c && P.view[(size_t)c * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
     P.dl[(size_t)j * P.N + c] = 0u;
@@ -152,26 +159,6 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
 // ---------------------------------------------------------------------------------------
 // Gossip round.
 // ---------------------------------------------------------------------------------------
-__global__ void k_gossip_prep(KP P) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  Ctl* c = P.ctl;
-  const uint32_t hi = c->gcount;
-  uint32_t lo = c->glo;
-  // a gossip is dead once every holder has swept it: the last holder got it at g_last
-  while (lo < hi && (hi - lo > P.GC || P.g_last[lo & P.gmask] + P.sweepmax < P.round)) ++lo;
-  c->glo = lo;
-  c->scan_lo = lo;
-  c->scan_hi = hi;
-}
-
-// One wave per member m, on the start-of-round state (before any delivery of round r):
-// doSpreadGossip's "gossips non-empty" test (GossipProtocolImpl.java:144-146), the peer
-// choice selectGossipMembers (:253-274), the send window (:242-251) written to wb, and the
-// sweep sweepGossips (:281-304) of entries with r > infectionPeriod + sweep, cleared before
-// round-r deliveries so receivers see them absent. A gossip swept in round r still counts as
-// held at its start (r-1 <= inf + sweep). Lane = one 32-slot bitmap word: a wave covers 2,048
-// slots per step; the 32 infection offsets (64 B) and creation rounds (128 B) of a word are
-// vector loads, so every lane has its loads in flight at once.
 __device__ __forceinline__ uint32_t range_mask(uint32_t id0, uint32_t lo, uint32_t hi) {
   // bits b of the word whose id id0 + b lies in [lo, hi)
   uint32_t m = 0xFFFFFFFFu;
@@ -180,6 +167,103 @@ __device__ __forceinline__ uint32_t range_mask(uint32_t id0, uint32_t lo, uint32
   return m;
 }
 
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* total, uint32_t* lds16) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63u) lds16[w] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64u; ++k) {
+    const uint32_t t = lds16[k];
+    if (k < w) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// One workgroup, once per round, before any member acts. Advances the oldest-live pointer (a
+// gossip is dead once every holder has swept it: the last holder got it by wlast) and lists the
+// ACTIVE bitmap words: those where some holder's send window (age <= spread) may be non-empty or
+// some holder's sweep (age > sweep, GossipProtocolImpl.java:281-304) may fire this round. Every
+// holder's infection round of a slot lies in [g_create, wlast], so a word whose whole age range
+// is past every window and short of every sweep is idle for all members and is never touched.
+// Spread/sweep bounds use the min/max bit_length(others+1) over alive members (bl_hist).
+__global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
+  __shared__ uint32_t s_lo, s_hi, s_blo, s_bhi;
+  __shared__ uint32_t s_part[16];
+  Ctl* c = P.ctl;
+  if (threadIdx.x == 0) {
+    const uint32_t hi = c->gcount;
+    uint32_t lo = c->glo;
+    // word granularity: wlast bounds the infection round of every slot of the word
+    while (lo < hi && (hi - lo > P.GC || P.wlast[(lo & P.gmask) >> 5] + P.sweepmax < P.round)) ++lo;
+    c->glo = lo;
+    c->n_alist = 0;
+    c->n_inov = 0;
+    c->scan_lo = lo;
+    c->scan_hi = hi;
+    uint32_t blo = 32, bhi = 0;
+    for (uint32_t b = 0; b < 32u; ++b)
+      if (c->bl_hist[b]) {
+        blo = b < blo ? b : blo;
+        bhi = b;
+      }
+    if (blo > bhi) blo = bhi = 1;  // nobody alive: nothing will be scanned anyway
+    s_lo = lo;
+    s_hi = hi;
+    s_blo = blo;
+    s_bhi = bhi;
+  }
+  __syncthreads();
+  const uint32_t lo = s_lo, hi = s_hi;
+  const uint32_t w_beg = lo >> 5, w_end = (hi + 31u) >> 5;
+  const int32_t r = (int32_t)P.round;
+  const int32_t spread_lo = (int32_t)(P.rm * s_blo), spread_hi = (int32_t)(P.rm * s_bhi);
+  const int32_t sweep_lo = 2 * (spread_lo + 1), sweep_hi = 2 * (spread_hi + 1);
+  const uint32_t W32 = P.GC >> 5;
+  uint32_t base = 0;
+  for (uint32_t t0 = w_beg; t0 < w_end; t0 += blockDim.x) {
+    const uint32_t wi = t0 + threadIdx.x;
+    uint32_t e = 0;
+    bool on = false;
+    if (wi < w_end) {
+      const uint32_t ws = wi & (W32 - 1u);
+      const uint32_t id0 = (wi << 5) > lo ? (wi << 5) : lo;
+      const int32_t inf_lo = (int32_t)P.g_create[id0 & P.gmask];
+      const int32_t inf_hi = (int32_t)P.wlast[ws];
+      const int32_t amin = r - inf_hi, amax = r - inf_lo;  // holders' ages lie in [amin, amax]
+      const uint32_t wc = amin > spread_hi ? WC_NONE : (amax <= spread_lo ? WC_ALL : WC_MIXED);
+      const uint32_t sc = amax <= sweep_lo ? WC_NONE : (amin > sweep_hi ? WC_ALL : WC_MIXED);
+      on = wc != WC_NONE || sc != WC_NONE;
+      e = (wi - w_beg) | (wc << 26) | (sc << 28);
+    }
+    uint32_t total;
+    const uint32_t off = block_excl_scan1024(on ? 1u : 0u, &total, s_part);
+    if (on) P.act[base + off] = e;
+    base += total;
+  }
+  if (threadIdx.x == 0) {
+    c->n_act = base;
+    c->w_beg = w_beg;
+  }
+}
+
+// One wave per member m, on the start-of-round state (before any delivery of round r):
+// doSpreadGossip's "gossips non-empty" test (GossipProtocolImpl.java:144-146, the held count),
+// the peer choice selectGossipMembers (:253-274), the send window (:242-251) and the sweep
+// sweepGossips (:281-304) of entries with r > infectionPeriod + sweep, over the ACTIVE words only.
+// Swept entries are cleared before round-r deliveries so receivers see them absent; a gossip
+// swept in round r still counts as held at its start. Window words go to wb, indexed by position
+// in the active list. A word's infection rounds (64 B) are read only when its class is MIXED;
+// ALL/NONE words are decided by the class. A member with a non-empty window registers with each
+// chosen peer (in_cnt), so delivery can run receiver-side (k_gossip_pull).
 __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
@@ -188,47 +272,61 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const bool active = (m < N) && P.alive[m] && lo < hi;
   const uint32_t W32 = P.GC >> 5;
-  uint32_t others = 0;
-  bool any_l = false;
-  if (active) {
+  uint32_t others = 0, nclear = 0, hdw = 0, winw = 0;
+  bool win_l = false;
+  const bool any = active && P.held[m] > 0u;  // wave-uniform
+  if (any) {
     others = P.cnt[m];
     const uint32_t sweep = sweep_rounds(P, others);
     const uint32_t spread = spread_rounds(P, others);
     uint32_t* hbr = P.hb + (size_t)m * W32;
     uint32_t* wbr = P.wb + (size_t)m * W32;
-    const uint16_t* hdr = P.hd + (size_t)m * P.GC;
-    const uint32_t w_end = ((hi + 63u) & ~63u) >> 5;
-    for (uint32_t wi = ((lo & ~63u) >> 5) + lane; wi < w_end; wi += 64u) {
+    const uint8_t* hdr = P.hd + (size_t)m * P.GC;
+    for (uint32_t k = lane; k < n_act; k += 64u) {
+      const uint32_t e = P.act[k];
+      const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+      const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
       const uint32_t ws = wi & (W32 - 1u);
       const uint32_t word = hbr[ws];
       const uint32_t held = word & range_mask(wi << 5, lo, hi);
       uint32_t clear = 0, win = 0;
       if (held) {
-        any_l = true;
-        // age = r - infectionPeriod, exact mod 2^16 (every held entry received before round r)
-        uint4 dv[4];
-        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
+        if (wc == WC_MIXED || sc == WC_MIXED) {
+          // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
+          ++hdw;
+          uint4 dv[2];
+          const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
+          dv[0] = dp[0];
+          dv[1] = dp[1];
+          const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dv);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dv[k] = dp[k];
-        const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dv);
-#pragma unroll
-        for (uint32_t b = 0; b < 32u; ++b) {
-          const uint32_t age = (r - (d32[b >> 1] >> ((b & 1u) * 16u))) & 0xFFFFu;
-          const uint32_t hbit = (held >> b) & 1u;
-          clear |= (hbit & (age > sweep ? 1u : 0u)) << b;  // sweepGossips
-          win |= (hbit & (age <= spread ? 1u : 0u)) << b;
+          for (uint32_t b = 0; b < 32u; ++b) {
+            const uint32_t age = (r - (d32[b >> 2] >> ((b & 3u) * 8u))) & 0xFFu;
+            const uint32_t hbit = (held >> b) & 1u;
+            clear |= (hbit & (age > sweep ? 1u : 0u)) << b;  // sweepGossips
+            win |= (hbit & (age <= spread ? 1u : 0u)) << b;
+          }
+        } else {
+          if (wc == WC_ALL) win = held;
+          if (sc == WC_ALL) clear = held;
         }
-        if (clear) hbr[ws] = word & ~clear;
+        if (clear) {
+          hbr[ws] = word & ~clear;
+          nclear += (uint32_t)__popc(clear);
+        }
       }
-      wbr[ws] = win;
-      P.hs[(size_t)m * W32 + ws] = word & ~clear;  // holds at the start of this round's deliveries
+      if (wc != WC_NONE) {
+        ++winw;
+        wbr[k] = win;
+        win_l |= win != 0u;
+      }
     }
   }
-  const bool any = __any(any_l);
   uint32_t np = 0;
-  if (active && any) {
+  if (any) {
     // selectGossipMembers, wave-cooperative: lanes test 64 consecutive positions of the
     // keyed shuffle, ballot, take the first members in position order.
     const uint32_t* row = P.view + (size_t)m * N;
@@ -291,172 +389,264 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (lane < np) P.peers[(size_t)m * P.f + lane] = s_peers[w][lane];
   }
-  if (m < N && lane == 0) P.npeers[m] = np;
-  add_stat(P, ST_G_SCANNED, (active && lane == 0) ? hi - lo : 0u);
+  // spreadGossipsTo is a no-op for an empty window: only non-empty windows reach receivers
+  const bool reg = __any(win_l) && np > 0u;
+  if (reg && lane < np) {
+    const uint32_t p = s_peers[w][lane];
+    const uint32_t slot = atomicAdd(&P.in_cnt[p], 1u);
+    if (slot < INCAP) {
+      P.in_list[(size_t)p * INCAP + slot] = m;
+    } else {  // rare: a receiver picked by more than INCAP senders
+      const uint32_t o = atomicAdd(&P.ctl->n_inov, 1u);
+      P.in_ov[2 * o] = p;
+      P.in_ov[2 * o + 1] = m;
+    }
+  }
+  nclear = wave_sum(nclear);
+  if (any && lane == 0 && nclear) P.held[m] -= nclear;
+  if (m < N && lane == 0) P.npeers[m] = reg ? np : 0u;
+  add_stat(P, ST_G_SCANNED, (any && lane == 0) ? n_act : 0u);
+  add_stat(P, ST_G_HDREAD, hdw);
+  add_stat(P, ST_G_WINW, winw);
 }
 
-// One wave per sender m: spreadGossipsTo (GossipProtocolImpl.java:215-251) for the peers chosen
-// by k_gossip_select over its start-of-round window wb. Each window gossip goes to each alive
-// peer (one GossipRequest per gossip, :225-239); the receiver adopts it iff its holds-now bit
-// is clear (onGossipReq :171-183). Lane = one 32-slot word: the probe of a peer is one bitmap
-// word, and all of that word's deliveries to the peer are ONE fire-and-forget atomicOr. Every
-// copy delivered in a round has the same effect, so no winner is needed; k_gossip_apply finds
-// the round's first receipts as hb & ~hs.
-__global__ void __launch_bounds__(256) k_gossip_send(KP P) {
+// One wave per receiver p: spreadGossipsTo (GossipProtocolImpl.java:215-251) seen from the
+// receiving side. Every sender that picked p sends each gossip of its start-of-round window as
+// one GossipRequest (:225-239); p adopts a gossip iff it does not hold it (onGossipReq :171-183).
+// So p's first receipts of the round are (U over senders of window & delivered) & ~holds, computed
+// in registers per active word: no atomics, every copy delivered in a round has the same effect.
+// NetworkEmulator.evaluateLoss draws one value per (sender, receiver, gossip) message and is drawn
+// only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
+// receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
+__global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
+  __shared__ uint32_t s_snd[4][64];  // the current chunk of senders (read inside divergent loops)
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t m = blockIdx.x * 4u + (threadIdx.x >> 6);
-  const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t p = blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (p >= P.N) return;  // whole wave
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
-  uint32_t sends = 0, probes = 0;
-  const uint32_t np = m < P.N ? P.npeers[m] : 0u;
-  if (np > 0u) {
-    // the words k_gossip_select rewrote this round: [lo & ~63, hi rounded up to 64)
-    const uint32_t* wbr = P.wb + (size_t)m * W32;
-    const uint32_t w_beg = (lo & ~63u) >> 5, w_end = ((hi + 63u) & ~63u) >> 5;
-    for (uint32_t k = 0; k < np; ++k) {  // peers are wave-uniform
-      const uint32_t p = __builtin_amdgcn_readfirstlane(P.peers[(size_t)m * P.f + k]);
-      if (!P.alive[p]) continue;  // a stopped transport loses every message
-      const bool reach = link_open(P, m, p) && P.loss_mode != 2u;
-      uint32_t* hbp = P.hb + (size_t)p * W32;
-      for (uint32_t wi = w_beg + lane; wi < w_end; wi += 64u) {
-        const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t win = wbr[ws];
-        if (!win) continue;
-        const uint32_t hw = hbp[ws];
-        ++probes;
-        sends += (uint32_t)__popc(win);
-        uint32_t mask = reach ? (win & ~hw) : 0u;  // receiver lacks it (at load time)
-        if (mask && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
-          uint32_t need = mask;
-          mask = 0u;
-          while (need) {
-            const uint32_t b = (uint32_t)__builtin_ctz(need);
-            need &= need - 1u;
-            if (draw1(P.seed, K_GOSSIP, m, p, P.g_hash[ws * 32u + b], P.tick) >= P.loss_thr) mask |= 1u << b;
+  const uint32_t deg = P.in_cnt[p];
+  uint32_t sends = 0, probes = 0, receipts = 0, words = 0;
+  if (deg && P.alive[p] && n_act) {  // a stopped transport loses every message
+    uint32_t* hbr = P.hb + (size_t)p * W32;
+    uint32_t* nbr = P.nb + (size_t)p * W32;
+    const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
+    uint32_t ov_pos = 0;
+    for (uint32_t done = 0; done < deg;) {
+      // next chunk of senders: lane q holds sender q
+      uint32_t sreg = 0, cdeg = 0;
+      if (done == 0) {
+        cdeg = deg < INCAP ? deg : INCAP;
+        if (lane < cdeg) sreg = P.in_list[(size_t)p * INCAP + lane];
+      } else {
+        while (cdeg == 0 && ov_pos < n_ov) {
+          const uint32_t o = ov_pos + lane;
+          const bool mine = o < n_ov && P.in_ov[2 * o] == p;
+          const unsigned long long b = __ballot(mine);
+          const uint32_t rank = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+          const uint32_t snd = mine ? P.in_ov[2 * o + 1] : 0u;
+          // gather: lane `rank` of the chunk takes sender `snd`
+          for (uint32_t t = 0; t < 64u; ++t) {
+            const uint32_t v = __shfl(snd, (int)t, 64);
+            const uint32_t rk = __shfl(rank, (int)t, 64);
+            if (((b >> t) & 1ull) && lane == rk) sreg = v;
+          }
+          cdeg = (uint32_t)__popcll(b);
+          ov_pos += 64u;
+        }
+        if (cdeg == 0) break;  // invariant: in_cnt counts every registration
+      }
+      done += cdeg;
+      const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sreg, p);
+      const unsigned long long reach = __ballot(ok_l);
+      uint32_t* snd = s_snd[threadIdx.x >> 6];
+      snd[lane] = sreg;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (uint32_t k = lane; k < n_act; k += 64u) {
+        const uint32_t e = P.act[k];
+        if (((e >> 26) & 3u) == WC_NONE) continue;
+        const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+        const uint32_t hw = hbr[ws];
+        ++words;
+        uint32_t u = 0;
+        for (uint32_t q0 = 0; q0 < cdeg; q0 += 4u) {
+          uint32_t wv[4], mv[4];
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {  // issue the window loads of 4 senders together
+            mv[j] = q0 + j < cdeg ? snd[q0 + j] : 0u;
+            wv[j] = q0 + j < cdeg ? P.wb[(size_t)mv[j] * W32 + k] : 0u;
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t win = wv[j];
+            if (!win) continue;
+            ++probes;
+            sends += (uint32_t)__popc(win);
+            if (!((reach >> (q0 + j)) & 1ull)) continue;
+            uint32_t cand = win & ~hw & ~u;
+            if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+              uint32_t need = cand;
+              cand = 0u;
+              while (need) {
+                const uint32_t b = (uint32_t)__builtin_ctz(need);
+                need &= need - 1u;
+                if (draw1(P.seed, K_GOSSIP, mv[j], p, P.g_hash[ws * 32u + b], P.tick) >= P.loss_thr)
+                  cand |= 1u << b;
+              }
+            }
+            u |= cand;
           }
         }
-        if (mask) atomicOr(&hbp[ws], mask);
+        if (u) {
+          hbr[ws] = hw | u;
+          nbr[k] |= u;
+          receipts += (uint32_t)__popc(u);
+        }
       }
+      __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
+    }
+    const uint32_t total = wave_sum(receipts);
+    if (lane == 0 && total) {
+      const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);
+      P.alist[idx] = p;
     }
   }
+  if (lane == 0) P.in_cnt[p] = 0u;  // ready for the next round
   add_stat(P, ST_GOSSIP_SENDS, sends);
   add_stat(P, ST_G_PROBES, probes);
-  add_stat(P, ST_G_SCANNED, (np > 0u && lane == 0) ? hi - lo : 0u);
+  add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
+  add_stat(P, ST_G_PULLW, words);
 }
 
-constexpr uint32_t HCAP = 512;  // per-wave LDS hash slots (power of two)
-
-// Hands the set bits of the lanes' receipt words to the whole wave, two words per step: lanes
-// 0-31 take bit (lane) of one word, lanes 32-63 bit (lane-32) of the next. fn(slot) runs once per
-// set bit. All lanes must call it (wave-uniform control flow).
-template <typename F>
-__device__ __forceinline__ void wave_for_bits(uint32_t ws, uint32_t bits, F&& fn) {
-  const uint32_t lane = threadIdx.x & 63u;
-  unsigned long long bal = __ballot(bits != 0u);
-  while (bal) {
-    const uint32_t la = (uint32_t)__builtin_ctzll(bal);
-    bal &= bal - 1ull;
-    uint32_t lb = 64u;
-    if (bal) {
-      lb = (uint32_t)__builtin_ctzll(bal);
-      bal &= bal - 1ull;
-    }
-    const uint32_t src = lane < 32u ? la : lb;
-    const uint32_t my_ws = __shfl(ws, (int)(src & 63u), 64);
-    const uint32_t my_bits = __shfl(bits, (int)(src & 63u), 64);
-    const uint32_t b = lane & 31u;
-    if (src < 64u && ((my_bits >> b) & 1u)) fn(my_ws * 32u + b);
-  }
-}
+constexpr uint32_t HCAP_LOG = 13;
+constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 64 KiB of keys + values
+constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
+constexpr uint32_t APPLY_THREADS = 512;
+constexpr uint32_t APPLY_BLOCKS = 512;     // persistent: 2 workgroups per CU (LDS-bound)
 
 // Membership apply of a round's first receipts: onGossipReq's new-gossip branch
 // (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
-// the records that reached a cell this round. One wave per receiver p: the
-// first receipts are exactly hb & ~hs. They get infectionPeriod r+1; their records are
-// max-reduced per subject in a per-wave LDS hash table (the global inbox is the fallback when a
-// receiver gets more than HCAP/2 new gossips in one round), then applied once per subject.
-__global__ void __launch_bounds__(256) k_gossip_apply(KP P) {
-  __shared__ uint32_t s_key[4][HCAP];
-  __shared__ uint32_t s_val[4][HCAP];
+// the records that reached a cell this round. Persistent workgroups take the
+// receivers of alist; for receiver p the receipts are nb. They get infectionPeriod r+1 (one
+// 64-B read-modify-write of the word's infection rounds); their records are max-reduced per
+// subject in an LDS hash sized to the receipt count (a storm round brings a receiver tens of
+// thousands of gossips about a few thousand subjects); a subject that finds no slot within
+// HPROBE probes goes to the global inbox instead, consistently for the whole round. Then one
+// updateMembership per subject.
+__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
+  __shared__ uint32_t s_key[HCAP];
+  __shared__ uint32_t s_val[HCAP];
+  __shared__ uint32_t s_red[APPLY_THREADS / 64];
+  __shared__ uint32_t s_spill;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t w = threadIdx.x >> 6;
-  const uint32_t p = blockIdx.x * 4u + w;
+  const uint32_t wv = threadIdx.x >> 6;
   const uint32_t r = P.round;
-  const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
-  uint32_t created = 0, receipts = 0;
-  const bool act = p < P.N && P.alive[p] && lo < hi;
-  const uint32_t* hbr = P.hb + (size_t)p * W32;
-  const uint32_t* hsr = P.hs + (size_t)p * W32;
-  const uint32_t w_beg = (lo & ~63u) >> 5, w_end = ((hi + 63u) & ~63u) >> 5;
-  // receipts = hb & ~hs; ids >= hi are gossips this kernel itself creates (refutations)
-  auto new_bits = [&](uint32_t wi) -> uint32_t {
-    const uint32_t ws = wi & (W32 - 1u);
-    return wi < w_end ? (hbr[ws] & ~hsr[ws] & range_mask(wi << 5, lo, hi)) : 0u;
-  };
-  if (act)
-    for (uint32_t wi = w_beg + lane; wi < w_end; wi += 64u) receipts += (uint32_t)__popc(new_bits(wi));
-  const uint32_t total = wave_sum(receipts);
-  if (act && total) {
-    const bool lds = total <= HCAP / 2u;
-    uint32_t* hk = s_key[w];
-    uint32_t* hv = s_val[w];
-    if (lds) {
-      for (uint32_t t = lane; t < HCAP; t += 64u) {
-        hk[t] = NONE;
-        hv[t] = 0u;
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  uint32_t created = 0;
+  for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const uint32_t p = P.alist[li];
+    uint32_t* nbr = P.nb + (size_t)p * W32;
+    // receipts of p and the table size (>= 2x receipts, 64 .. HCAP)
+    uint32_t c = 0;
+    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x)
+      if (((P.act[k] >> 26) & 3u) != WC_NONE) c += (uint32_t)__popc(nbr[k]);
+    c = wave_sum(c);
+    if (lane == 0) s_red[wv] = c;
+    if (threadIdx.x == 0) s_spill = 0u;
+    __syncthreads();
+    uint32_t total = 0;
+    for (uint32_t q = 0; q < blockDim.x / 64u; ++q) total += s_red[q];
+    uint32_t lg = 6;
+    while (lg < HCAP_LOG && (1u << lg) < 2u * total) ++lg;
+    const uint32_t hm = (1u << lg) - 1u;
+    for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x) {
+      s_key[t] = NONE;
+      s_val[t] = 0u;
     }
-    // infection round, gossip liveness, and the lattice max per subject
-    for (uint32_t wb0 = w_beg; wb0 < w_end; wb0 += 64u) {
-      const uint32_t wi = wb0 + lane;
-      wave_for_bits(wi & (W32 - 1u), new_bits(wi), [&](uint32_t s) {
-        P.hd[(size_t)p * P.GC + s] = (uint16_t)(r + 1u);
-        if (P.g_last[s] != r + 1u) P.g_last[s] = r + 1u;
-        const uint32_t subj = P.g_subject[s], rec = P.g_record[s];
-        if (lds) {
-          uint32_t h = (subj * 0x9E3779B1u) >> (32u - 9u);  // HCAP = 2^9
-          for (;;) {  // linear probing; at most HCAP/2 keys, so a slot is always found
-            const uint32_t prev = atomicCAS(&hk[h], NONE, subj);
-            if (prev == NONE || prev == subj) break;
-            h = (h + 1u) & (HCAP - 1u);
+    __syncthreads();
+    // infection rounds, word liveness, and the lattice max per subject
+    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {
+      const uint32_t e = P.act[k];
+      if (((e >> 26) & 3u) == WC_NONE) continue;
+      const uint32_t bits = nbr[k];
+      if (!bits) continue;
+      const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+      if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
+      uint4* dp = reinterpret_cast<uint4*>(P.hd + (size_t)p * P.GC + (size_t)ws * 32u);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
+        const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
+        if (!nb16) continue;
+        uint4 v = dp[q];
+        uint32_t* v32 = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+        for (uint32_t b = 0; b < 16u; ++b)
+          if ((nb16 >> b) & 1u) {
+            const uint32_t sh = (b & 3u) * 8u;
+            v32[b >> 2] = (v32[b >> 2] & ~(0xFFu << sh)) | (((r + 1u) & 0xFFu) << sh);
           }
-          atomicMax(&hv[h], rec);
-        } else {
-          atomicMax(&P.inbox[(size_t)p * P.N + subj], rec);
+        dp[q] = v;
+      }
+      uint32_t left = bits;
+      while (left) {
+        const uint32_t b = (uint32_t)__builtin_ctz(left);
+        left &= left - 1u;
+        const uint2 sr = P.g_sr[ws * 32u + b];
+        uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
+        bool placed = false;
+        for (uint32_t q = 0; q < HPROBE; ++q) {
+          const uint32_t prev = atomicCAS(&s_key[h], NONE, sr.x);
+          if (prev == NONE || prev == sr.x) {
+            atomicMax(&s_val[h], sr.y);
+            placed = true;
+            break;
+          }
+          h = (h + 1u) & hm;
         }
-      });
+        if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
+          atomicMax(&P.inbox[(size_t)p * P.N + sr.x], sr.y);
+          s_spill = 1u;
+        }
+      }
     }
+    __syncthreads();
     const uint32_t snap = P.cnt[p];
     auto apply = [&](uint32_t subj, uint32_t r1) {
       const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, snap, T);
-      if (rec) {  // only onSelfMemberDetected spreads here (reason MEMBERSHIP_GOSSIP)
+      if (rec) {  // only onSelfMemberDetected spreads here (reason MEMBERSHIP_GOSSIP): one per round
         emit_gossip(P, p, subj, rec, P.gseq[p]++);
         ++created;
       }
     };
-    if (lds) {
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      for (uint32_t t = lane; t < HCAP; t += 64u)  // one updateMembership per subject
-        if (hk[t] != NONE) apply(hk[t], hv[t]);
-    } else {
+    for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x)  // one updateMembership per subject
+      if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
+    if (s_spill) {
       __threadfence();
-      for (uint32_t wb0 = w_beg; wb0 < w_end; wb0 += 64u) {
-        const uint32_t wi = wb0 + lane;
-        wave_for_bits(wi & (W32 - 1u), new_bits(wi), [&](uint32_t s) {
-          const uint32_t subj = P.g_subject[s];
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {
+        const uint32_t e = P.act[k];
+        if (((e >> 26) & 3u) == WC_NONE) continue;
+        uint32_t left = nbr[k];
+        const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+        while (left) {
+          const uint32_t b = (uint32_t)__builtin_ctz(left);
+          left &= left - 1u;
+          const uint32_t subj = P.g_sr[ws * 32u + b].x;
           const uint32_t r1 = atomicExch(&P.inbox[(size_t)p * P.N + subj], 0u);
           if (r1) apply(subj, r1);  // several new gossips about one subject: applied once
-        });
+        }
       }
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x)  // nb is all-zero between rounds
+      if (((P.act[k] >> 26) & 3u) != WC_NONE && nbr[k]) nbr[k] = 0u;
+    if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
+    __syncthreads();  // the table is reused by the next receiver
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
-  add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
   flush_tally(P, T);
 }
 

@@ -95,6 +95,9 @@ STAT_FIELDS = [
     "sweep_cells",
     "merge_cells",
     "ack_cells",
+    "gossip_hd_words",
+    "gossip_window_words",
+    "gossip_pull_words",
 ]
 
 

@@ -235,7 +235,7 @@ class SwimCluster:
         return {k: out[i * self.n:(i + 1) * self.n] for i, k in enumerate(names)}
 
     # -- bench helpers (HIP library only) ---------------------------------------------------
-    KERNEL_CLASSES = ["k_fd", "k_gossip_send", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
+    KERNEL_CLASSES = ["k_fd", "k_gossip_pull", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
                       "k_sync_snapshot", "bookkeeping", "k_gossip_select"]
 
     def step_async(self, periods: int = 1):
