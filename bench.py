@@ -9,8 +9,9 @@ Philox-chosen crash set) and resident in HBM before the timed region.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3s]
 
 N > 1 runs under torch.distributed.run, one rank per GPU (RANK/LOCAL_RANK/WORLD_SIZE from the
-env); each rank steps its own independent cluster replica (the row-sharded RCCL
-path is not built yet), barrier + max-over-ranks timing, value = all ranks' member-periods / time.
+env): the workload's ONE cluster is split into observer-row shards, one per GPU, exchanging
+gossip windows, gossip ids and SYNC tables over RCCL each round (DESIGN.md §7; strong scaling);
+barrier + max-over-ranks timing, value = the cluster's member-periods / time.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -90,12 +91,15 @@ def preset_config(preset):
     return {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
 
 
-def make_cluster(workload, device, seed, event_capacity=0):
-    from swimhip import SwimCluster
+def make_cluster(workload, device, seed, event_capacity=0, sharded=False):
+    """One cluster of the workload: on this GPU alone, or (sharded) this rank's observer rows of
+    a cluster spread over the torch.distributed world."""
+    from swimhip import ShardedSwimCluster, SwimCluster
 
     w = WORKLOADS[workload]
-    c = SwimCluster(preset_config(w["preset"]), w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
-                    event_capacity=event_capacity, sync_capacity=w.get("scap", 0))
+    cls = ShardedSwimCluster if sharded else SwimCluster
+    c = cls(preset_config(w["preset"]), w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
+            event_capacity=event_capacity, sync_capacity=w.get("scap", 0))
     if w["loss"]:
         c.set_loss(w["loss"])
     return c
@@ -183,7 +187,7 @@ def main():
 
     w = WORKLOADS[args.workload]
     n = w["n"]
-    c = make_cluster(args.workload, local, args.seed)
+    c = make_cluster(args.workload, local, args.seed, sharded=world > 1)
     log(f"created {args.workload}: N={n}")
     c.step(args.warmup)
     log(f"warmup {args.warmup} periods done")
@@ -223,7 +227,7 @@ def main():
     ms, launches = ktimes[dom]
     byts = kernel_bytes(dom, d, n)
     avg_s = ms / 1e3 / max(1, launches)
-    per_launch = byts / max(1, launches)
+    per_launch = byts / world / max(1, launches)  # work counters are cluster-wide, launches per shard
     achieved = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
 
     # periods to DEAD convergence (untimed): every alive observer removed every crashed member
@@ -241,7 +245,7 @@ def main():
         if c.stats()["not_converged"] == 0:
             periods_to_dead = int(max(last[crashed])) - 1 - crash_period
 
-    value = world * n * args.steps / elapsed
+    value = n * args.steps / elapsed  # the one cluster's member-periods (all shards together)
     out = {
         "metric": "member-periods/sec (whole node)",
         "value": value,
@@ -251,11 +255,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (converged start, Philox-chosen crash set, seeded)",
-        "config": {"workload": w["desc"], "members": n, "members_per_gpu": n, "parallelism": f"replicas x{world}",
+        "config": {"workload": w["desc"], "members": n, "members_per_gpu": n // world,
+                   "parallelism": f"observer-row shards x{world}" if world > 1 else "1 GPU",
                    "crashed": len(crashed), "loss_pct": w["loss"], "partition_periods": w["part"],
                    "gossip_ring_slots": w["gcap"]},
         "periods_to_dead": periods_to_dead,

@@ -105,6 +105,8 @@ typedef struct swim_config {
   uint32_t dirty_capacity;  /* gossip (observer, subject) inbox cells per round (0 = default) */
   uint32_t flags;           /* reserved, 0                                                */
   int32_t device;           /* HIP device ordinal the handle lives on                     */
+  uint32_t shard_rank;      /* observer-row shard of this handle (0 .. shard_world-1)     */
+  uint32_t shard_world;     /* shards of the cluster (0 or 1 = unsharded); see swim_shard_step */
 } swim_config;
 
 typedef struct swim_stats {
@@ -165,9 +167,40 @@ int swim_step(swim_handle* h, uint32_t periods);
 int swim_step_async(swim_handle* h, uint32_t periods);
 int swim_sync(swim_handle* h);
 
+/* ---- observer-row sharding over several GPUs ----------------------------
+ * A cluster of N members may be split into W = shard_world handles (one per GPU / process),
+ * handle r owning observers [r*N/W, (r+1)*N/W) (N % W == 0). Every handle is created with
+ * the same config except shard_rank, and receives the same fault-injection calls. A period
+ * is then advanced with swim_shard_step, which runs the period's kernels up to the next
+ * cross-shard exchange and describes it in a swim_xchg; the host performs the collective
+ * over its communicator (RCCL all-gather / all-to-all-v / all-reduce) on the two device
+ * buffers it attached, fills recv_counts, and calls swim_shard_step again. The exchanges of
+ * one period: gossip-id commits (all-gather of the gossips created in a phase), the
+ * per-round gossip-liveness maximum (all-reduce MAX), the per-round sender windows bound for
+ * receivers on other shards (all-to-all-v), and the SYNC / SYNC_ACK membership-table rows of
+ * cross-shard pairs (all-to-all-v). Results are identical to the unsharded handle's. */
+#define SWIM_MAX_WORLD 64
+#define SWIM_X_DONE 0          /* the period is complete                                   */
+#define SWIM_X_ALLGATHER 1     /* every rank contributes send_words (host pads to the max)  */
+#define SWIM_X_ALLTOALLV 2     /* send_counts[q] words to rank q, consecutive in rank order */
+#define SWIM_X_ALLREDUCE_MAX 3 /* element-wise u32 max of send_words words, in place       */
+typedef struct swim_xchg {
+  uint32_t op;
+  uint32_t world;
+  uint64_t send_words;
+  uint64_t send_counts[SWIM_MAX_WORLD];
+  uint64_t recv_counts[SWIM_MAX_WORLD]; /* host: words received from each rank             */
+  uint64_t recv_stride;                 /* host, ALLGATHER: words per rank block in recv    */
+} swim_xchg;
+/* Device buffer sizes (u32 words) the host must allocate and attach before stepping. */
+int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv_words);
+int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev);
+/* Begin a period (when none is in flight) or resume it after the described exchange. */
+int swim_shard_step(swim_handle* h, swim_xchg* x);
+
 /* MembershipEvents in canonical order (period, observer, phase, subject, type). */
 int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);
-/* One observer's membershipTable as packed cells (n = n_members). */
+/* One observer's membershipTable as packed cells (n = n_members; the observer's shard). */
 int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);
 /* Suspicion deadlines (period at which the timer fires, 0 = none) for one observer. */
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);

@@ -730,7 +730,7 @@ extern "C" {
 int oracle_create(const swim_config* cfg, oracle_handle** out) {
   if (!cfg || !out) return SWIM_EINVAL;
   if (cfg->n_members < 1 || cfg->n_members > (1u << 24) || cfg->ping_interval_ms <= 0 || cfg->gossip_interval_ms <= 0 ||
-      cfg->gossip_fanout < 1 || cfg->sync_interval_ms <= 0)
+      cfg->gossip_fanout < 1 || cfg->sync_interval_ms <= 0 || cfg->shard_world > 1)  // one unsharded replay
     return SWIM_EINVAL;
   oracle_handle* h = new (std::nothrow) oracle_handle();
   if (!h) return SWIM_ENOMEM;

@@ -36,6 +36,17 @@ struct swim_handle {
   uint64_t part_t0 = 0, part_t1 = 0;
   hipStream_t stream = nullptr;
   KP base{};
+  // period in flight (sharded handles stop at exchanges)
+  KP cur{};
+  int pc = 0;
+  uint32_t q = 0;
+  // sharding
+  uint32_t world = 1, rank = 0, xrec = 0;
+  void* xsend = nullptr;
+  void* xrecv = nullptr;
+  uint64_t xsend_words = 0, xrecv_words = 0;
+  uint32_t* d_xcounts = nullptr;
+  uint32_t* d_blx = nullptr;
   unsigned long long* d_digest = nullptr;
   std::vector<void*> allocs;
   std::string err;
@@ -134,68 +145,259 @@ void memset_ctl_u32(swim_handle* h, size_t offset) {
   (void)hipMemsetAsync(reinterpret_cast<char*>(h->base.ctl) + offset, 0, 4, h->stream);
 }
 
-// One protocol period.
-int step_one(swim_handle* h) {
-  KP P = h->base;
-  const uint32_t t = (uint32_t)h->period;
-  const uint32_t N = h->N, G = h->G, TPP = h->TPP;
+// ---- one protocol period as a resumable sequence ---------------------
+// Unsharded handles run a period straight through. Sharded handles (world > 1) stop at each
+// cross-shard exchange, describe it in a swim_xchg, and resume after the host's collective.
+enum Pc : int { PC_FD = 0, PC_FD_C, PC_R_MAX, PC_R_SEL, PC_R_PULL, PC_R_C, PC_SUSP, PC_SYNC_REQ, PC_SYNC_ACK, PC_END };
+
+void set_phase(swim_handle* h, KP& P, uint32_t phase) {
+  const uint32_t t = (uint32_t)h->period, G = h->G, TPP = h->TPP;
+  P = h->base;
   P.period = t;
   P.part_active = (h->period >= h->part_t0 && h->period < h->part_t1) ? 1u : 0u;
-  const uint32_t gN = blocks_for(N, 256);
-  hipStream_t s = h->stream;
-
-  // phase 0: failure detector
-  P.phase = 0;
-  P.tick = t * TPP;
-  P.round = t * G;
-  P.create_round = t * G;
-  timed(h, 0, [&] { hipLaunchKernelGGL(k_fd, dim3(gN), dim3(256), 0, s, P); });
-
-  // phases 1..G: gossip rounds
-  for (uint32_t q = 0; q < G; ++q) {
-    P.phase = 1 + q;
-    P.tick = t * TPP + 1 + q;
-    P.round = t * G + q;
-    P.create_round = t * G + q + 1;
-    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
-    timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
-    timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(N, 4)), dim3(256), 0, s, P); });
-    timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
-    timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
+  P.phase = phase;
+  P.tick = t * TPP + phase;
+  if (phase == 0) {
+    P.round = t * G;
+    P.create_round = t * G;
+  } else if (phase <= G) {
+    P.round = t * G + phase - 1;
+    P.create_round = t * G + phase;
+  } else {
+    P.round = (t + 1) * G;
+    P.create_round = (t + 1) * G;
   }
+}
 
-  // phase G+1: suspicion timeouts
-  P.phase = G + 1;
-  P.tick = t * TPP + G + 1;
-  P.create_round = (t + 1) * G;
-  memset_ctl_u32(h, offsetof(Ctl, due_count));
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_due, dim3(gN), dim3(256), 0, s, P); });
-  timed(h, 3, [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
-
-  // phase G+2: SYNC
-  P.phase = G + 2;
-  P.tick = t * TPP + G + 2;
-  memset_ctl_u32(h, offsetof(Ctl, stage_count));
-  (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
-  (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_select, dim3(gN), dim3(256), 0, s, P); });
-  timed(h, 6, [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * N, 256)), dim3(256), 0, s, P); });
-  timed(h, 4, [&] { hipLaunchKernelGGL(k_sync_merge, dim3(N), dim3(256), 0, s, P); });
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
-
-  // phase G+3: SYNC_ACK
-  P.phase = G + 3;
-  P.tick = t * TPP + G + 3;
-  timed(h, 5, [&] { hipLaunchKernelGGL(k_sync_ack, dim3(N), dim3(256), 0, s, P); });
-  timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gN), dim3(256), 0, s, P); });
-
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
-  h->period++;
+int read_ctl(swim_handle* h, Ctl* c) {
+  HIPC(h, hipMemcpyAsync(c, h->base.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
+}
+
+void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
+  std::memset(x, 0, sizeof *x);
+  x->op = op;
+  x->world = world;
+}
+
+// Commit the phase's staged gossips. Unsharded: in place, no host round trip. Sharded: the
+// host all-gathers every shard's stage (returns true: exchange pending).
+bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
+  hipStream_t s = h->stream;
+  if (h->world == 1) {
+    timed(h, 7, [&] {
+      hipLaunchKernelGGL(k_gossip_commit, dim3(256), dim3(256), 0, s, P, P.stg, &P.ctl->stg_count, 0u);
+    });
+    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, &P.ctl->stg_count); });
+    return false;
+  }
+  Ctl c;
+  if ((*rc = read_ctl(h, &c))) return false;
+  const uint32_t n = std::min(c.stg_count, P.stg_cap);
+  if (n) (void)hipMemcpyAsync(h->xsend, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
+  (void)hipStreamSynchronize(s);
+  xchg_clear(x, SWIM_X_ALLGATHER, h->world);
+  x->send_words = 4ull * n;
+  return true;
+}
+
+int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
+  hipStream_t s = h->stream;
+  uint32_t counts[SWIM_MAX_WORLD], total = 0, base[SWIM_MAX_WORLD];
+  for (uint32_t q = 0; q < h->world; ++q) {
+    counts[q] = (uint32_t)(x->recv_counts[q] / 4);
+    base[q] = total;
+    total += counts[q];
+  }
+  counts[h->world] = total;  // world < SWIM_MAX_WORLD
+  HIPC(h, hipMemcpyAsync(h->d_xcounts, counts, 4ull * (h->world + 1), hipMemcpyHostToDevice, s));
+  const uint32_t* xr = reinterpret_cast<const uint32_t*>(h->xrecv);
+  for (uint32_t q = 0; q < h->world; ++q)
+    if (counts[q])
+      hipLaunchKernelGGL(k_gossip_commit, dim3(blocks_for(counts[q], 256)), dim3(256), 0, s, P,
+                         reinterpret_cast<const uint4*>(xr + q * x->recv_stride), h->d_xcounts + q, base[q]);
+  hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, h->d_xcounts + h->world);
+  return SWIM_OK;
+}
+
+// Runs the current period from h->pc. Returns SWIM_OK with x->op = SWIM_X_DONE at the end of
+// the period, or SWIM_OK with another op when an exchange must happen first (world > 1).
+int period_resume(swim_handle* h, swim_xchg* x) {
+  const uint32_t N = h->N, G = h->G, W = h->world, nloc = h->base.nloc;
+  const uint32_t gL = blocks_for(nloc, 256);
+  hipStream_t s = h->stream;
+  KP& P = h->cur;
+  int rc = SWIM_OK;
+  for (;;) {
+    switch (h->pc) {
+      case PC_FD:  // phase 0: failure detector
+        set_phase(h, P, 0);
+        timed(h, 0, [&] { hipLaunchKernelGGL(k_fd, dim3(gL), dim3(256), 0, s, P); });
+        h->pc = PC_FD_C;
+        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        if (rc) return rc;
+        break;
+      case PC_FD_C:
+        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        h->q = 0;
+        h->pc = PC_R_MAX;
+        break;
+      case PC_R_MAX:  // phases 1..G: gossip rounds
+        set_phase(h, P, 1 + h->q);
+        h->pc = PC_R_SEL;
+        if (W > 1) {  // liveness + bounds over every shard
+          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+          hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, P);
+          HIPC(h, hipStreamSynchronize(s));
+          xchg_clear(x, SWIM_X_ALLREDUCE_MAX, W);
+          x->send_words = h->GC / 32 + 2;
+          return SWIM_OK;
+        }
+        break;
+      case PC_R_SEL:
+        if (W > 1) {
+          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+          hipLaunchKernelGGL(k_round_max_unpack, dim3(64), dim3(256), 0, s, P);
+          HIPC(h, hipMemcpyAsync(h->d_blx, P.xsend + h->GC / 32, 8, hipMemcpyDeviceToDevice, s));
+          P.blx = h->d_blx;
+          HIPC(h, hipMemsetAsync(P.ctl->xg_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
+        }
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
+        timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        h->pc = PC_R_PULL;
+        if (W > 1) {  // windows bound for receivers on other shards
+          Ctl c;
+          if ((rc = read_ctl(h, &c))) return rc;
+          const uint32_t rec = 2u + c.n_act;
+          uint32_t n_rec = 0;
+          xchg_clear(x, SWIM_X_ALLTOALLV, W);
+          for (uint32_t q = 0; q < W; ++q) {
+            x->send_counts[q] = (uint64_t)c.xg_cnt[q] * rec;
+            n_rec += c.xg_cnt[q];
+          }
+          if ((uint64_t)n_rec * rec > h->xsend_words) return fail(h, SWIM_EOVERFLOW, "gossip exchange buffer too small");
+          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+          if (n_rec) hipLaunchKernelGGL(k_gossip_pack, dim3(std::min<uint32_t>(n_rec, 4096)), dim3(256), 0, s, P, n_rec, rec);
+          HIPC(h, hipStreamSynchronize(s));
+          h->xrec = rec;
+          return SWIM_OK;
+        }
+        break;
+      case PC_R_PULL:
+        if (W > 1) {
+          uint64_t words = 0;
+          for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
+          const uint32_t n_rec = (uint32_t)(words / h->xrec);
+          P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+          P.xrec_words = h->xrec;
+          if (n_rec) hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+        }
+        timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        h->pc = PC_R_C;
+        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        if (rc) return rc;
+        break;
+      case PC_R_C:
+        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        h->q++;
+        h->pc = h->q < G ? PC_R_MAX : PC_SUSP;
+        break;
+      case PC_SUSP:  // phase G+1: suspicion timeouts
+        set_phase(h, P, G + 1);
+        memset_ctl_u32(h, offsetof(Ctl, due_count));
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_due, dim3(blocks_for(N, 256)), dim3(256), 0, s, P); });
+        timed(h, 3, [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        // phase G+2: SYNC requests
+        set_phase(h, P, G + 2);
+        memset_ctl_u32(h, offsetof(Ctl, stage_count));
+        HIPC(h, hipMemsetAsync(P.ctl->xs_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
+        (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
+        (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 6, [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
+        h->pc = PC_SYNC_REQ;
+        if (W > 1) {  // tables of requesters whose receiver lives on another shard
+          Ctl c;
+          if ((rc = read_ctl(h, &c))) return rc;
+          uint32_t n_rec = 0;
+          xchg_clear(x, SWIM_X_ALLTOALLV, W);
+          for (uint32_t q = 0; q < W; ++q) {
+            x->send_counts[q] = (uint64_t)c.xs_cnt[q] * (N + 2u);
+            n_rec += c.xs_cnt[q];
+          }
+          if (n_rec > h->scap) return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
+          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+          if (n_rec) hipLaunchKernelGGL(k_sync_pack, dim3(std::min<uint32_t>(n_rec, 4096)), dim3(256), 0, s, P, n_rec);
+          HIPC(h, hipStreamSynchronize(s));
+          return SWIM_OK;
+        }
+        break;
+      case PC_SYNC_REQ: {
+        uint32_t n_rec = 0;
+        if (W > 1) {
+          uint64_t words = 0;
+          for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
+          n_rec = (uint32_t)(words / (N + 2u));
+          if (n_rec > h->scap) return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
+          P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+          if (n_rec) hipLaunchKernelGGL(k_sync_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+        }
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
+        timed(h, 7, [&] {
+          hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * nloc, 256)), dim3(256), 0, s, P);
+        });
+        if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+        timed(h, 4, [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        h->pc = PC_SYNC_ACK;
+        if (W > 1) {  // SYNC_ACK tables back to the requesters' shards, in the order received
+          uint64_t back[SWIM_MAX_WORLD];
+          for (uint32_t q = 0; q < W; ++q) back[q] = x->recv_counts[q];
+          xchg_clear(x, SWIM_X_ALLTOALLV, W);
+          for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
+          HIPC(h, hipStreamSynchronize(s));
+          return SWIM_OK;
+        }
+        break;
+      }
+      case PC_SYNC_ACK:  // phase G+3: SYNC_ACK
+        set_phase(h, P, G + 3);
+        if (W > 1) {
+          uint64_t words = 0;
+          for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
+          const uint32_t n_rec = (uint32_t)(words / (N + 2u));
+          P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+          if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+        }
+        timed(h, 5, [&] { hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
+        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        if (rc) return rc;
+        break;
+      case PC_END: {
+        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
+        h->period++;
+        h->pc = PC_FD;
+        xchg_clear(x, SWIM_X_DONE, W);
+        return SWIM_OK;
+      }
+    }
+  }
+}
+
+int step_one(swim_handle* h) {
+  swim_xchg x;
+  int rc = period_resume(h, &x);
+  if (rc) return rc;
+  return x.op == SWIM_X_DONE ? SWIM_OK : fail(h, SWIM_EINVAL, "sharded handle: use swim_shard_step");
 }
 
 int check_overflow(swim_handle* h) {
@@ -225,6 +427,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
       c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
     return SWIM_EINVAL;
+  const uint32_t world = c.shard_world ? c.shard_world : 1u;
+  if (world >= SWIM_MAX_WORLD || c.shard_rank >= world || c.n_members % world) return SWIM_EINVAL;
   // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
   if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
     return SWIM_EINVAL;
@@ -289,11 +493,20 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.ecap = h->ecap;
   P.scap = h->scap;
   P.seed = c.seed;
+  h->world = world;
+  h->rank = c.shard_rank;
+  P.world = world;
+  P.rank = c.shard_rank;
+  P.nloc = N / world;
+  P.row0 = c.shard_rank * P.nloc;
+  P.blx = nullptr;
+  P.stg_cap = h->GC;
   P.loss_mode = 0;
   P.loss_thr = 0;
   P.link = nullptr;
 
-  const size_t NN = (size_t)N * N;
+  const size_t NN = (size_t)P.nloc * N;  // this shard's rows
+  const size_t NL = P.nloc;
   int rc = SWIM_OK;
   uint8_t* group = nullptr;
 #define ALLOC(ptr, count)                       \
@@ -301,9 +514,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.view, NN);
   ALLOC(P.dl, NN);
   ALLOC(P.inbox, NN);
-  ALLOC(P.hb, (size_t)N * (h->GC / 32));
-  ALLOC(P.wb, (size_t)N * (h->GC / 32));
-  ALLOC(P.hd, (size_t)N * h->GC);
+  ALLOC(P.hb, NL * (h->GC / 32));
+  ALLOC(P.wb, NL * (h->GC / 32));
+  ALLOC(P.hd, NL * h->GC);
   ALLOC(P.colmin, N);
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
@@ -320,7 +533,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_sr, h->GC);
   ALLOC(P.g_hash, h->GC);
   ALLOC(P.g_create, h->GC);
-  ALLOC(P.nb, (size_t)N * (h->GC / 32));
+  ALLOC(P.nb, NL * (h->GC / 32));
+  ALLOC(P.stg, P.stg_cap);
+  ALLOC(P.xg_pend, 2ull * world * NL * c.gossip_fanout);
+  ALLOC(P.xs_pend, 2ull * world * NL);
+  ALLOC(P.rs_ref, 2ull * N);
+  ALLOC(P.ack_ref, 2ull * N);
+  ALLOC(h->d_xcounts, SWIM_MAX_WORLD + 1);
+  ALLOC(h->d_blx, 2);
   ALLOC(P.wlast, h->GC / 32);
   ALLOC(P.in_cnt, N);
   ALLOC(P.in_list, (size_t)N * INCAP);
@@ -340,7 +560,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_count, N);
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
-  ALLOC(P.bucket, h->scap);
+  ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
   ALLOC(P.ctl, 1);
   ALLOC(P.stat_shards, (size_t)STAT_SHARDS * STAT_STRIDE);
   ALLOC(h->d_digest, 2);
@@ -358,11 +578,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, SWIM_PACK(0, SWIM_ALIVE));
   (void)hipMemsetAsync(P.dl, 0, NN * 4, s);
   (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
-  (void)hipMemsetAsync(P.hb, 0, (size_t)N * (h->GC / 32) * 4, s);
-  (void)hipMemsetAsync(P.wb, 0, (size_t)N * (h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.hb, 0, NL * (h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.wb, 0, NL * (h->GC / 32) * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmin, (size_t)N, NONE);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, N - 1);
-  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, N - 1);
+  // presence is per shard: observers of this shard holding the subject (all but the subject itself)
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, P.nloc);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P.pres + P.row0, (size_t)P.nloc,
+                     P.nloc - 1);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.sync_fd, (size_t)N, NONE);
   (void)hipMemsetAsync(P.cnt_delta, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.alive, 1, N, s);
@@ -373,14 +596,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.g_cursor, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.gseq, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.in_cnt, 0, (size_t)N * 4, s);
-  (void)hipMemsetAsync(P.nb, 0, (size_t)N * (h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.nb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
-  {  // every member starts with others = N - 1
-    const uint32_t all = N;
+  {  // every member of this shard starts with others = N - 1
+    const uint32_t all = P.nloc;
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
   }
@@ -473,6 +696,7 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
 
 int swim_step_async(swim_handle* h, uint32_t periods) {
   if (!h) return SWIM_EINVAL;
+  if (h->world > 1) return fail(h, SWIM_EINVAL, "sharded handle: use swim_shard_step");
   for (uint32_t p = 0; p < periods; ++p) {
     int rc = step_one(h);
     if (rc) return rc;
@@ -518,16 +742,18 @@ int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n
 }
 
 int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
-  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
-  HIPC(h, hipMemcpyAsync(row, h->base.view + (size_t)observer * h->N, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
+  const size_t lr = observer - h->base.row0;
+  HIPC(h, hipMemcpyAsync(row, h->base.view + lr * h->N, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
 }
 
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
-  if (!h || !row || observer >= h->N || n != h->N) return SWIM_EINVAL;
+  if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
   // subject-major storage: strided 2D copy of one observer column
-  HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + observer, (size_t)h->N * 4, 4, h->N, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
+                           hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
 }
@@ -535,7 +761,8 @@ int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32
 int swim_digest(swim_handle* h, uint64_t* vd, uint64_t* dd) {
   if (!h) return SWIM_EINVAL;
   HIPC(h, hipMemsetAsync(h->d_digest, 0, 16, h->stream));
-  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base.view, h->base.dl, h->N, h->d_digest);
+  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base.view, h->base.dl, h->N, h->base.row0,
+                     h->base.nloc, h->d_digest);
   unsigned long long out[2];
   HIPC(h, hipMemcpyAsync(out, h->d_digest, 16, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -643,15 +870,16 @@ int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t
 
 int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
                         uint32_t* n_out) {
-  if (!h || member >= h->N || !n_out) return SWIM_EINVAL;
+  if (!h || member - h->base.row0 >= h->base.nloc || !n_out) return SWIM_EINVAL;
+  const size_t lr = member - h->base.row0;
   Ctl ctl;
   HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   const uint32_t GC = h->GC;
   std::vector<uint32_t> bits(GC / 32), cr(GC), hs(GC);
   std::vector<uint8_t> d(GC);
-  HIPC(h, hipMemcpy(bits.data(), h->base.hb + (size_t)member * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
-  HIPC(h, hipMemcpy(d.data(), h->base.hd + (size_t)member * GC, (size_t)GC, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(bits.data(), h->base.hb + lr * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(d.data(), h->base.hd + lr * GC, (size_t)GC, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(cr.data(), h->base.g_create, (size_t)GC * 4, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(hs.data(), h->base.g_hash, (size_t)GC * 4, hipMemcpyDeviceToHost));
   uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;
@@ -677,6 +905,43 @@ int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n) {
   for (int k = 0; k < 6; ++k)
     HIPC(h, hipMemcpyAsync(out6n + (size_t)k * n, src[k], (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv_words) {
+  if (!h || !send_words || !recv_words) return SWIM_EINVAL;
+  const uint64_t W32 = h->GC / 32, nloc = h->base.nloc;
+  // window records: <= f per local sender, 2 + active words each; SYNC rows: <= scap, 2 + N each;
+  // gossip commits: 4 words per staged gossip (x world when gathered); round maxima: W32 + 2
+  const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
+  const uint64_t rows = (uint64_t)h->scap * (h->N + 2ull);
+  const uint64_t stg = 4ull * h->base.stg_cap;
+  *send_words = std::max({win, rows, stg, W32 + 2});
+  *recv_words = std::max({(uint64_t)(h->N - nloc) * h->base.f * (2 + W32), rows, stg * h->world});
+  return SWIM_OK;
+}
+
+int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev) {
+  if (!h || !send_dev || !recv_dev) return SWIM_EINVAL;
+  h->xsend = send_dev;
+  h->xrecv = recv_dev;
+  uint64_t sw = 0, rw = 0;
+  swim_shard_buffer_words(h, &sw, &rw);
+  h->xsend_words = sw;
+  h->xrecv_words = rw;
+  return SWIM_OK;
+}
+
+int swim_shard_step(swim_handle* h, swim_xchg* x) {
+  if (!h || !x) return SWIM_EINVAL;
+  if (h->world > 1 && (!h->xsend || !h->xrecv)) return fail(h, SWIM_EINVAL, "swim_shard_attach first");
+  int rc = period_resume(h, x);
+  if (rc) return rc;
+  if (x->op == SWIM_X_DONE) {  // end of period: surface overflows like swim_step
+    HIPC(h, hipStreamSynchronize(h->stream));
+    resolve_timing(h);
+    return check_overflow(h);
+  }
   return SWIM_OK;
 }
 

@@ -77,12 +77,15 @@ struct Ctl {
   uint32_t stage_count; // staged SYNC requests this period
   uint32_t due_count;   // subject columns due for the suspicion sweep
   uint32_t overflow;
+  uint32_t stg_count;   // gossips staged by emit_gossip since the last commit
   uint32_t n_act;       // active bitmap words this round (k_gossip_prep)
   uint32_t w_beg;       // unwrapped index of the live range's first bitmap word this round
   uint32_t n_alist;     // receivers with first receipts this round (k_gossip_pull)
   uint32_t n_inov;      // entries of in_ov this round
-  uint32_t pad[3];
+  uint32_t pad[2];
   uint32_t bl_hist[32]; // alive members per bit_length(others + 1) (spread/sweep bounds)
+  uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
+  uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
@@ -93,6 +96,9 @@ enum WordClass : uint32_t { WC_NONE = 0, WC_MIXED = 1, WC_ALL = 2 };
 struct KP {
   // sizes / config
   uint32_t N, GC, gmask, G, S, f, kreq, rm, mult, n_seeds, time_left_pos;
+  // observer-row shard of this handle: members [row0, row0 + nloc) live here;
+  // view/inbox/hb/wb/nb/hd rows and dl columns are indexed by the local row m - row0
+  uint32_t row0, nloc, rank, world;
   uint32_t sweepmax;  // max gossipPeriodsToSweep + 1: last round a holder may still count a gossip
   uint32_t ecap, scap;
   uint64_t seed;
@@ -149,11 +155,27 @@ struct KP {
   uint32_t* recv_off;   // [N+1]
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
+  uint4* stg;         // [stg_cap] gossips created since the last commit: origin, subject, record, id hash
+  uint32_t stg_cap;
+  // cross-shard exchange (world > 1)
+  const uint32_t* blx;  // global (max bit_length, 32 - min bit_length) after the round's all-reduce
+  uint32_t* xsend;      // host-attached device buffers of the current exchange
+  const uint32_t* xrecv;
+  uint32_t xrec_words;  // words per received record (window records: 2 + n_act; rows: 2 + N)
+  uint32_t* xg_pend;    // [world][nloc*f][2] (sender, remote peer) pairs of the round
+  uint32_t* xs_pend;    // [world][2*nloc] SYNC requests bound for each remote shard
+  uint32_t* rs_ref;     // [2N] receiver side: record index of remote request q
+  uint32_t* ack_ref;    // [2N] requester side: record index of the SYNC_ACK of remote request q
   Ctl* ctl;
   unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
 
+__device__ __forceinline__ size_t lrow(const KP& P, uint32_t m) { return (size_t)(m - P.row0); }
+__device__ __forceinline__ bool is_local(const KP& P, uint32_t m) { return m - P.row0 < P.nloc; }
+
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t REMOTE = 0xFFFFFFFEu;   // req_stage of a request staged on another shard
+constexpr uint32_t XREC = 0x80000000u;     // in_list entry: a received window record, not a local row
 constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
 
 // partition cut and directed link blocks only (no liveness, no loss draw)
@@ -209,23 +231,17 @@ struct Tally {
   uint32_t accepted = 0, refut = 0, added = 0, removed = 0;
 };
 
-// GossipProtocolImpl.spread -> createAndPutGossip (GossipProtocolImpl.java:124-128,163-169):
-// allocate a ring slot, publish the record, the origin holds it from `create_round`.
+// GossipProtocolImpl.spread -> createAndPutGossip (GossipProtocolImpl.java:124-128,163-169),
+// first half: stage the gossip. k_gossip_commit gives it a ring slot after the phase (on every
+// shard, in shard order), publishes the record, and the origin holds it from `create_round`.
 __device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32_t subject, uint32_t record,
                                             uint32_t seq) {
-  const uint32_t id = atomicAdd(&P.ctl->gcount, 1u);
-  const uint32_t s = id & P.gmask;
-  // the live id range must stay below GC - 64 slots so bitmap words never alias across the
-  // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
-  if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
-  P.g_sr[s] = make_uint2(subject, record);
-  P.g_hash[s] = gossip_hash(origin, seq);
-  P.g_create[s] = P.create_round;
-  P.hd[(size_t)origin * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
-  const uint32_t old = atomicOr(&P.hb[(size_t)origin * (P.GC >> 5) + (s >> 5)], 1u << (s & 31u));
-  if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
-  // a reused word's stale maximum is older than any live creation round, so max() resets it
-  if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
+  const uint32_t idx = atomicAdd(&P.ctl->stg_count, 1u);
+  if (idx >= P.stg_cap) {
+    atomicOr(&P.ctl->overflow, OV_GOSSIP);
+    return;
+  }
+  P.stg[idx] = make_uint4(origin, subject, record, gossip_hash(origin, seq));
 }
 
 // MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip.
@@ -240,7 +256,7 @@ __device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t sub
 // number so that every origin's ids are canonical.
 __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint32_t subj, uint32_t r1,
                                                  uint32_t reason, uint32_t attempt, uint32_t others_snap, Tally& T) {
-  uint32_t* cellp = P.view + (size_t)obs * P.N + subj;
+  uint32_t* cellp = P.view + lrow(P, obs) * P.N + subj;
   const uint32_t r0 = *cellp;
   if (!is_overrides(r1, r0)) return 0u;
   const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;
@@ -253,7 +269,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.refut++;
     return r2;
   }
-  uint32_t* dlp = P.dl + (size_t)subj * P.N + obs;
+  uint32_t* dlp = P.dl + (size_t)subj * P.nloc + lrow(P, obs);
   if (r1 == SWIM_DEAD) {
     *dlp = 0u;
     *cellp = SWIM_ABSENT;

@@ -30,8 +30,8 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
 }
 
 __global__ void k_finalize(KP P) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < P.N) {
+  const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P.row0 + P.nloc) {
     const int32_t d = P.cnt_delta[i];
     if (d) {
       const uint32_t old = P.cnt[i], now = (uint32_t)((int32_t)old + d);
@@ -47,25 +47,60 @@ __global__ void k_finalize(KP P) {
 }
 
 // swim_crash: transport.stop() — presence no longer counted, timers dropped.
+// Only the shard that owns row c has anything to drop (presence counts are per-shard partials).
 __global__ void k_crash(KP P, uint32_t c) {
+  if (!is_local(P, c)) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < P.N; j += gridDim.x * blockDim.x) {
-    if (j != c && P.view[(size_t)c * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[(size_t)j * P.N + c] = 0u;
+    if (j != c && P.view[lrow(P, c) * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
+    P.dl[(size_t)j * P.nloc + lrow(P, c)] = 0u;
   }
+}
+
+// Second half of emit_gossip: `count` staged gossips at `ents` get ids gcount + base + i (every
+// shard commits the same entries in the same order, so the ring stays replicated); the origin's
+// shard marks it held with infectionPeriod = create_round.
+__global__ void k_gossip_commit(KP P, const uint4* ents, const uint32_t* count, uint32_t base) {
+  const uint32_t n = *count;
+  const uint32_t g0 = P.ctl->gcount + base;
+  const uint32_t W32 = P.GC >> 5;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint4 e = ents[i];
+    const uint32_t id = g0 + i;
+    const uint32_t s = id & P.gmask;
+    // the live id range must stay below GC - 64 slots so bitmap words never alias across the
+    // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
+    if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+    P.g_sr[s] = make_uint2(e.y, e.z);
+    P.g_hash[s] = e.w;
+    P.g_create[s] = P.create_round;
+    // a reused word's stale maximum is older than any live creation round, so max() resets it
+    if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
+    if (is_local(P, e.x)) {
+      P.hd[lrow(P, e.x) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
+      const uint32_t old = atomicOr(&P.hb[lrow(P, e.x) * W32 + (s >> 5)], 1u << (s & 31u));
+      if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[e.x], 1u);
+    }
+  }
+}
+
+// after the commit launches of a phase: advance the id counter, empty the local stage
+__global__ void k_gossip_commit_fin(KP P, const uint32_t* total) {
+  P.ctl->gcount += *total;
+  P.ctl->stg_count = 0u;
 }
 
 // ---------------------------------------------------------------------------------------
 // Phase 0: failure detector, one thread per observer.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_fd(KP P) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t probes = 0, direct = 0, preq = 0, sev = 0, aev = 0, created = 0;
   Tally T;
-  if (i < P.N && P.alive[i] && P.cnt[i] > 0u) {
+  if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
     const uint32_t N = P.N;
     const uint32_t half = perm_half_bits(N);
-    const uint32_t* row = P.view + (size_t)i * N;
+    const uint32_t* row = P.view + lrow(P, i) * N;
     // selectPingMember (FailureDetectorImpl.java:340-349)
     uint32_t ep = P.fd_epoch[i], cur = P.fd_cursor[i];
     PermKey key = perm_key(P.seed, K_FD_PERM, i, ep);
@@ -167,6 +202,18 @@ __device__ __forceinline__ uint32_t range_mask(uint32_t id0, uint32_t lo, uint32
   return m;
 }
 
+// receiver p gets sender entry e this round (a local member id, or XREC | received record)
+__device__ __forceinline__ void register_sender(const KP& P, uint32_t p, uint32_t e) {
+  const uint32_t slot = atomicAdd(&P.in_cnt[p], 1u);
+  if (slot < INCAP) {
+    P.in_list[(size_t)p * INCAP + slot] = e;
+  } else {  // rare: a receiver picked by more than INCAP senders
+    const uint32_t o = atomicAdd(&P.ctl->n_inov, 1u);
+    P.in_ov[2 * o] = p;
+    P.in_ov[2 * o + 1] = e;
+  }
+}
+
 __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* total, uint32_t* lds16) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t x = v;
@@ -196,25 +243,43 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* to
 // is past every window and short of every sweep is idle for all members and is never touched.
 // Spread/sweep bounds use the min/max bit_length(others+1) over alive members (bl_hist).
 __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
-  __shared__ uint32_t s_lo, s_hi, s_blo, s_bhi;
+  __shared__ uint32_t s_lo, s_hi, s_blo, s_bhi, s_first;
   __shared__ uint32_t s_part[16];
   Ctl* c = P.ctl;
+  if (threadIdx.x == 0) s_first = NONE;
+  __syncthreads();
+  {  // the first word (from glo) that may still be held: wlast bounds every slot's infection round
+    const uint32_t hi0 = c->gcount, lo0 = c->glo;
+    const uint32_t lo1 = hi0 - lo0 > P.GC ? hi0 - P.GC : lo0;
+    for (uint32_t wi = (lo1 >> 5) + threadIdx.x; wi < ((hi0 + 31u) >> 5); wi += blockDim.x)
+      if (P.wlast[wi & ((P.GC >> 5) - 1u)] + P.sweepmax >= P.round) {
+        atomicMin(&s_first, wi);
+        break;  // later words of this thread are larger
+      }
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t hi = c->gcount;
     uint32_t lo = c->glo;
-    // word granularity: wlast bounds the infection round of every slot of the word
-    while (lo < hi && (hi - lo > P.GC || P.wlast[(lo & P.gmask) >> 5] + P.sweepmax < P.round)) ++lo;
+    if (hi - lo > P.GC) lo = hi - P.GC;
+    const uint32_t first = s_first == NONE ? hi : (s_first << 5);
+    if (first > lo) lo = first < hi ? first : hi;
     c->glo = lo;
     c->n_alist = 0;
     c->n_inov = 0;
     c->scan_lo = lo;
     c->scan_hi = hi;
     uint32_t blo = 32, bhi = 0;
-    for (uint32_t b = 0; b < 32u; ++b)
-      if (c->bl_hist[b]) {
-        blo = b < blo ? b : blo;
-        bhi = b;
-      }
+    if (P.blx) {  // sharded: bounds over every shard's alive members (all-reduced)
+      bhi = P.blx[0];
+      blo = 32u - P.blx[1];
+    } else {
+      for (uint32_t b = 0; b < 32u; ++b)
+        if (c->bl_hist[b]) {
+          blo = b < blo ? b : blo;
+          bhi = b;
+        }
+    }
     if (blo > bhi) blo = bhi = 1;  // nobody alive: nothing will be scanned anyway
     s_lo = lo;
     s_hi = hi;
@@ -268,12 +333,13 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
-  const uint32_t m = blockIdx.x * 4u + w;
+  const uint32_t m = P.row0 + blockIdx.x * 4u + w;
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
-  const bool active = (m < N) && P.alive[m] && lo < hi;
+  const bool mine = m < P.row0 + P.nloc;
+  const bool active = mine && P.alive[m] && lo < hi;
   const uint32_t W32 = P.GC >> 5;
   uint32_t others = 0, nclear = 0, hdw = 0, winw = 0;
   bool win_l = false;
@@ -282,15 +348,21 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
     others = P.cnt[m];
     const uint32_t sweep = sweep_rounds(P, others);
     const uint32_t spread = spread_rounds(P, others);
-    uint32_t* hbr = P.hb + (size_t)m * W32;
-    uint32_t* wbr = P.wb + (size_t)m * W32;
-    const uint8_t* hdr = P.hd + (size_t)m * P.GC;
+    uint32_t* hbr = P.hb + lrow(P, m) * W32;
+    uint32_t* wbr = P.wb + lrow(P, m) * W32;
+    const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
+    // two-stage software pipeline: the next iteration's list entry and holds word are in flight
+    uint32_t e_n = lane < n_act ? P.act[lane] : 0u;
+    uint32_t word_n = lane < n_act ? hbr[(w_beg + (e_n & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
     for (uint32_t k = lane; k < n_act; k += 64u) {
-      const uint32_t e = P.act[k];
+      const uint32_t e = e_n, word = word_n;
+      if (k + 64u < n_act) {
+        e_n = P.act[k + 64u];
+        word_n = hbr[(w_beg + (e_n & ACT_OFF_MASK)) & (W32 - 1u)];
+      }
       const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
       const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
       const uint32_t ws = wi & (W32 - 1u);
-      const uint32_t word = hbr[ws];
       const uint32_t held = word & range_mask(wi << 5, lo, hi);
       uint32_t clear = 0, win = 0;
       if (held) {
@@ -329,7 +401,7 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   if (any) {
     // selectGossipMembers, wave-cooperative: lanes test 64 consecutive positions of the
     // keyed shuffle, ballot, take the first members in position order.
-    const uint32_t* row = P.view + (size_t)m * N;
+    const uint32_t* row = P.view + lrow(P, m) * N;
     if (others < P.f) {
       for (uint32_t base = 0; base < N; base += 64u) {
         const uint32_t x = base + lane;
@@ -393,18 +465,19 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   const bool reg = __any(win_l) && np > 0u;
   if (reg && lane < np) {
     const uint32_t p = s_peers[w][lane];
-    const uint32_t slot = atomicAdd(&P.in_cnt[p], 1u);
-    if (slot < INCAP) {
-      P.in_list[(size_t)p * INCAP + slot] = m;
-    } else {  // rare: a receiver picked by more than INCAP senders
-      const uint32_t o = atomicAdd(&P.ctl->n_inov, 1u);
-      P.in_ov[2 * o] = p;
-      P.in_ov[2 * o + 1] = m;
+    if (is_local(P, p)) {
+      register_sender(P, p, m);
+    } else {  // the window travels to p's shard (k_gossip_pack / k_gossip_unpack)
+      const uint32_t dst = p / P.nloc;
+      const uint32_t o = atomicAdd(&P.ctl->xg_cnt[dst], 1u);
+      uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + o);
+      e[0] = m;
+      e[1] = p;
     }
   }
   nclear = wave_sum(nclear);
   if (any && lane == 0 && nclear) P.held[m] -= nclear;
-  if (m < N && lane == 0) P.npeers[m] = reg ? np : 0u;
+  if (mine && lane == 0) P.npeers[m] = reg ? np : 0u;
   add_stat(P, ST_G_SCANNED, (any && lane == 0) ? n_act : 0u);
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
@@ -419,17 +492,18 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
 // only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
 // receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
 __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
-  __shared__ uint32_t s_snd[4][64];  // the current chunk of senders (read inside divergent loops)
+  __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
+  __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = blockIdx.x * 4u + (threadIdx.x >> 6);
-  if (p >= P.N) return;  // whole wave
+  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (p >= P.row0 + P.nloc) return;  // whole wave
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
   const uint32_t deg = P.in_cnt[p];
   uint32_t sends = 0, probes = 0, receipts = 0, words = 0;
   if (deg && P.alive[p] && n_act) {  // a stopped transport loses every message
-    uint32_t* hbr = P.hb + (size_t)p * W32;
-    uint32_t* nbr = P.nb + (size_t)p * W32;
+    uint32_t* hbr = P.hb + lrow(P, p) * W32;
+    uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
     for (uint32_t done = 0; done < deg;) {
@@ -457,14 +531,20 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
         if (cdeg == 0) break;  // invariant: in_cnt counts every registration
       }
       done += cdeg;
-      const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sreg, p);
+      // an entry is a local sender's member id, or XREC | index of a window record received
+      // from the sender's shard: [sender, receiver, window words of the round's active list]
+      const uint32_t sid = lane < cdeg ? ((sreg & XREC) ? P.xrecv[(size_t)(sreg & ~XREC) * P.xrec_words] : sreg) : 0u;
+      const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sid, p);
       const unsigned long long reach = __ballot(ok_l);
       uint32_t* snd = s_snd[threadIdx.x >> 6];
       snd[lane] = sreg;
+      s_sid[threadIdx.x >> 6][lane] = sid;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      uint32_t e_n = lane < n_act ? P.act[lane] : 0u;  // next list entry in flight
       for (uint32_t k = lane; k < n_act; k += 64u) {
-        const uint32_t e = P.act[k];
+        const uint32_t e = e_n;
+        if (k + 64u < n_act) e_n = P.act[k + 64u];
         if (((e >> 26) & 3u) == WC_NONE) continue;
         const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
         const uint32_t hw = hbr[ws];
@@ -474,8 +554,11 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
           uint32_t wv[4], mv[4];
 #pragma unroll
           for (uint32_t j = 0; j < 4u; ++j) {  // issue the window loads of 4 senders together
-            mv[j] = q0 + j < cdeg ? snd[q0 + j] : 0u;
-            wv[j] = q0 + j < cdeg ? P.wb[(size_t)mv[j] * W32 + k] : 0u;
+            const uint32_t en = q0 + j < cdeg ? snd[q0 + j] : 0u;
+            mv[j] = q0 + j < cdeg ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
+            wv[j] = q0 + j >= cdeg ? 0u
+                    : (en & XREC) ? P.xrecv[(size_t)(en & ~XREC) * P.xrec_words + 2u + k]
+                                  : P.wb[lrow(P, en) * W32 + k];
           }
 #pragma unroll
           for (uint32_t j = 0; j < 4u; ++j) {
@@ -548,7 +631,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   uint32_t created = 0;
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
     const uint32_t p = P.alist[li];
-    uint32_t* nbr = P.nb + (size_t)p * W32;
+    uint32_t* nbr = P.nb + lrow(P, p) * W32;
     // receipts of p and the table size (>= 2x receipts, 64 .. HCAP)
     uint32_t c = 0;
     for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x)
@@ -575,7 +658,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       if (!bits) continue;
       const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
-      uint4* dp = reinterpret_cast<uint4*>(P.hd + (size_t)p * P.GC + (size_t)ws * 32u);
+      uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
         const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
@@ -592,23 +675,34 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       }
       uint32_t left = bits;
       while (left) {
-        const uint32_t b = (uint32_t)__builtin_ctz(left);
-        left &= left - 1u;
-        const uint2 sr = P.g_sr[ws * 32u + b];
-        uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
-        bool placed = false;
-        for (uint32_t q = 0; q < HPROBE; ++q) {
-          const uint32_t prev = atomicCAS(&s_key[h], NONE, sr.x);
-          if (prev == NONE || prev == sr.x) {
-            atomicMax(&s_val[h], sr.y);
-            placed = true;
-            break;
+        uint2 sr[4];  // four ring-record loads in flight per lane
+        uint32_t nl = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j)
+          if (left) {
+            const uint32_t b = (uint32_t)__builtin_ctz(left);
+            left &= left - 1u;
+            sr[j] = P.g_sr[ws * 32u + b];
+            ++nl;
           }
-          h = (h + 1u) & hm;
-        }
-        if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
-          atomicMax(&P.inbox[(size_t)p * P.N + sr.x], sr.y);
-          s_spill = 1u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+          if (j >= nl) break;
+          uint32_t h = (sr[j].x * 0x9E3779B1u) >> (32u - lg);
+          bool placed = false;
+          for (uint32_t q = 0; q < HPROBE; ++q) {
+            const uint32_t prev = atomicCAS(&s_key[h], NONE, sr[j].x);
+            if (prev == NONE || prev == sr[j].x) {
+              atomicMax(&s_val[h], sr[j].y);
+              placed = true;
+              break;
+            }
+            h = (h + 1u) & hm;
+          }
+          if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
+            atomicMax(&P.inbox[lrow(P, p) * P.N + sr[j].x], sr[j].y);
+            s_spill = 1u;
+          }
         }
       }
     }
@@ -635,7 +729,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           const uint32_t b = (uint32_t)__builtin_ctz(left);
           left &= left - 1u;
           const uint32_t subj = P.g_sr[ws * 32u + b].x;
-          const uint32_t r1 = atomicExch(&P.inbox[(size_t)p * P.N + subj], 0u);
+          const uint32_t r1 = atomicExch(&P.inbox[lrow(P, p) * P.N + subj], 0u);
           if (r1) apply(subj, r1);  // several new gossips about one subject: applied once
         }
       }
@@ -648,6 +742,113 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
+}
+
+// ---------------------------------------------------------------------------------------
+// Cross-shard exchange (world > 1): pack before the host's collective, unpack after it.
+// ---------------------------------------------------------------------------------------
+// locate record g of the send layout: destination shards in rank order, `cnt` records each
+__device__ __forceinline__ bool xrec_locate(const KP& P, const uint32_t* cnt, uint32_t g, uint32_t* dst,
+                                            uint32_t* idx) {
+  for (uint32_t q = 0; q < P.world; ++q) {
+    if (g < cnt[q]) {
+      *dst = q;
+      *idx = g;
+      return true;
+    }
+    g -= cnt[q];
+  }
+  return false;
+}
+
+// window records [sender, receiver, wb row over the active list] for every remote peer
+__global__ void __launch_bounds__(256) k_gossip_pack(KP P, uint32_t n_rec, uint32_t rec_words) {
+  const uint32_t n_act = P.ctl->n_act;
+  const uint32_t W32 = P.GC >> 5;
+  for (uint32_t g = blockIdx.x; g < n_rec; g += gridDim.x) {
+    uint32_t dst, i;
+    if (!xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) break;
+    const uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + i);
+    const uint32_t m = e[0];
+    uint32_t* out = P.xsend + (size_t)g * rec_words;
+    if (threadIdx.x == 0) {
+      out[0] = m;
+      out[1] = e[1];
+    }
+    const uint32_t* wbr = P.wb + lrow(P, m) * W32;
+    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) out[2 + k] = wbr[k];
+  }
+}
+
+// received window records join their receivers' sender lists
+__global__ void k_gossip_unpack(KP P, uint32_t n_rec) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_rec) register_sender(P, P.xrecv[(size_t)g * P.xrec_words + 1], XREC | g);
+}
+
+// SYNC request records [q, receiver, requester's table at phase start]
+__global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
+  const uint32_t N = P.N;
+  for (uint32_t g = blockIdx.x; g < n_rec; g += gridDim.x) {
+    uint32_t dst, i;
+    if (!xrec_locate(P, P.ctl->xs_cnt, g, &dst, &i)) break;
+    const uint32_t q = P.xs_pend[(size_t)dst * 2u * P.nloc + i];
+    uint32_t* out = P.xsend + (size_t)g * (N + 2u);
+    if (threadIdx.x == 0) {
+      out[0] = q;
+      out[1] = P.req_to[q];
+    }
+    const uint32_t* row = P.view + lrow(P, q >> 1) * N;
+    for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) out[2 + c] = row[c];
+  }
+}
+
+// received SYNC requests join their receivers' buckets (k_scan / k_sync_scatter_remote)
+__global__ void k_sync_unpack(KP P, uint32_t n_rec) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_rec) {
+    const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
+    P.rs_ref[rec[0]] = g;
+    atomicAdd(&P.recv_count[rec[1]], 1u);
+  }
+}
+
+__global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_rec) {
+    const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
+    const uint32_t to = rec[1];
+    P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = rec[0];
+  }
+}
+
+// requester side: where the SYNC_ACK of remote request q landed
+__global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.N + 2u)]] = g;
+}
+
+// the all-reduce MAX operand of a round: per-word gossip liveness + the bit_length bounds
+__global__ void k_round_max_pack(KP P) {
+  const uint32_t W32 = P.GC >> 5;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W32; i += gridDim.x * blockDim.x)
+    P.xsend[i] = P.wlast[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t blo = 32, bhi = 0;
+    for (uint32_t b = 0; b < 32u; ++b)
+      if (P.ctl->bl_hist[b]) {
+        blo = b < blo ? b : blo;
+        bhi = b;
+      }
+    P.xsend[W32] = bhi;
+    P.xsend[W32 + 1] = 32u - blo;  // 0 when this shard has no alive member
+  }
+}
+
+__global__ void k_round_max_unpack(KP P) {
+  const uint32_t W32 = P.GC >> 5;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W32; i += gridDim.x * blockDim.x)
+    P.wlast[i] = P.xsend[i];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -668,19 +869,20 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   const uint32_t n = P.ctl->due_count;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t j = P.due[k];
-    uint32_t* col = P.dl + (size_t)j * P.N;
+    uint32_t* col = P.dl + (size_t)j * P.nloc;
     uint32_t mn = NONE;
-    for (uint32_t i = threadIdx.x; i < P.N; i += blockDim.x) {
-      const uint32_t v = col[i];
+    for (uint32_t li = threadIdx.x; li < P.nloc; li += blockDim.x) {
+      const uint32_t i = P.row0 + li;
+      const uint32_t v = col[li];
       if (v == 0u) continue;
       if (!P.alive[i]) {
-        col[i] = 0u;
+        col[li] = 0u;
         continue;
       }
       const uint32_t dl = v - 1u;
       if (dl <= P.period) {  // onSuspicionTimeout (MembershipProtocolImpl.java:637-647)
-        col[i] = 0u;
-        if (P.view[(size_t)i * P.N + j] != 0u) {
+        col[li] = 0u;
+        if (P.view[(size_t)li * P.N + j] != 0u) {
           ++fired;
           apply_record(P, i, j, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
         }
@@ -703,7 +905,7 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     __syncthreads();
   }
   add_stat(P, ST_SUSP_TIMEOUTS, fired);
-  add_stat(P, ST_SWEEP_CELLS, threadIdx.x == 0 ? ((n + gridDim.x - 1u - blockIdx.x) / gridDim.x) * P.N : 0u);
+  add_stat(P, ST_SWEEP_CELLS, threadIdx.x == 0 ? ((n + gridDim.x - 1u - blockIdx.x) / gridDim.x) * P.nloc : 0u);
   flush_tally(P, T);
 }
 
@@ -713,7 +915,7 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
 // selectSyncAddress (MembershipProtocolImpl.java:416-427): uniform over seeds U others.
 __device__ uint32_t select_sync_address(const KP& P, uint32_t i) {
   const uint32_t N = P.N;
-  const uint32_t* row = P.view + (size_t)i * N;
+  const uint32_t* row = P.view + lrow(P, i) * N;
   uint32_t count = P.cnt[i];
   for (uint32_t s = 0; s < P.n_seeds && s < N; ++s)
     if (s != i && row[s] == 0u) ++count;
@@ -731,9 +933,9 @@ __device__ uint32_t select_sync_address(const KP& P, uint32_t i) {
 }
 
 __global__ void k_sync_select(KP P) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
-  if (i < P.N) {
+  if (i < P.row0 + P.nloc) {
     P.req_to[2 * i] = NONE;
     P.req_to[2 * i + 1] = NONE;
     P.req_stage[2 * i] = NONE;
@@ -750,6 +952,13 @@ __global__ void k_sync_select(KP P) {
         P.req_to[2 * i + k] = to[k];
         if (!delivered(P, K_SYNC, i, to[k], k, P.tick)) continue;
         ++dlv;
+        if (!is_local(P, to[k])) {  // the table travels to the receiver's shard (k_sync_pack)
+          const uint32_t dst = to[k] / P.nloc;
+          const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
+          P.xs_pend[(size_t)dst * 2u * P.nloc + o] = 2 * i + k;
+          P.req_stage[2 * i + k] = REMOTE;
+          continue;
+        }
         const uint32_t slot = atomicAdd(&P.ctl->stage_count, 1u);
         if (slot >= P.scap) {
           atomicOr(&P.ctl->overflow, OV_SYNC);
@@ -772,11 +981,11 @@ __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
   const uint32_t nv = P.N / 4u;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t from = P.stage_req[k] >> 1;
-    const uint4* src = reinterpret_cast<const uint4*>(P.view + (size_t)from * P.N);
+    const uint4* src = reinterpret_cast<const uint4*>(P.view + lrow(P, from) * P.N);
     uint4* dst = reinterpret_cast<uint4*>(P.stage_sync + (size_t)k * P.N);
     for (uint32_t c = threadIdx.x; c < nv; c += blockDim.x) dst[c] = src[c];
     for (uint32_t c = nv * 4u + threadIdx.x; c < P.N; c += blockDim.x)
-      P.stage_sync[(size_t)k * P.N + c] = P.view[(size_t)from * P.N + c];
+      P.stage_sync[(size_t)k * P.N + c] = P.view[lrow(P, from) * P.N + c];
   }
 }
 
@@ -807,8 +1016,8 @@ __global__ void __launch_bounds__(1024) k_scan(KP P) {
 }
 
 __global__ void k_sync_scatter(KP P) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < 2u * P.N && P.req_stage[q] != NONE) {
+  const uint32_t q = 2u * P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < 2u * (P.row0 + P.nloc) && P.req_stage[q] != NONE && P.req_stage[q] != REMOTE) {
     const uint32_t to = P.req_to[q];
     const uint32_t pos = P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u);
     P.bucket[pos] = q;
@@ -844,7 +1053,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
                                           uint32_t attempt, uint32_t snap, uint32_t& seq, Tally& T, uint32_t& created,
                                           uint32_t* lds4) {
   const uint32_t N = P.N;
-  uint32_t* row = P.view + (size_t)obs * N;
+  uint32_t* row = P.view + lrow(P, obs) * N;
   // 4 cells per thread (16-B loads) when rows are 16-B aligned, else 1; cells that the
   // incoming record does not override (the common case) never enter updateMembership.
   const uint32_t per = (N & 3u) == 0u ? 4u : 1u;
@@ -894,8 +1103,8 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
-  const uint32_t j = blockIdx.x;
-  if (j >= P.N) return;
+  const uint32_t j = P.row0 + blockIdx.x;
+  if (j >= P.row0 + P.nloc) return;
   uint32_t cntj = P.recv_count[j];
   if (cntj == 0u) return;
   if (cntj > (uint32_t)BUCKET_MAX) {
@@ -923,9 +1132,22 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   const uint32_t snap = P.cnt[j];
   for (uint32_t k = 0; k < cntj; ++k) {
     const uint32_t q = s_list[k];
-    const uint32_t slot = P.req_stage[q];
-    merge_row(P, j, P.stage_sync + (size_t)slot * P.N, P.stage_ack + (size_t)slot * P.N, q, snap, seq, T, created,
-              s_lds4);
+    const uint32_t* src;
+    uint32_t* ack;
+    if (is_local(P, q >> 1)) {
+      const uint32_t slot = P.req_stage[q];
+      src = P.stage_sync + (size_t)slot * P.N;
+      ack = P.stage_ack + (size_t)slot * P.N;
+    } else {  // request from another shard: payload in the received record, ack into the same
+      const size_t g = (size_t)P.rs_ref[q] * (P.N + 2u);  // position of the send buffer
+      src = P.xrecv + g + 2;
+      ack = P.xsend + g + 2;
+      if (threadIdx.x == 0) {
+        P.xsend[g] = q;
+        P.xsend[g + 1] = j;
+      }
+    }
+    merge_row(P, j, src, ack, q, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
   add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * P.N : 0u);
@@ -936,8 +1158,8 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
 // onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
 __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   __shared__ uint32_t s_lds4[4];
-  const uint32_t i = blockIdx.x;
-  if (i >= P.N) return;
+  const uint32_t i = P.row0 + blockIdx.x;
+  if (i >= P.row0 + P.nloc) return;
   uint32_t q[2], to[2], n = 0;
   for (uint32_t k = 0; k < 2; ++k) {
     const uint32_t qq = 2 * i + k;
@@ -964,7 +1186,9 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t slot = P.req_stage[q[k]];
     const uint32_t attempt = (to[k] << 1) | (q[k] & 1u);
-    merge_row(P, i, P.stage_ack + (size_t)slot * P.N, nullptr, attempt, snap, seq, T, created, s_lds4);
+    const uint32_t* src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[q[k]] * (P.N + 2u) + 2
+                                         : P.stage_ack + (size_t)slot * P.N;
+    merge_row(P, i, src, nullptr, attempt, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
@@ -976,16 +1200,17 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
 // ---------------------------------------------------------------------------------------
 // Observability.
 // ---------------------------------------------------------------------------------------
-__global__ void k_digest(const uint32_t* view, const uint32_t* dl, uint32_t N, unsigned long long* out) {
+__global__ void k_digest(const uint32_t* view, const uint32_t* dl, uint32_t N, uint32_t row0, uint32_t nloc,
+                         unsigned long long* out) {
   const uint64_t K = 0x9E3779B97F4A7C15ull;
   unsigned long long a = 0, b = 0;
-  const size_t total = (size_t)N * N;
+  const size_t total = (size_t)nloc * N;
   for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t v = view[x];
-    if (v) a += fmix64((uint64_t)x * K + v);
-    const uint32_t d = dl[x];  // x = subject * N + observer
+    const uint32_t v = view[x];  // x = local observer * N + subject
+    if (v) a += fmix64(((uint64_t)row0 * N + x) * K + v);
+    const uint32_t d = dl[x];  // x = subject * nloc + local observer
     if (d) {
-      const uint64_t subj = x / N, obs = x % N;
+      const uint64_t subj = x / nloc, obs = row0 + x % nloc;
       b += fmix64((obs * N + subj) * K + d);
     }
   }

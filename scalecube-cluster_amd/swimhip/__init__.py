@@ -5,6 +5,7 @@ this package is the host-side mirror of the reference's config/event surface.
 """
 from .config import ClusterConfig, FailureDetectorConfig, GossipConfig, MembershipConfig, to_swim_config
 from .cluster import MembershipEvent, MembershipRecord, SwimCluster, SwimError
+from .sharded import ShardedSwimCluster
 from . import _native as native
 from . import cluster_math
 
@@ -15,6 +16,7 @@ __all__ = [
     "MembershipConfig",
     "MembershipEvent",
     "MembershipRecord",
+    "ShardedSwimCluster",
     "SwimCluster",
     "SwimError",
     "cluster_math",

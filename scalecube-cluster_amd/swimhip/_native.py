@@ -53,6 +53,8 @@ class SwimConfig(ctypes.Structure):
         ("dirty_capacity", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
         ("device", ctypes.c_int32),
+        ("shard_rank", ctypes.c_uint32),
+        ("shard_world", ctypes.c_uint32),
     ]
 
 
@@ -105,6 +107,23 @@ class SwimStats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in STAT_FIELDS]
 
 
+MAX_WORLD = 64
+X_DONE, X_ALLGATHER, X_ALLTOALLV, X_ALLREDUCE_MAX = 0, 1, 2, 3
+
+
+class SwimXchg(ctypes.Structure):
+    """swim_xchg (include/swimhip.h): one cross-shard exchange of a sharded period."""
+
+    _fields_ = [
+        ("op", ctypes.c_uint32),
+        ("world", ctypes.c_uint32),
+        ("send_words", ctypes.c_uint64),
+        ("send_counts", ctypes.c_uint64 * MAX_WORLD),
+        ("recv_counts", ctypes.c_uint64 * MAX_WORLD),
+        ("recv_stride", ctypes.c_uint64),
+    ]
+
+
 # (name, restype, argtypes) for every entry point of include/swimhip.h
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -144,6 +163,9 @@ SWIM_ONLY = [
     ("swim_debug_member_state", _I, [_P, _pU32, _U32]),
     ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),
     ("swim_kernel_time_reset", _I, [_P, _I]),
+    ("swim_shard_buffer_words", _I, [_P, _pU64, _pU64]),
+    ("swim_shard_attach", _I, [_P, _P, _P]),
+    ("swim_shard_step", _I, [_P, ctypes.POINTER(SwimXchg)]),
 ]
 
 

@@ -232,7 +232,8 @@ class ClusterConfig(_Cfg):
 
 
 def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_capacity: int = 0,
-                   event_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0):
+                   event_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0,
+                   shard_rank: int = 0, shard_world: int = 1):
     """Marshal a ClusterConfig into the C struct of include/swimhip.h."""
     from ._native import SwimConfig
 
@@ -261,4 +262,6 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
     c.dirty_capacity = dirty_capacity
     c.flags = 0
     c.device = device
+    c.shard_rank = shard_rank
+    c.shard_world = shard_world
     return c

@@ -1,0 +1,166 @@
+"""ShardedSwimCluster — one simulated cluster row-sharded over several GPUs / processes.
+
+Rank r of a torch.distributed group owns observers [r*N/W, (r+1)*N/W): their membership tables,
+suspicion deadlines, gossip holdings and protocol cursors. Each rank drives its
+libswimhip.so handle with swim_shard_step and performs the exchanges the library describes on
+the group: all-gather of each phase's new gossips (ids stay identical on every shard), all-reduce
+MAX of per-word gossip liveness, all-to-all-v of sender windows bound for remote receivers and
+of SYNC / SYNC_ACK tables of cross-shard pairs. On ROCm the "nccl" backend is RCCL over xGMI and
+the buffers stay in HBM; with "gloo" (tests on one GPU, or CPU rehearsal of the protocol) they are
+staged through host memory. Results equal the unsharded SwimCluster's bit for bit.
+
+Every rank must make the same calls in the same order (fault injection, stepping and the
+observation accessors, which are collective).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+from .cluster import MembershipEvent, SwimCluster
+
+
+class ShardedSwimCluster(SwimCluster):
+    def __init__(self, config, n_members: int, seed: int = 0, *, group=None, device: int = 0, **kw):
+        import torch
+        import torch.distributed as dist
+
+        self._dist = dist
+        self._torch = torch
+        self._group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self._gloo = dist.get_backend(group) == "gloo"
+        super().__init__(config, n_members, seed, device=device, _shard=(self.rank, self.world), **kw)
+        self.nloc = self.n // self.world
+        self.row0 = self.rank * self.nloc
+        sw, rw = ctypes.c_uint64(), ctypes.c_uint64()
+        self._call("shard_buffer_words", self._h, ctypes.byref(sw), ctypes.byref(rw))
+        dev = torch.device("cuda", device)
+        self._send = torch.empty(max(1, sw.value), dtype=torch.int32, device=dev)
+        self._recv = torch.empty(max(1, rw.value), dtype=torch.int32, device=dev)
+        self._call("shard_attach", self._h, ctypes.c_void_p(self._send.data_ptr()),
+                   ctypes.c_void_p(self._recv.data_ptr()))
+        self._x = nat.SwimXchg()
+
+    # -- collectives ---------------------------------------------------------------------
+    def _all_gather_ints(self, vals):
+        t = self._torch.tensor(vals, dtype=self._torch.int64)
+        if not self._gloo:
+            t = t.to(self._send.device)
+        out = [self._torch.empty_like(t) for _ in range(self.world)]
+        self._dist.all_gather(out, t, group=self._group)
+        return [o.cpu().tolist() for o in out]
+
+    def _exchange(self):
+        torch, dist, x, W = self._torch, self._dist, self._x, self.world
+        if x.op == nat.X_ALLREDUCE_MAX:
+            n = int(x.send_words)
+            buf = self._send[:n]
+            if self._gloo:
+                h = buf.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self._group)
+                buf.copy_(h)
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=self._group)
+        elif x.op == nat.X_ALLGATHER:
+            counts = [c[0] for c in self._all_gather_ints([int(x.send_words)])]
+            m = max(counts)
+            if m:
+                src = self._send[:m]
+                dst = self._recv[:W * m]
+                if self._gloo:
+                    parts = [torch.empty(m, dtype=torch.int32) for _ in range(W)]
+                    dist.all_gather(parts, src.cpu(), group=self._group)
+                    dst.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(dst, src, group=self._group)
+            for q in range(W):
+                x.recv_counts[q] = counts[q]
+            x.recv_stride = m
+        elif x.op == nat.X_ALLTOALLV:
+            sc = [int(x.send_counts[q]) for q in range(W)]
+            allc = self._all_gather_ints(sc)  # allc[q][r] = words rank q sends to rank r
+            rc = [allc[q][self.rank] for q in range(W)]
+            si, ri = sum(sc), sum(rc)
+            if max(max(row) for row in allc):
+                src, dst = self._send[:si], self._recv[:ri]
+                if self._gloo:
+                    hd = torch.empty(ri, dtype=torch.int32)
+                    dist.all_to_all_single(hd, src.cpu(), rc, sc, group=self._group)
+                    dst.copy_(hd)
+                else:
+                    dist.all_to_all_single(dst, src, rc, sc, group=self._group)
+            for q in range(W):
+                x.recv_counts[q] = rc[q]
+        else:
+            raise RuntimeError(f"unknown exchange op {x.op}")
+        if self._send.is_cuda:  # the library resumes on its own stream
+            torch.cuda.synchronize(self._send.device)
+
+    def step(self, periods: int = 1):
+        for _ in range(int(periods)):
+            while True:
+                self._call("shard_step", self._h, ctypes.byref(self._x))
+                if self._x.op == nat.X_DONE:
+                    break
+                self._exchange()
+
+    def step_async(self, periods: int = 1):
+        self.step(periods)
+
+    def sync(self):
+        self._call("sync", self._h)
+
+    # -- collective observation ------------------------------------------------------------
+    def _owner(self, i):
+        return int(i) // self.nloc
+
+    def _bcast_row(self, i, reader):
+        obj = [reader(i) if self._owner(i) == self.rank else None]
+        self._dist.broadcast_object_list(obj, src=self._owner(i), group=self._group)
+        return obj[0]
+
+    def view(self, observer: int) -> np.ndarray:
+        return self._bcast_row(observer, lambda i: SwimCluster.view(self, i))
+
+    def deadlines(self, observer: int) -> np.ndarray:
+        return self._bcast_row(observer, lambda i: SwimCluster.deadlines(self, i))
+
+    def _gather_objects(self, obj):
+        out = [None] * self.world
+        self._dist.all_gather_object(out, obj, group=self._group)
+        return out
+
+    def digest(self):
+        parts = self._gather_objects(SwimCluster.digest(self))
+        m = (1 << 64) - 1
+        return sum(p[0] for p in parts) & m, sum(p[1] for p in parts) & m
+
+    def presence(self):
+        parts = self._gather_objects(SwimCluster.presence(self))
+        pres = np.sum([p[0] for p in parts], axis=0).astype(np.uint32)
+        last = np.max([p[1] for p in parts], axis=0).astype(np.uint32)
+        return pres, last
+
+    _SAME = ("period", "live_gossip_slots")
+
+    def stats(self) -> dict:
+        parts = self._gather_objects(SwimCluster.stats(self))
+        out = {}
+        for k in parts[0]:
+            if k in self._SAME:
+                out[k] = parts[0][k]
+            elif k == "overflow":
+                out[k] = int(np.bitwise_or.reduce([p[k] for p in parts]))
+            else:
+                out[k] = sum(p[k] for p in parts)
+        return out
+
+    def events(self, cap: int = 1 << 20):
+        mine = [tuple(e.__dict__.values()) for e in SwimCluster.events(self, cap)]
+        allev = [MembershipEvent(*t) for part in self._gather_objects(mine) for t in part]
+        allev.sort(key=lambda e: (e.period, e.observer, e.phase, e.member, e.type))
+        return allev

@@ -1,0 +1,97 @@
+"""Observer-row sharding: the host exchange protocol on CPU (gloo, 2 ranks), and
+the sharded HIP path against the unsharded one, bit for bit, on one GPU (2 ranks, gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from swimhip import _native as nat
+from swimhip.sharded import ShardedSwimCluster
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _exchange_worker(rank, world, port):
+    """Drive ShardedSwimCluster._exchange with host buffers and check every op's semantics."""
+    _init(rank, world, port)
+    try:
+        c = object.__new__(ShardedSwimCluster)
+        c._dist, c._torch, c._group = dist, torch, None
+        c.rank, c.world, c._gloo = rank, world, True
+        c._send = torch.zeros(64, dtype=torch.int32)
+        c._recv = torch.zeros(256, dtype=torch.int32)
+        x = c._x = nat.SwimXchg()
+        # all-gather of unequal contributions, padded to the max
+        n = 2 + 3 * rank
+        c._send[:n] = torch.arange(n, dtype=torch.int32) + 100 * rank
+        x.op, x.send_words = nat.X_ALLGATHER, n
+        c._exchange()
+        m = int(x.recv_stride)
+        assert m == 2 + 3 * (world - 1)
+        for q in range(world):
+            cnt = int(x.recv_counts[q])
+            assert cnt == 2 + 3 * q
+            assert c._recv[q * m:q * m + cnt].tolist() == [100 * q + i for i in range(cnt)]
+        # all-to-all-v: rank r sends (q + 1) words of value 10 r + q to rank q
+        x.op = nat.X_ALLTOALLV
+        off = 0
+        for q in range(world):
+            x.send_counts[q] = q + 1
+            c._send[off:off + q + 1] = 10 * rank + q
+            off += q + 1
+        c._exchange()
+        got, off = [], 0
+        for q in range(world):
+            cnt = int(x.recv_counts[q])
+            assert cnt == rank + 1
+            got.append(c._recv[off:off + cnt].tolist())
+            off += cnt
+        assert got == [[10 * q + rank] * (rank + 1) for q in range(world)]
+        # element-wise max
+        c._send[:4] = torch.tensor([rank, 5 - rank, 7, rank * 3], dtype=torch.int32)
+        x.op, x.send_words = nat.X_ALLREDUCE_MAX, 4
+        c._exchange()
+        assert c._send[:4].tolist() == [world - 1, 5, 7, 3 * (world - 1)]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_protocol_gloo_cpu():
+    mp.spawn(_exchange_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _parity_worker(rank, world, port, names):
+    import scenarios
+    from swimhip import SwimCluster
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        for name in names:
+            scenarios.run_pair(name, lambda *a, **k: ShardedSwimCluster(*a, **k), SwimCluster)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("names", [["c1_local32_crash", "local48_links"],
+                                   ["lan256_loss5_crash3", "local128_partition_heal"],
+                                   ["test64_long_partition_rejoin"]])
+def test_two_shards_match_unsharded(names):
+    """2 ranks sharing cuda:0, gloo exchanges: views, deadlines, events, counters, digests and
+    presence equal the unsharded handle's after every period."""
+    mp.spawn(_parity_worker, args=(2, _free_port(), names), nprocs=2, join=True)
