@@ -69,7 +69,7 @@ def kernel_bytes(name, d, n):
     if name == "k_sync_snapshot":  # copy the sender's row into the SYNC payload
         return 8 * d["merge_cells"]
     if name == "k_gossip_select":  # holds word per active word, 64 B of infection rounds per MIXED word,
-        return 4 * d["gossip_scanned"] + 64 * d["gossip_hd_words"] + 4 * d["gossip_window_words"]  # + window
+        return 4 * d["gossip_scanned"] + 32 * d["gossip_hd_words"] + 4 * d["gossip_window_words"]  # + window
     if name == "k_gossip_pull":  # receiver holds word r/w + receipts word per active window word, one
         return 12 * d["gossip_pull_words"] + 4 * d["gossip_probes"]  # sender window word per probe
     if name == "k_gossip_apply":  # per receipt: infection round (2 B) + ring record (8 B)
@@ -79,6 +79,19 @@ def kernel_bytes(name, d, n):
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
         return 24 * d["fd_probes"]
     return 0
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/gpu_pmc.sh: separate
+    FETCH_SIZE and WRITE_SIZE rocprofv3 passes over the same workload; FETCH_SIZE doubled per the
+    gfx950 note in MI355X_MICROARCH.md), or None when no summary covers it."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    k = d.get(kernel)
+    return None if k is None else k["fetch_bytes_x2"] + k["write_bytes"]
 
 
 def log(msg):
@@ -167,6 +180,8 @@ def main():
                     help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for --gpus > 1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -177,8 +192,9 @@ def main():
         import torch
         import torch.distributed as tdist
 
+        local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(args.backend)
         dist = tdist
 
     def barrier():
@@ -214,7 +230,7 @@ def main():
     if dist is not None:
         import torch
 
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     s1 = c.stats()
@@ -265,7 +281,7 @@ def main():
                    "gossip_ring_slots": w["gcap"]},
         "periods_to_dead": periods_to_dead,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom),
                      "bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3, "launches": launches},
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",

@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include <hipcub/device/device_radix_sort.hpp>
+
 #include "swim_kernels.hip"
 
 using namespace swim;
@@ -47,6 +49,11 @@ struct swim_handle {
   uint64_t xsend_words = 0, xrecv_words = 0;
   uint32_t* d_xcounts = nullptr;
   uint32_t* d_blx = nullptr;
+  // gossip commits: sort keys/values (in, out) and radix-sort scratch
+  unsigned long long* ck[2] = {nullptr, nullptr};
+  unsigned long long* cv[2] = {nullptr, nullptr};
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   unsigned long long* d_digest = nullptr;
   std::vector<void*> allocs;
   std::string err;
@@ -73,6 +80,15 @@ int fail(swim_handle* h, int code, const std::string& what) {
   do {                                                                                             \
     hipError_t e_ = (expr);                                                                        \
     if (e_ != hipSuccess) return fail((h), SWIM_EHIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+#define HIPC_RC(h, rcp, expr)                                                                      \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) {                                                                        \
+      *(rcp) = fail((h), SWIM_EHIP, std::string(#expr ": ") + hipGetErrorString(e_));              \
+      return false;                                                                                \
+    }                                                                                              \
   } while (0)
 
 template <typename T>
@@ -181,22 +197,38 @@ void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
   x->world = world;
 }
 
-// Commit the phase's staged gossips. Unsharded: in place, no host round trip. Sharded: the
-// host all-gathers every shard's stage (returns true: exchange pending).
+// Sort the n gossips staged in h->ck[0] / h->cv[0] by (subject, record) and commit them.
+int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
+  hipStream_t s = h->stream;
+  if (n) {
+    size_t tb = h->sort_tmp_bytes;
+    const int end_bit = 32 + (int)bitlen(h->N);
+    HIPC(h, hipcub::DeviceRadixSort::SortPairs(h->sort_tmp, tb, h->ck[0], h->ck[1], h->cv[0], h->cv[1], (int)n, 0,
+                                                end_bit, s));
+    timed(h, 7, [&] {
+      hipLaunchKernelGGL(k_gossip_commit, dim3(std::min<uint32_t>(blocks_for(n, 256), 2048)), dim3(256), 0, s, P,
+                         h->ck[1], h->cv[1], n);
+    });
+  }
+  hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, n);
+  return SWIM_OK;
+}
+
+// Commit the phase's staged gossips. Unsharded: in place. Sharded: the host all-gathers every
+// shard's stage first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
   hipStream_t s = h->stream;
+  uint32_t n = 0;
+  HIPC_RC(h, rc, hipMemcpyAsync(&n, &P.ctl->stg_count, 4, hipMemcpyDeviceToHost, s));
+  HIPC_RC(h, rc, hipStreamSynchronize(s));
+  n = std::min(n, P.stg_cap);  // beyond: OV_GOSSIP already raised
   if (h->world == 1) {
-    timed(h, 7, [&] {
-      hipLaunchKernelGGL(k_gossip_commit, dim3(256), dim3(256), 0, s, P, P.stg, &P.ctl->stg_count, 0u);
-    });
-    timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, &P.ctl->stg_count); });
+    if (n) hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(n, 256)), dim3(256), 0, s, P.stg, n, 0u, h->ck[0], h->cv[0]);
+    *rc = commit_sorted(h, P, n);
     return false;
   }
-  Ctl c;
-  if ((*rc = read_ctl(h, &c))) return false;
-  const uint32_t n = std::min(c.stg_count, P.stg_cap);
   if (n) (void)hipMemcpyAsync(h->xsend, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
-  (void)hipStreamSynchronize(s);
+  HIPC_RC(h, rc, hipStreamSynchronize(s));
   xchg_clear(x, SWIM_X_ALLGATHER, h->world);
   x->send_words = 4ull * n;
   return true;
@@ -204,21 +236,16 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
 
 int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   hipStream_t s = h->stream;
-  uint32_t counts[SWIM_MAX_WORLD], total = 0, base[SWIM_MAX_WORLD];
-  for (uint32_t q = 0; q < h->world; ++q) {
-    counts[q] = (uint32_t)(x->recv_counts[q] / 4);
-    base[q] = total;
-    total += counts[q];
-  }
-  counts[h->world] = total;  // world < SWIM_MAX_WORLD
-  HIPC(h, hipMemcpyAsync(h->d_xcounts, counts, 4ull * (h->world + 1), hipMemcpyHostToDevice, s));
   const uint32_t* xr = reinterpret_cast<const uint32_t*>(h->xrecv);
-  for (uint32_t q = 0; q < h->world; ++q)
-    if (counts[q])
-      hipLaunchKernelGGL(k_gossip_commit, dim3(blocks_for(counts[q], 256)), dim3(256), 0, s, P,
-                         reinterpret_cast<const uint4*>(xr + q * x->recv_stride), h->d_xcounts + q, base[q]);
-  hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, h->d_xcounts + h->world);
-  return SWIM_OK;
+  uint32_t total = 0;
+  for (uint32_t q = 0; q < h->world; ++q) {
+    const uint32_t c = (uint32_t)(x->recv_counts[q] / 4);
+    if (c)
+      hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(c, 256)), dim3(256), 0, s,
+                         reinterpret_cast<const uint4*>(xr + q * x->recv_stride), c, total, h->ck[0], h->cv[0]);
+    total += c;
+  }
+  return commit_sorted(h, P, total);
 }
 
 // Runs the current period from h->pc. Returns SWIM_OK with x->op = SWIM_X_DONE at the end of
@@ -517,6 +544,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.hb, NL * (h->GC / 32));
   ALLOC(P.wb, NL * (h->GC / 32));
   ALLOC(P.hd, NL * h->GC);
+  ALLOC(P.mmin, NL * (h->GC / 32));
+  ALLOC(P.mmax, NL * (h->GC / 32));
   ALLOC(P.colmin, N);
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
@@ -534,18 +563,33 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_hash, h->GC);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
+  ALLOC(P.nsum, NL * NSUM);
   ALLOC(P.stg, P.stg_cap);
   ALLOC(P.xg_pend, 2ull * world * NL * c.gossip_fanout);
   ALLOC(P.xs_pend, 2ull * world * NL);
   ALLOC(P.rs_ref, 2ull * N);
   ALLOC(P.ack_ref, 2ull * N);
   ALLOC(h->d_xcounts, SWIM_MAX_WORLD + 1);
+  ALLOC(P.runw, h->GC / 32);
+  for (int k = 0; k < 2; ++k) {
+    ALLOC(h->ck[k], (size_t)P.stg_cap * world);
+    ALLOC(h->cv[k], (size_t)P.stg_cap * world);
+  }
+  if (rc == SWIM_OK) {
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, h->ck[0], h->ck[1], h->cv[0], h->cv[1],
+                                             (int)(P.stg_cap * world), 0, 64, h->stream);
+    h->sort_tmp_bytes = tb;
+    char* tmp = nullptr;
+    rc = dalloc(h, &tmp, tb);
+    h->sort_tmp = tmp;
+  }
   ALLOC(h->d_blx, 2);
   ALLOC(P.wlast, h->GC / 32);
   ALLOC(P.in_cnt, N);
   ALLOC(P.in_list, (size_t)N * INCAP);
   ALLOC(P.in_ov, 2ull * N * c.gossip_fanout);
-  ALLOC(P.alist, N);
+  ALLOC(P.alist, 2ull * N);
   ALLOC(P.act, h->GC / 32);
   ALLOC(P.held, N);
   ALLOC(P.due, N);
@@ -601,6 +645,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   {  // every member of this shard starts with others = N - 1
     const uint32_t all = P.nloc;

@@ -116,10 +116,13 @@ struct KP {
   uint32_t* colmin;
   uint32_t* inbox;
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
+  uint8_t* mmin;  // [N][GC/32] oldest / newest infection round (mod 2^8) the member holds in the
+  uint8_t* mmax;  //            word (valid while it holds any): most MIXED words resolve per member
   uint8_t* hd;   // [N][GC] infection round mod 2^8, valid where the hb bit is set (exact: an
                  // alive member's held entry is at most sweep+1 <= sweepmax rounds old, < 2^8)
   uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select (act-indexed)
   uint32_t* nb;  // [N][GC/32] first receipts of the round found by k_gossip_pull (act-indexed)
+  uint32_t* nsum;  // [N][NSUM] bit k: nb[k] != 0 this round (written for receivers with receipts)
   uint32_t* cnt;
   int32_t* cnt_delta;
   uint8_t* alive;
@@ -132,6 +135,8 @@ struct KP {
   uint32_t* peers;   // [N][f] gossip peers chosen this round
   uint32_t* npeers;  // [N]
   uint2* g_sr;        // [GC] (subject, packed record) of each gossip
+  uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
+                      // by (subject, record), so within a run records ascend)
   uint32_t* g_hash;
   uint32_t* g_create;
   uint32_t* wlast;    // [GC/32] max infection round of any holder over the word's slots
@@ -177,6 +182,7 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t REMOTE = 0xFFFFFFFEu;   // req_stage of a request staged on another shard
 constexpr uint32_t XREC = 0x80000000u;     // in_list entry: a received window record, not a local row
 constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
+constexpr uint32_t NSUM = 1024;  // receipt-summary words per receiver: active lists up to 32,768 words
 
 // partition cut and directed link blocks only (no liveness, no loss draw)
 __device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t dst) {

@@ -57,36 +57,57 @@ __global__ void k_crash(KP P, uint32_t c) {
   }
 }
 
-// Second half of emit_gossip: `count` staged gossips at `ents` get ids gcount + base + i (every
-// shard commits the same entries in the same order, so the ring stays replicated); the origin's
-// shard marks it held with infectionPeriod = create_round.
-__global__ void k_gossip_commit(KP P, const uint4* ents, const uint32_t* count, uint32_t base) {
-  const uint32_t n = *count;
-  const uint32_t g0 = P.ctl->gcount + base;
+// Second half of emit_gossip, step 1: sort keys of the phase's gossips, (subject, record) and
+// (origin, id hash). Sorting only permutes ring slots, which nothing observable depends on.
+__global__ void k_stage_keys(const uint4* ents, uint32_t n, uint32_t out_off, unsigned long long* keys,
+                             unsigned long long* vals) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint4 e = ents[i];
+    keys[out_off + i] = ((unsigned long long)e.y << 32) | e.z;
+    vals[out_off + i] = ((unsigned long long)e.x << 32) | e.w;
+  }
+}
+
+// Step 2: the n sorted gossips get ids gcount + i (every shard commits the same sorted batch, so
+// the ring stays replicated), runs of one subject are marked in runw, and the origin's shard
+// marks each gossip held with infectionPeriod = create_round.
+__global__ void k_gossip_commit(KP P, const unsigned long long* keys, const unsigned long long* vals, uint32_t n) {
+  const uint32_t g0 = P.ctl->gcount;
   const uint32_t W32 = P.GC >> 5;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint4 e = ents[i];
+    const unsigned long long k = keys[i], v = vals[i];
+    const uint32_t subject = (uint32_t)(k >> 32), record = (uint32_t)k;
+    const uint32_t origin = (uint32_t)(v >> 32), hash = (uint32_t)v;
     const uint32_t id = g0 + i;
     const uint32_t s = id & P.gmask;
     // the live id range must stay below GC - 64 slots so bitmap words never alias across the
     // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
     if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
-    P.g_sr[s] = make_uint2(e.y, e.z);
-    P.g_hash[s] = e.w;
+    P.g_sr[s] = make_uint2(subject, record);
+    P.g_hash[s] = hash;
     P.g_create[s] = P.create_round;
+    const bool start = i == 0 || (uint32_t)(keys[i - 1] >> 32) != subject;
+    if (start)
+      atomicOr(&P.runw[s >> 5], 1u << (s & 31u));
+    else
+      atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
     // a reused word's stale maximum is older than any live creation round, so max() resets it
     if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
-    if (is_local(P, e.x)) {
-      P.hd[lrow(P, e.x) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
-      const uint32_t old = atomicOr(&P.hb[lrow(P, e.x) * W32 + (s >> 5)], 1u << (s & 31u));
-      if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[e.x], 1u);
+    if (is_local(P, origin)) {
+      P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
+      const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
+      if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
+      // newest/oldest infection round the origin holds in the word (same value for the batch)
+      P.mmax[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
+      if (old == 0u) P.mmin[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
     }
   }
 }
 
-// after the commit launches of a phase: advance the id counter, empty the local stage
-__global__ void k_gossip_commit_fin(KP P, const uint32_t* total) {
-  P.ctl->gcount += *total;
+// after the commit of a phase: advance the id counter, empty the local stage
+__global__ void k_gossip_commit_fin(KP P, uint32_t n) {
+  P.ctl->gcount += n;
   P.ctl->stg_count = 0u;
 }
 
@@ -329,7 +350,7 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
 // in the active list. A word's infection rounds (64 B) are read only when its class is MIXED;
 // ALL/NONE words are decided by the class. A member with a non-empty window registers with each
 // chosen peer (in_cnt), so delivery can run receiver-side (k_gossip_pull).
-__global__ void __launch_bounds__(256) k_gossip_select(KP P) {
+__global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
@@ -341,7 +362,7 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   const bool mine = m < P.row0 + P.nloc;
   const bool active = mine && P.alive[m] && lo < hi;
   const uint32_t W32 = P.GC >> 5;
-  uint32_t others = 0, nclear = 0, hdw = 0, winw = 0;
+  uint32_t others = 0, nclear = 0, hdw = 0, winw = 0, winbits = 0;
   bool win_l = false;
   const bool any = active && P.held[m] > 0u;  // wave-uniform
   if (any) {
@@ -351,6 +372,8 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
     uint32_t* hbr = P.hb + lrow(P, m) * W32;
     uint32_t* wbr = P.wb + lrow(P, m) * W32;
     const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
+    uint8_t* mminr = P.mmin + lrow(P, m) * W32;
+    const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
     // two-stage software pipeline: the next iteration's list entry and holds word are in flight
     uint32_t e_n = lane < n_act ? P.act[lane] : 0u;
     uint32_t word_n = lane < n_act ? hbr[(w_beg + (e_n & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
@@ -366,7 +389,14 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
       const uint32_t held = word & range_mask(wi << 5, lo, hi);
       uint32_t clear = 0, win = 0;
       if (held) {
-        if (wc == WC_MIXED || sc == WC_MIXED) {
+        uint32_t wcm = wc, scm = sc;
+        if (wcm == WC_MIXED || scm == WC_MIXED) {
+          // this member's own age range in the word: [r - newest, r - oldest] (mod 2^8)
+          const uint32_t amin = (r - mmaxr[ws]) & 0xFFu, amax = (r - mminr[ws]) & 0xFFu;
+          if (wcm == WC_MIXED) wcm = amin > spread ? WC_NONE : (amax <= spread ? WC_ALL : WC_MIXED);
+          if (scm == WC_MIXED) scm = amax <= sweep ? WC_NONE : (amin > sweep ? WC_ALL : WC_MIXED);
+        }
+        if (wcm == WC_MIXED || scm == WC_MIXED) {
           // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
           ++hdw;
           uint4 dv[2];
@@ -374,16 +404,20 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
           dv[0] = dp[0];
           dv[1] = dp[1];
           const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dv);
-#pragma unroll
+          uint32_t oldest_kept = 0;
+#pragma unroll 8
           for (uint32_t b = 0; b < 32u; ++b) {
             const uint32_t age = (r - (d32[b >> 2] >> ((b & 3u) * 8u))) & 0xFFu;
             const uint32_t hbit = (held >> b) & 1u;
-            clear |= (hbit & (age > sweep ? 1u : 0u)) << b;  // sweepGossips
+            const uint32_t gone = hbit & (age > sweep ? 1u : 0u);
+            clear |= gone << b;  // sweepGossips
             win |= (hbit & (age <= spread ? 1u : 0u)) << b;
+            if (hbit && !gone && age > oldest_kept) oldest_kept = age;
           }
+          if (clear && (held & ~clear)) mminr[ws] = (uint8_t)(r - oldest_kept);
         } else {
-          if (wc == WC_ALL) win = held;
-          if (sc == WC_ALL) clear = held;
+          if (wcm == WC_ALL) win = held;
+          if (scm == WC_ALL) clear = held;
         }
         if (clear) {
           hbr[ws] = word & ~clear;
@@ -394,6 +428,7 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
         ++winw;
         wbr[k] = win;
         win_l |= win != 0u;
+        winbits += (uint32_t)__popc(win);
       }
     }
   }
@@ -463,6 +498,10 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   }
   // spreadGossipsTo is a no-op for an empty window: only non-empty windows reach receivers
   const bool reg = __any(win_l) && np > 0u;
+  // GossipRequest messages: every window gossip to every alive peer (GPI:225-239), counted here
+  // because receivers that already hold a whole word never look at the senders' windows
+  const uint32_t alive_peers = (uint32_t)__popcll(__ballot(reg && lane < np && P.alive[s_peers[w][lane]]));
+  winbits = wave_sum(winbits);
   if (reg && lane < np) {
     const uint32_t p = s_peers[w][lane];
     if (is_local(P, p)) {
@@ -479,6 +518,7 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
   if (any && lane == 0 && nclear) P.held[m] -= nclear;
   if (mine && lane == 0) P.npeers[m] = reg ? np : 0u;
   add_stat(P, ST_G_SCANNED, (any && lane == 0) ? n_act : 0u);
+  add_stat(P, ST_GOSSIP_SENDS, (reg && lane == 0) ? winbits * alive_peers : 0u);
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
 }
@@ -492,6 +532,7 @@ __global__ void __launch_bounds__(256) k_gossip_select(KP P) {
 // only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
 // receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
 __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
+  __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   const uint32_t lane = threadIdx.x & 63u;
@@ -500,10 +541,15 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
   const uint32_t deg = P.in_cnt[p];
-  uint32_t sends = 0, probes = 0, receipts = 0, words = 0;
+  uint32_t probes = 0, receipts = 0, words = 0;
+  const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  uint32_t* sum = s_sum[threadIdx.x >> 6];
+  const uint32_t nsw = (n_act + 31u) >> 5;
   if (deg && P.alive[p] && n_act) {  // a stopped transport loses every message
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
+    if (nsw <= NSUM)
+      for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
     for (uint32_t done = 0; done < deg;) {
@@ -546,9 +592,12 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
         const uint32_t e = e_n;
         if (k + 64u < n_act) e_n = P.act[k + 64u];
         if (((e >> 26) & 3u) == WC_NONE) continue;
-        const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+        const uint32_t ws = wi & (W32 - 1u);
         const uint32_t hw = hbr[ws];
         ++words;
+        const uint32_t live = range_mask(wi << 5, lo, hi);
+        if ((hw & live) == live) continue;  // holds every live gossip of the word: nothing is new
         uint32_t u = 0;
         for (uint32_t q0 = 0; q0 < cdeg; q0 += 4u) {
           uint32_t wv[4], mv[4];
@@ -565,7 +614,6 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
             const uint32_t win = wv[j];
             if (!win) continue;
             ++probes;
-            sends += (uint32_t)__popc(win);
             if (!((reach >> (q0 + j)) & 1ull)) continue;
             uint32_t cand = win & ~hw & ~u;
             if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
@@ -585,6 +633,7 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
           hbr[ws] = hw | u;
           nbr[k] |= u;
           receipts += (uint32_t)__popc(u);
+          if (nsw <= NSUM) atomicOr(&sum[k >> 5], 1u << (k & 31u));
         }
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
@@ -592,11 +641,16 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
     const uint32_t total = wave_sum(receipts);
     if (lane == 0 && total) {
       const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);
-      P.alist[idx] = p;
+      P.alist[2 * idx] = p;
+      P.alist[2 * idx + 1] = total;
+    }
+    if (total && nsw <= NSUM) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (uint32_t t = lane; t < nsw; t += 64u) P.nsum[lrow(P, p) * NSUM + t] = sum[t];
     }
   }
   if (lane == 0) P.in_cnt[p] = 0u;  // ready for the next round
-  add_stat(P, ST_GOSSIP_SENDS, sends);
   add_stat(P, ST_G_PROBES, probes);
   add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
   add_stat(P, ST_G_PULLW, words);
@@ -605,59 +659,63 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
 constexpr uint32_t HCAP_LOG = 13;
 constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 64 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
+constexpr uint32_t SPILL_CAP = 2048;       // spilled subjects per receiver and round (LDS list)
 constexpr uint32_t APPLY_THREADS = 512;
 constexpr uint32_t APPLY_BLOCKS = 512;     // persistent: 2 workgroups per CU (LDS-bound)
 
 // Membership apply of a round's first receipts: onGossipReq's new-gossip branch
 // (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
 // the records that reached a cell this round. Persistent workgroups take the
-// receivers of alist; for receiver p the receipts are nb. They get infectionPeriod r+1 (one
-// 64-B read-modify-write of the word's infection rounds); their records are max-reduced per
-// subject in an LDS hash sized to the receipt count (a storm round brings a receiver tens of
-// thousands of gossips about a few thousand subjects); a subject that finds no slot within
-// HPROBE probes goes to the global inbox instead, consistently for the whole round. Then one
-// updateMembership per subject.
+// receivers of alist (receiver, receipt count); for receiver p the receipts are nb, cleared on
+// the way. They get infectionPeriod r+1 (one 32-B read-modify-write of the word's infection
+// rounds). Ring slots of one commit are sorted by (subject, record), so one representative per
+// run of one subject carries the run's lattice max; representatives are max-reduced per subject
+// in an LDS hash sized to the receipt count. A subject that finds no slot within HPROBE probes
+// goes to the global inbox instead (consistently for the whole round) and onto an LDS list.
+// Then one updateMembership per subject.
 __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   __shared__ uint32_t s_key[HCAP];
   __shared__ uint32_t s_val[HCAP];
-  __shared__ uint32_t s_red[APPLY_THREADS / 64];
-  __shared__ uint32_t s_spill;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
+  __shared__ uint32_t s_spl[SPILL_CAP];
+  __shared__ uint32_t s_nspill;
   const uint32_t r = P.round;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
   uint32_t created = 0;
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
-    const uint32_t p = P.alist[li];
+    const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
-    // receipts of p and the table size (>= 2x receipts, 64 .. HCAP)
-    uint32_t c = 0;
-    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x)
-      if (((P.act[k] >> 26) & 3u) != WC_NONE) c += (uint32_t)__popc(nbr[k]);
-    c = wave_sum(c);
-    if (lane == 0) s_red[wv] = c;
-    if (threadIdx.x == 0) s_spill = 0u;
-    __syncthreads();
-    uint32_t total = 0;
-    for (uint32_t q = 0; q < blockDim.x / 64u; ++q) total += s_red[q];
-    uint32_t lg = 6;
+    uint32_t lg = 6;  // table size >= 2x receipts, 64 .. HCAP
     while (lg < HCAP_LOG && (1u << lg) < 2u * total) ++lg;
     const uint32_t hm = (1u << lg) - 1u;
     for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x) {
       s_key[t] = NONE;
       s_val[t] = 0u;
     }
+    if (threadIdx.x == 0) s_nspill = 0u;
     __syncthreads();
-    // infection rounds, word liveness, and the lattice max per subject
-    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {
+    // infection rounds, word liveness, and the lattice max per subject, over the words the
+    // receipt summary lists (or every active word when the list is too long to summarize)
+    const uint32_t nsw = (n_act + 31u) >> 5;
+    const bool summ = nsw <= NSUM;
+    const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
+    const uint32_t n_items = summ ? nsw * 32u : n_act;
+    for (uint32_t it = threadIdx.x; it < n_items; it += blockDim.x) {
+      uint32_t k = it;
+      if (summ) {  // item = (summary word, bit): consecutive threads share one summary word
+        if (!((sumr[it >> 5] >> (it & 31u)) & 1u)) continue;
+      }
       const uint32_t e = P.act[k];
       if (((e >> 26) & 3u) == WC_NONE) continue;
       const uint32_t bits = nbr[k];
       if (!bits) continue;
+      nbr[k] = 0u;  // nb is all-zero between rounds
       const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
+      const size_t mi = lrow(P, p) * W32 + ws;
+      P.mmax[mi] = (uint8_t)(r + 1u);
+      if ((P.hb[mi] & ~bits) == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
       uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
@@ -673,6 +731,9 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           }
         dp[q] = v;
       }
+      // one representative receipt per run of one subject: records ascend within a run, so the
+      // highest receipt of the run carries the lattice max of the run's receipts
+      const uint32_t rs = P.runw[ws] | 1u;
       uint32_t left = bits;
       while (left) {
         uint2 sr[4];  // four ring-record loads in flight per lane
@@ -680,8 +741,10 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j)
           if (left) {
-            const uint32_t b = (uint32_t)__builtin_ctz(left);
-            left &= left - 1u;
+            const uint32_t b = 31u - (uint32_t)__builtin_clz(left);
+            const uint32_t below = b == 31u ? 0xFFFFFFFFu : ((2u << b) - 1u);
+            const uint32_t a = 31u - (uint32_t)__builtin_clz(rs & below);  // start of b's run
+            left &= (1u << a) - 1u;
             sr[j] = P.g_sr[ws * 32u + b];
             ++nl;
           }
@@ -700,8 +763,13 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
             h = (h + 1u) & hm;
           }
           if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
-            atomicMax(&P.inbox[lrow(P, p) * P.N + sr[j].x], sr[j].y);
-            s_spill = 1u;
+            if (atomicMax(&P.inbox[lrow(P, p) * P.N + sr[j].x], sr[j].y) == 0u) {
+              const uint32_t o = atomicAdd(&s_nspill, 1u);
+              if (o < SPILL_CAP)
+                s_spl[o] = sr[j].x;
+              else
+                atomicOr(&P.ctl->overflow, OV_DIRTY);
+            }
           }
         }
       }
@@ -717,26 +785,12 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     };
     for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x)  // one updateMembership per subject
       if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
-    if (s_spill) {
-      __threadfence();
-      __syncthreads();
-      for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {
-        const uint32_t e = P.act[k];
-        if (((e >> 26) & 3u) == WC_NONE) continue;
-        uint32_t left = nbr[k];
-        const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
-        while (left) {
-          const uint32_t b = (uint32_t)__builtin_ctz(left);
-          left &= left - 1u;
-          const uint32_t subj = P.g_sr[ws * 32u + b].x;
-          const uint32_t r1 = atomicExch(&P.inbox[lrow(P, p) * P.N + subj], 0u);
-          if (r1) apply(subj, r1);  // several new gossips about one subject: applied once
-        }
-      }
+    const uint32_t nsp = s_nspill < SPILL_CAP ? s_nspill : SPILL_CAP;
+    if (nsp) __threadfence();
+    for (uint32_t t = threadIdx.x; t < nsp; t += blockDim.x) {
+      const uint32_t subj = s_spl[t];
+      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.N + subj], 0u));
     }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x)  // nb is all-zero between rounds
-      if (((P.act[k] >> 26) & 3u) != WC_NONE && nbr[k]) nbr[k] = 0u;
     if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
     __syncthreads();  // the table is reused by the next receiver
   }

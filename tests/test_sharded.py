@@ -88,10 +88,11 @@ def _parity_worker(rank, world, port, names):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("names", [["c1_local32_crash", "local48_links"],
-                                   ["lan256_loss5_crash3", "local128_partition_heal"],
-                                   ["test64_long_partition_rejoin"]])
-def test_two_shards_match_unsharded(names):
-    """2 ranks sharing cuda:0, gloo exchanges: views, deadlines, events, counters, digests and
-    presence equal the unsharded handle's after every period."""
-    mp.spawn(_parity_worker, args=(2, _free_port(), names), nprocs=2, join=True)
+@pytest.mark.parametrize("world,names", [(2, ["c1_local32_crash", "local48_links"]),
+                                         (2, ["lan256_loss5_crash3", "local128_partition_heal"]),
+                                         (2, ["test64_long_partition_rejoin"]),
+                                         (4, ["local128_partition_heal", "lan1024_loss5_crash10"])])
+def test_shards_match_unsharded(world, names):
+    """`world` ranks sharing cuda:0, gloo exchanges: views, deadlines, events, counters, digests
+    and presence equal the unsharded handle's after every period."""
+    mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
