@@ -46,7 +46,7 @@ WORKLOADS = {
     "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",
                     n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 20, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
-               n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 16),
+               n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }

@@ -374,15 +374,24 @@ __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
     const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
     uint8_t* mminr = P.mmin + lrow(P, m) * W32;
     const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
-    // two-stage software pipeline: the next iteration's list entry and holds word are in flight
-    uint32_t e_n = lane < n_act ? P.act[lane] : 0u;
-    uint32_t word_n = lane < n_act ? hbr[(w_beg + (e_n & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
-    for (uint32_t k = lane; k < n_act; k += 64u) {
-      const uint32_t e = e_n, word = word_n;
-      if (k + 64u < n_act) {
-        e_n = P.act[k + 64u];
-        word_n = hbr[(w_beg + (e_n & ACT_OFF_MASK)) & (W32 - 1u)];
+    // four list entries per lane per step, their holds words loaded together (bytes in flight)
+    for (uint32_t k0 = 0; k0 < n_act; k0 += 256u) {
+      uint32_t ev[4], wv[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t k = k0 + 64u * j + lane;
+        ev[j] = k < n_act ? P.act[k] : 0u;
       }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t k = k0 + 64u * j + lane;
+        wv[j] = k < n_act ? hbr[(w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
+      }
+#pragma unroll 1
+      for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t k = k0 + 64u * j + lane;
+      if (k >= n_act) break;
+      const uint32_t e = ev[j], word = wv[j];
       const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
       const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
       const uint32_t ws = wi & (W32 - 1u);
@@ -425,10 +434,15 @@ __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
         }
       }
       if (wc != WC_NONE) {
-        ++winw;
-        wbr[k] = win;
+        // a globally ALL word's window is the member's holdings after the sweep, which receivers
+        // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
+        if (wc == WC_MIXED) {
+          ++winw;
+          wbr[k] = win;
+        }
         win_l |= win != 0u;
         winbits += (uint32_t)__popc(win);
+      }
       }
     }
   }
@@ -553,6 +567,7 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
     for (uint32_t done = 0; done < deg;) {
+      const bool first_chunk = done == 0;  // later chunks only add gossips earlier ones did not bring
       // next chunk of senders: lane q holds sender q
       uint32_t sreg = 0, cdeg = 0;
       if (done == 0) {
@@ -587,17 +602,33 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
       s_sid[threadIdx.x >> 6][lane] = sid;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      uint32_t e_n = lane < n_act ? P.act[lane] : 0u;  // next list entry in flight
-      for (uint32_t k = lane; k < n_act; k += 64u) {
-        const uint32_t e = e_n;
-        if (k + 64u < n_act) e_n = P.act[k + 64u];
-        if (((e >> 26) & 3u) == WC_NONE) continue;
+      for (uint32_t k0 = 0; k0 < n_act; k0 += 256u) {
+        uint32_t ev[4], hv[4];  // four list entries per lane per step, holds words loaded together
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+          const uint32_t k = k0 + 64u * j + lane;
+          ev[j] = k < n_act ? P.act[k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+          const uint32_t k = k0 + 64u * j + lane;
+          hv[j] = (k < n_act && ((ev[j] >> 26) & 3u) != WC_NONE) ? hbr[(w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u)]
+                                                                 : 0u;
+        }
+#pragma unroll 1
+        for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t k = k0 + 64u * j + lane;
+        if (k >= n_act) break;
+        const uint32_t e = ev[j];
+        const uint32_t wc = (e >> 26) & 3u;
+        if (wc == WC_NONE) continue;
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t hw = hbr[ws];
+        const uint32_t hw = hv[j];
         ++words;
         const uint32_t live = range_mask(wi << 5, lo, hi);
         if ((hw & live) == live) continue;  // holds every live gossip of the word: nothing is new
+        const uint32_t prev = first_chunk ? 0u : nbr[k];
         uint32_t u = 0;
         for (uint32_t q0 = 0; q0 < cdeg; q0 += 4u) {
           uint32_t wv[4], mv[4];
@@ -606,8 +637,9 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
             const uint32_t en = q0 + j < cdeg ? snd[q0 + j] : 0u;
             mv[j] = q0 + j < cdeg ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
             wv[j] = q0 + j >= cdeg ? 0u
-                    : (en & XREC) ? P.xrecv[(size_t)(en & ~XREC) * P.xrec_words + 2u + k]
-                                  : P.wb[lrow(P, en) * W32 + k];
+                    : (en & XREC)      ? P.xrecv[(size_t)(en & ~XREC) * P.xrec_words + 2u + k]
+                    : wc == WC_ALL     ? P.hb[lrow(P, en) * W32 + ws] & live
+                                       : P.wb[lrow(P, en) * W32 + k];
           }
 #pragma unroll
           for (uint32_t j = 0; j < 4u; ++j) {
@@ -615,7 +647,7 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
             if (!win) continue;
             ++probes;
             if (!((reach >> (q0 + j)) & 1ull)) continue;
-            uint32_t cand = win & ~hw & ~u;
+            uint32_t cand = win & ~hw & ~u & ~prev;
             if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
               uint32_t need = cand;
               cand = 0u;
@@ -629,11 +661,11 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
             u |= cand;
           }
         }
-        if (u) {
-          hbr[ws] = hw | u;
-          nbr[k] |= u;
+        if (u) {  // holdings are updated by k_gossip_apply, after every receiver has pulled
+          nbr[k] = prev | u;
           receipts += (uint32_t)__popc(u);
           if (nsw <= NSUM) atomicOr(&sum[k >> 5], 1u << (k & 31u));
+        }
         }
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
@@ -714,8 +746,10 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
       const size_t mi = lrow(P, p) * W32 + ws;
+      const uint32_t prior = P.hb[mi];
+      P.hb[mi] = prior | bits;  // onGossipReq: the receiver now holds them
       P.mmax[mi] = (uint8_t)(r + 1u);
-      if ((P.hb[mi] & ~bits) == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
+      if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
       uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
@@ -830,7 +864,15 @@ __global__ void __launch_bounds__(256) k_gossip_pack(KP P, uint32_t n_rec, uint3
       out[1] = e[1];
     }
     const uint32_t* wbr = P.wb + lrow(P, m) * W32;
-    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) out[2 + k] = wbr[k];
+    const uint32_t* hbr = P.hb + lrow(P, m) * W32;
+    const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi, w_beg = P.ctl->w_beg;
+    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {  // the window as k_gossip_pull reads it
+      const uint32_t e = P.act[k];
+      const uint32_t wc = (e >> 26) & 3u, wi = w_beg + (e & ACT_OFF_MASK);
+      out[2 + k] = wc == WC_NONE ? 0u
+                   : wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi)
+                                  : wbr[k];
+    }
   }
 }
 

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=${1:-pmc}
 out=gpurun_out/$tag
 mkdir -p $out
-args="--steps ${PMC_STEPS:-20} --no-cpu-baseline --converge 0 ${BENCH_ARGS}"
+args="--steps ${PMC_STEPS:-100} --no-cpu-baseline --converge 0 ${BENCH_ARGS}"
 echo "start $(date +%T)" > $out/status.log
 timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- \
     python3 bench.py $args > $out/fetch_bench.json 2> $out/fetch_bench.err \
