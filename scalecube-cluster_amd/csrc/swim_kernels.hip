@@ -602,29 +602,15 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
       s_sid[threadIdx.x >> 6][lane] = sid;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      for (uint32_t k0 = 0; k0 < n_act; k0 += 256u) {
-        uint32_t ev[4], hv[4];  // four list entries per lane per step, holds words loaded together
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-          const uint32_t k = k0 + 64u * j + lane;
-          ev[j] = k < n_act ? P.act[k] : 0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-          const uint32_t k = k0 + 64u * j + lane;
-          hv[j] = (k < n_act && ((ev[j] >> 26) & 3u) != WC_NONE) ? hbr[(w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u)]
-                                                                 : 0u;
-        }
-#pragma unroll 1
-        for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t k = k0 + 64u * j + lane;
-        if (k >= n_act) break;
-        const uint32_t e = ev[j];
+      uint32_t e_n = lane < n_act ? P.act[lane] : 0u;  // next list entry in flight
+      for (uint32_t k = lane; k < n_act; k += 64u) {
+        const uint32_t e = e_n;
+        if (k + 64u < n_act) e_n = P.act[k + 64u];
         const uint32_t wc = (e >> 26) & 3u;
         if (wc == WC_NONE) continue;
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t hw = hv[j];
+        const uint32_t hw = hbr[ws];
         ++words;
         const uint32_t live = range_mask(wi << 5, lo, hi);
         if ((hw & live) == live) continue;  // holds every live gossip of the word: nothing is new
@@ -665,7 +651,6 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
           nbr[k] = prev | u;
           receipts += (uint32_t)__popc(u);
           if (nsw <= NSUM) atomicOr(&sum[k >> 5], 1u << (k & 31u));
-        }
         }
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
@@ -733,20 +718,12 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     const bool summ = nsw <= NSUM;
     const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
     const uint32_t n_items = summ ? nsw * 32u : n_act;
-    for (uint32_t it = threadIdx.x; it < n_items; it += blockDim.x) {
-      uint32_t k = it;
-      if (summ) {  // item = (summary word, bit): consecutive threads share one summary word
-        if (!((sumr[it >> 5] >> (it & 31u)) & 1u)) continue;
-      }
-      const uint32_t e = P.act[k];
-      if (((e >> 26) & 3u) == WC_NONE) continue;
-      const uint32_t bits = nbr[k];
-      if (!bits) continue;
+    // per word with receipts: holdings, liveness, age bounds, infection rounds (32-B read-modify-
+    // write), then one representative per subject run into the LDS table
+    auto process = [&](uint32_t k, uint32_t ws, uint32_t bits, uint32_t prior, uint32_t rs, uint4 v0, uint4 v1) {
       nbr[k] = 0u;  // nb is all-zero between rounds
-      const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
       const size_t mi = lrow(P, p) * W32 + ws;
-      const uint32_t prior = P.hb[mi];
       P.hb[mi] = prior | bits;  // onGossipReq: the receiver now holds them
       P.mmax[mi] = (uint8_t)(r + 1u);
       if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
@@ -755,7 +732,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
         const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
         if (!nb16) continue;
-        uint4 v = dp[q];
+        uint4 v = q == 0 ? v0 : v1;
         uint32_t* v32 = reinterpret_cast<uint32_t*>(&v);
 #pragma unroll
         for (uint32_t b = 0; b < 16u; ++b)
@@ -765,9 +742,8 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           }
         dp[q] = v;
       }
-      // one representative receipt per run of one subject: records ascend within a run, so the
-      // highest receipt of the run carries the lattice max of the run's receipts
-      const uint32_t rs = P.runw[ws] | 1u;
+      // records ascend within a run, so the run's highest receipt carries its lattice max
+      rs |= 1u;
       uint32_t left = bits;
       while (left) {
         uint2 sr[4];  // four ring-record loads in flight per lane
@@ -807,6 +783,38 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           }
         }
       }
+    };
+    const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
+    for (uint32_t it0 = 0; it0 < n_items; it0 += 4u * blockDim.x) {
+      // four items per thread: their loads are issued together, stage by stage
+      uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
+      uint4 v0[4], v1[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t it = it0 + j * blockDim.x + threadIdx.x;
+        // summary item = (summary word, bit): consecutive threads share one summary word
+        const bool ok = it < n_items && (!summ || ((sumr[it >> 5] >> (it & 31u)) & 1u));
+        kv[j] = ok ? it : NONE;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) ev[j] = kv[j] != NONE ? P.act[kv[j]] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        bv[j] = (kv[j] != NONE && ((ev[j] >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        wsv[j] = (w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u);
+        if (bv[j]) {
+          pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
+          rv[j] = P.runw[wsv[j]];
+          const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
+          v0[j] = dp[0];
+          v1[j] = dp[1];
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        if (bv[j]) process(kv[j], wsv[j], bv[j], pv[j], rv[j], v0[j], v1[j]);
     }
     __syncthreads();
     const uint32_t snap = P.cnt[p];
