@@ -14,6 +14,7 @@
 #include <vector>
 
 #include <hipcub/device/device_radix_sort.hpp>
+#include <hipcub/device/device_scan.hpp>
 
 #include "swim_kernels.hip"
 
@@ -54,6 +55,11 @@ struct swim_handle {
   unsigned long long* cv[2] = {nullptr, nullptr};
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
+  uint32_t n_out_pairs = 0, n_in_pairs = 0, nneed = 0;
+  uint32_t out_pairs[SWIM_MAX_WORLD] = {0};
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
   unsigned long long* d_digest = nullptr;
   std::vector<void*> allocs;
   std::string err;
@@ -164,7 +170,7 @@ void memset_ctl_u32(swim_handle* h, size_t offset) {
 // ---- one protocol period as a resumable sequence ---------------------
 // Unsharded handles run a period straight through. Sharded handles (world > 1) stop at each
 // cross-shard exchange, describe it in a swim_xchg, and resume after the host's collective.
-enum Pc : int { PC_FD = 0, PC_FD_C, PC_R_MAX, PC_R_SEL, PC_R_PULL, PC_R_C, PC_SUSP, PC_SYNC_REQ, PC_SYNC_ACK, PC_END };
+enum Pc : int { PC_FD = 0, PC_FD_C, PC_R_MAX, PC_R_SEL, PC_R_NEED, PC_R_WIN, PC_R_PULL, PC_R_C, PC_SUSP, PC_SYNC_REQ, PC_SYNC_ACK, PC_END };
 
 void set_phase(swim_handle* h, KP& P, uint32_t phase) {
   const uint32_t t = (uint32_t)h->period, G = h->G, TPP = h->TPP;
@@ -292,33 +298,81 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        h->pc = PC_R_PULL;
-        if (W > 1) {  // windows bound for receivers on other shards
+        h->pc = PC_R_NEED;
+        if (W > 1) {  // (1) registrations with receivers on other shards
           Ctl c;
           if ((rc = read_ctl(h, &c))) return rc;
-          const uint32_t rec = 2u + c.n_act;
+          if (c.n_act > 32u * 1024u) return fail(h, SWIM_EOVERFLOW, "active list too long for sharded need bitmaps");
+          h->nneed = (c.n_act + 31u) / 32u;
           uint32_t n_rec = 0;
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
           for (uint32_t q = 0; q < W; ++q) {
-            x->send_counts[q] = (uint64_t)c.xg_cnt[q] * rec;
+            x->send_counts[q] = 2ull * c.xg_cnt[q];
+            h->out_pairs[q] = c.xg_cnt[q];
             n_rec += c.xg_cnt[q];
           }
-          if ((uint64_t)n_rec * rec > h->xsend_words) return fail(h, SWIM_EOVERFLOW, "gossip exchange buffer too small");
+          h->n_out_pairs = n_rec;
           P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-          if (n_rec) hipLaunchKernelGGL(k_gossip_pack, dim3(std::min<uint32_t>(n_rec, 4096)), dim3(256), 0, s, P, n_rec, rec);
+          if (n_rec) hipLaunchKernelGGL(k_gossip_pack_pairs, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
           HIPC(h, hipStreamSynchronize(s));
-          h->xrec = rec;
           return SWIM_OK;
         }
+        h->pc = PC_R_PULL;
         break;
+      case PC_R_NEED: {  // (2) receiver side: what each received pair's receiver still lacks
+        uint64_t words = 0;
+        for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
+        const uint32_t n_in = (uint32_t)(words / 2);
+        uint64_t back[SWIM_MAX_WORLD];
+        for (uint32_t q = 0; q < W; ++q) back[q] = x->recv_counts[q] / 2 * h->nneed;
+        h->n_in_pairs = n_in;
+        P.nneed = h->nneed;
+        P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+        P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+        if (n_in) {
+          hipLaunchKernelGGL(k_gossip_need, dim3(std::min<uint32_t>(n_in, 8192)), dim3(256), 0, s, P, n_in, h->nneed);
+          size_t tb = h->scan_tmp_bytes;
+          HIPC(h, hipcub::DeviceScan::ExclusiveSum(h->scan_tmp, tb, P.rtot, P.roff, (int)n_in, s));
+        }
+        xchg_clear(x, SWIM_X_ALLTOALLV, W);
+        for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
+        HIPC(h, hipStreamSynchronize(s));
+        h->pc = PC_R_WIN;
+        return SWIM_OK;
+      }
+      case PC_R_WIN: {  // (3) sender side: ship the needed window words
+        const uint32_t n_out = h->n_out_pairs;
+        P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+        P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+        P.nneed = h->nneed;
+        xchg_clear(x, SWIM_X_ALLTOALLV, W);
+        if (n_out) {
+          hipLaunchKernelGGL(k_gossip_wcount, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, P, n_out, h->nneed);
+          size_t tb = h->scan_tmp_bytes;
+          HIPC(h, hipcub::DeviceScan::ExclusiveSum(h->scan_tmp, tb, P.wcnt, P.woff, (int)n_out + 1, s));
+          std::vector<uint32_t> woff(n_out + 1);
+          HIPC(h, hipMemcpyAsync(woff.data(), P.woff, 4ull * (n_out + 1), hipMemcpyDeviceToHost, s));
+          HIPC(h, hipStreamSynchronize(s));
+          if (woff[n_out] > h->xsend_words) return fail(h, SWIM_EOVERFLOW, "gossip exchange buffer too small");
+          uint32_t g = 0;
+          for (uint32_t q = 0; q < W; ++q) {
+            x->send_counts[q] = woff[g + h->out_pairs[q]] - woff[g];
+            g += h->out_pairs[q];
+          }
+          hipLaunchKernelGGL(k_gossip_pack_sparse, dim3(std::min<uint32_t>(n_out, 8192)), dim3(256), 0, s, P, n_out,
+                             h->nneed);
+        }
+        HIPC(h, hipStreamSynchronize(s));
+        h->pc = PC_R_PULL;
+        return SWIM_OK;
+      }
       case PC_R_PULL:
         if (W > 1) {
-          uint64_t words = 0;
-          for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
-          const uint32_t n_rec = (uint32_t)(words / h->xrec);
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
-          P.xrec_words = h->xrec;
-          if (n_rec) hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+          P.nneed = h->nneed;
+          if (h->n_in_pairs)
+            hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(h->n_in_pairs, 256)), dim3(256), 0, s, P,
+                               h->n_in_pairs);
         }
         timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
@@ -571,6 +625,25 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.ack_ref, 2ull * N);
   ALLOC(h->d_xcounts, SWIM_MAX_WORLD + 1);
   ALLOC(P.runw, h->GC / 32);
+  if (world > 1) {
+    const size_t pin = (size_t)(N - P.nloc) * c.gossip_fanout, pout = NL * c.gossip_fanout, nw = h->GC / 1024;
+    ALLOC(P.rpairs, 2 * pin);
+    ALLOC(P.rneed, pin * nw);
+    ALLOC(P.rpref, pin * nw);
+    ALLOC(P.rtot, pin);
+    ALLOC(P.roff, pin);
+    ALLOC(P.wcnt, pout + 1);
+    ALLOC(P.woff, pout + 1);
+    if (rc == SWIM_OK) {
+      size_t tb = 0;
+      (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P.rtot, P.roff, (int)std::max(pin, pout + 1), h->stream);
+      h->scan_tmp_bytes = tb;
+      char* tmp = nullptr;
+      rc = dalloc(h, &tmp, tb);
+      h->scan_tmp = tmp;
+      if (rc == SWIM_OK) (void)hipMemsetAsync(P.wcnt, 0, (pout + 1) * 4, h->stream);
+    }
+  }
   for (int k = 0; k < 2; ++k) {
     ALLOC(h->ck[k], (size_t)P.stg_cap * world);
     ALLOC(h->cv[k], (size_t)P.stg_cap * world);

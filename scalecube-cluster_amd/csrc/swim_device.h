@@ -166,7 +166,15 @@ struct KP {
   const uint32_t* blx;  // global (max bit_length, 32 - min bit_length) after the round's all-reduce
   uint32_t* xsend;      // host-attached device buffers of the current exchange
   const uint32_t* xrecv;
-  uint32_t xrec_words;  // words per received record (window records: 2 + n_act; rows: 2 + N)
+  uint32_t xrec_words;  // words per received record (SYNC rows: 2 + N)
+  uint32_t nneed;       // words of a need bitmap over this round's active list
+  uint32_t* rpairs;     // [(N-nloc)*f][2] received (sender, receiver) pairs of the round
+  uint32_t* rneed;      // [pairs][W32/32] per pair: active words the receiver lacks something in
+  uint32_t* rpref;      // [pairs][W32/32] exclusive prefix of the need bits' popcounts
+  uint32_t* rtot;       // [pairs] needed words per received pair
+  uint32_t* roff;       // [pairs] where its window words start in the received buffer
+  uint32_t* wcnt;       // [nloc*f] words each sent pair ships
+  uint32_t* woff;       // [nloc*f + 1] exclusive scan of wcnt
   uint32_t* xg_pend;    // [world][nloc*f][2] (sender, remote peer) pairs of the round
   uint32_t* xs_pend;    // [world][2*nloc] SYNC requests bound for each remote shard
   uint32_t* rs_ref;     // [2N] receiver side: record index of remote request q

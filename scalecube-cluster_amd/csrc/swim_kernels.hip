@@ -537,6 +537,8 @@ __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
   add_stat(P, ST_G_WINW, winw);
 }
 
+__device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
+
 // One wave per receiver p: spreadGossipsTo (GossipProtocolImpl.java:215-251) seen from the
 // receiving side. Every sender that picked p sends each gossip of its start-of-round window as
 // one GossipRequest (:225-239); p adopts a gossip iff it does not hold it (onGossipReq :171-183).
@@ -592,9 +594,9 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
         if (cdeg == 0) break;  // invariant: in_cnt counts every registration
       }
       done += cdeg;
-      // an entry is a local sender's member id, or XREC | index of a window record received
-      // from the sender's shard: [sender, receiver, window words of the round's active list]
-      const uint32_t sid = lane < cdeg ? ((sreg & XREC) ? P.xrecv[(size_t)(sreg & ~XREC) * P.xrec_words] : sreg) : 0u;
+      // an entry is a local sender's member id, or XREC | index of a pair received from the
+      // sender's shard (its window words arrive sparse, see k_gossip_need)
+      const uint32_t sid = lane < cdeg ? ((sreg & XREC) ? P.rpairs[2 * (sreg & ~XREC)] : sreg) : 0u;
       const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sid, p);
       const unsigned long long reach = __ballot(ok_l);
       uint32_t* snd = s_snd[threadIdx.x >> 6];
@@ -623,7 +625,7 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
             const uint32_t en = q0 + j < cdeg ? snd[q0 + j] : 0u;
             mv[j] = q0 + j < cdeg ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
             wv[j] = q0 + j >= cdeg ? 0u
-                    : (en & XREC)      ? P.xrecv[(size_t)(en & ~XREC) * P.xrec_words + 2u + k]
+                    : (en & XREC)      ? remote_window(P, en & ~XREC, k)
                     : wc == WC_ALL     ? P.hb[lrow(P, en) * W32 + ws] & live
                                        : P.wb[lrow(P, en) * W32 + k];
           }
@@ -857,37 +859,138 @@ __device__ __forceinline__ bool xrec_locate(const KP& P, const uint32_t* cnt, ui
   return false;
 }
 
-// window records [sender, receiver, wb row over the active list] for every remote peer
-__global__ void __launch_bounds__(256) k_gossip_pack(KP P, uint32_t n_rec, uint32_t rec_words) {
-  const uint32_t n_act = P.ctl->n_act;
+// Cross-shard gossip delivery asks before it ships: (1) the sender shard sends its (sender,
+// receiver) registrations; (2) the receiver shard answers, per pair, a bitmap over the round's
+// active list of the words the receiver still lacks something in (exactly the words
+// k_gossip_pull will look at); (3) the sender shard ships the window words of those positions
+// only. After a storm, when everyone holds everything, (3) is empty.
+
+// (1) registrations [sender, receiver], destination shards in rank order
+__global__ void k_gossip_pack_pairs(KP P, uint32_t n_rec) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t dst, i;
+  if (g < n_rec && xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) {
+    const uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + i);
+    P.xsend[2 * g] = e[0];
+    P.xsend[2 * g + 1] = e[1];
+  }
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* total, uint32_t* lds4);
+
+// block-wide exclusive scan of 4 consecutive values per thread (blockDim = 256)
+__device__ __forceinline__ void scan4_256(const uint32_t v[4], uint32_t out[4], uint32_t* total, uint32_t* lds4) {
+  const uint32_t loc = v[0] + v[1] + v[2] + v[3];
+  const uint32_t base = block_excl_scan256(loc, total, lds4);
+  out[0] = base;
+  out[1] = base + v[0];
+  out[2] = out[1] + v[1];
+  out[3] = out[2] + v[2];
+}
+
+// (2) receiver shard: keep the received pairs, compute each pair's need bitmap (kept for the
+// pull, and sent back), its per-word prefix counts and its total
+__global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uint32_t nneed) {
+  __shared__ uint32_t s_lds4[4];
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const uint32_t W32 = P.GC >> 5;
-  for (uint32_t g = blockIdx.x; g < n_rec; g += gridDim.x) {
+  for (uint32_t i = blockIdx.x; i < n_pairs; i += gridDim.x) {
+    const uint32_t p = P.xrecv[2 * i + 1];
+    if (threadIdx.x == 0) {
+      P.rpairs[2 * i] = P.xrecv[2 * i];
+      P.rpairs[2 * i + 1] = p;
+    }
+    const uint32_t* hbr = P.hb + lrow(P, p) * W32;
+    uint32_t cnt[4], pre[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t t = 4u * threadIdx.x + j;
+      uint32_t bits = 0;
+      if (t < nneed)
+        for (uint32_t b = 0; b < 32u; ++b) {
+          const uint32_t k = 32u * t + b;
+          if (k >= n_act) break;
+          const uint32_t e = P.act[k];
+          if (((e >> 26) & 3u) == WC_NONE) continue;
+          const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+          const uint32_t live = range_mask(wi << 5, lo, hi);
+          if ((hbr[wi & (W32 - 1u)] & live) != live) bits |= 1u << b;
+        }
+      if (t < nneed) {
+        P.rneed[(size_t)i * nneed + t] = bits;
+        P.xsend[(size_t)i * nneed + t] = bits;
+      }
+      cnt[j] = (uint32_t)__popc(bits);
+    }
+    uint32_t total;
+    scan4_256(cnt, pre, &total, s_lds4);
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t t = 4u * threadIdx.x + j;
+      if (t < nneed) P.rpref[(size_t)i * nneed + t] = pre[j];
+    }
+    if (threadIdx.x == 0) P.rtot[i] = total;
+  }
+}
+
+// (3a) sender shard: words each of its pairs must ship (the need bitmaps came back in send order)
+__global__ void k_gossip_wcount(KP P, uint32_t n_pairs, uint32_t nneed) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_pairs) {
+    uint32_t c = 0;
+    for (uint32_t t = 0; t < nneed; ++t) c += (uint32_t)__popc(P.xrecv[(size_t)g * nneed + t]);
+    P.wcnt[g] = c;
+  }
+}
+
+// (3b) the needed window words of each pair, in need-bit order, at woff[g]
+__global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pairs, uint32_t nneed) {
+  __shared__ uint32_t s_lds4[4];
+  const uint32_t w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t W32 = P.GC >> 5;
+  for (uint32_t g = blockIdx.x; g < n_pairs; g += gridDim.x) {
     uint32_t dst, i;
     if (!xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) break;
-    const uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + i);
-    const uint32_t m = e[0];
-    uint32_t* out = P.xsend + (size_t)g * rec_words;
-    if (threadIdx.x == 0) {
-      out[0] = m;
-      out[1] = e[1];
-    }
+    const uint32_t m = P.xg_pend[2 * ((size_t)dst * P.nloc * P.f + i)];
     const uint32_t* wbr = P.wb + lrow(P, m) * W32;
     const uint32_t* hbr = P.hb + lrow(P, m) * W32;
-    const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi, w_beg = P.ctl->w_beg;
-    for (uint32_t k = threadIdx.x; k < n_act; k += blockDim.x) {  // the window as k_gossip_pull reads it
-      const uint32_t e = P.act[k];
-      const uint32_t wc = (e >> 26) & 3u, wi = w_beg + (e & ACT_OFF_MASK);
-      out[2 + k] = wc == WC_NONE ? 0u
-                   : wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi)
-                                  : wbr[k];
+    uint32_t nv[4], cnt[4], pre[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t t = 4u * threadIdx.x + j;
+      nv[j] = t < nneed ? P.xrecv[(size_t)g * nneed + t] : 0u;
+      cnt[j] = (uint32_t)__popc(nv[j]);
+    }
+    uint32_t total;
+    scan4_256(cnt, pre, &total, s_lds4);
+    uint32_t* out = P.xsend + P.woff[g];
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      uint32_t bits = nv[j], o = pre[j];
+      while (bits) {  // the window as k_gossip_pull reads it
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1u;
+        const uint32_t k = 32u * (4u * threadIdx.x + j) + b;
+        const uint32_t e = P.act[k];
+        const uint32_t wc = (e >> 26) & 3u, wi = w_beg + (e & ACT_OFF_MASK);
+        out[o++] = wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi) : wbr[k];
+      }
     }
   }
 }
 
-// received window records join their receivers' sender lists
-__global__ void k_gossip_unpack(KP P, uint32_t n_rec) {
+// received sparse windows join their receivers' sender lists
+__global__ void k_gossip_unpack(KP P, uint32_t n_pairs) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n_rec) register_sender(P, P.xrecv[(size_t)g * P.xrec_words + 1], XREC | g);
+  if (g < n_pairs) register_sender(P, P.rpairs[2 * g + 1], XREC | g);
+}
+
+// window word k of received pair i (0 where the receiver needed nothing: pull skips those)
+__device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k) {
+  const size_t nw = (size_t)i * P.nneed + (k >> 5);
+  const uint32_t nb = P.rneed[nw], bit = 1u << (k & 31u);
+  if (!(nb & bit)) return 0u;
+  return P.xrecv[P.roff[i] + P.rpref[nw] + (uint32_t)__popc(nb & (bit - 1u))];
 }
 
 // SYNC request records [q, receiver, requester's table at phase start]
