@@ -678,7 +678,8 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
 constexpr uint32_t HCAP_LOG = 13;
 constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 64 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
-constexpr uint32_t SPILL_CAP = 2048;       // spilled subjects per receiver and round (LDS list)
+constexpr uint32_t SPILL_CAP = 1024;       // spilled subjects per receiver and round (LDS list)
+constexpr uint32_t PRES_WORDS = 2048;     // subject-presence bitmap for N <= 65,536
 constexpr uint32_t APPLY_THREADS = 512;
 constexpr uint32_t APPLY_BLOCKS = 512;     // persistent: 2 workgroups per CU (LDS-bound)
 
@@ -696,6 +697,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   __shared__ uint32_t s_key[HCAP];
   __shared__ uint32_t s_val[HCAP];
   __shared__ uint32_t s_spl[SPILL_CAP];
+  __shared__ uint32_t s_pres[PRES_WORDS];  // subjects in the table (N <= 65,536): row-order apply
   __shared__ uint32_t s_nspill;
   const uint32_t r = P.round;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
@@ -713,6 +715,9 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       s_val[t] = 0u;
     }
     if (threadIdx.x == 0) s_nspill = 0u;
+    const bool pres = P.N <= 32u * PRES_WORDS;
+    if (pres)
+      for (uint32_t t = threadIdx.x; t < (P.N + 31u) / 32u; t += blockDim.x) s_pres[t] = 0u;
     __syncthreads();
     // infection rounds, word liveness, and the lattice max per subject, over the words the
     // receipt summary lists (or every active word when the list is too long to summarize)
@@ -769,6 +774,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
             const uint32_t prev = atomicCAS(&s_key[h], NONE, sr[j].x);
             if (prev == NONE || prev == sr[j].x) {
               atomicMax(&s_val[h], sr[j].y);
+              if (prev == NONE && pres) atomicOr(&s_pres[sr[j].x >> 5], 1u << (sr[j].x & 31u));
               placed = true;
               break;
             }
@@ -827,8 +833,22 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         ++created;
       }
     };
-    for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x)  // one updateMembership per subject
-      if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
+    if (pres) {  // one updateMembership per subject, in subject order: neighbouring threads touch
+                 // neighbouring cells of the receiver's row (coalesced, line reuse)
+      for (uint32_t t = threadIdx.x; t < (P.N + 31u) / 32u; t += blockDim.x) {
+        uint32_t bits = s_pres[t];
+        while (bits) {
+          const uint32_t subj = 32u * t + (uint32_t)__builtin_ctz(bits);
+          bits &= bits - 1u;
+          uint32_t h = (subj * 0x9E3779B1u) >> (32u - lg);
+          while (s_key[h] != subj) h = (h + 1u) & hm;  // present: placed within HPROBE probes
+          apply(subj, s_val[h]);
+        }
+      }
+    } else {
+      for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x)  // one updateMembership per subject
+        if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
+    }
     const uint32_t nsp = s_nspill < SPILL_CAP ? s_nspill : SPILL_CAP;
     if (nsp) __threadfence();
     for (uint32_t t = threadIdx.x; t < nsp; t += blockDim.x) {

@@ -1,0 +1,39 @@
+"""bench.py's workload and byte-model helpers (CPU only)."""
+import numpy as np
+
+import bench
+
+
+def test_c3_workload_matches_baseline_config():
+    w = bench.WORKLOADS["c3"]
+    assert w["n"] == 65536 and w["crash"] == 0.10 and w["part"] == 40 and w["preset"] == "lan"
+    assert w["part"] < 85  # heals before the 85-period suspicion timeout (ClusterMath at N = 65,536)
+
+
+def test_partition_groups_spread_evenly():
+    g = bench.partition_groups(65536, 16)
+    ids = np.nonzero(g)[0]
+    assert len(ids) == 16 and ids.tolist() == [k * 4096 for k in range(16)]
+    assert bench.partition_groups(8192, 16).sum() == 16
+
+
+def test_crash_set_is_seeded_and_sized():
+    a, b = bench.crash_set(65536, 0.10, 1), bench.crash_set(65536, 0.10, 1)
+    assert a == b and len(a) == 6554 and len(set(a)) == 6554 and a == sorted(a)
+    assert bench.crash_set(100, 0.0, 1) == []
+
+
+def test_kernel_bytes_covers_every_timed_class():
+    from swimhip import SwimCluster
+
+    d = {k: 1 for k in ("merge_cells", "ack_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
+                        "gossip_pull_words", "gossip_probes", "gossip_first_receipts", "sweep_cells", "fd_probes")}
+    for name in SwimCluster.KERNEL_CLASSES:
+        if name != "bookkeeping":
+            assert bench.kernel_bytes(name, d, 1) > 0, name
+
+
+def test_pmc_traffic_reads_committed_summary():
+    t = bench.pmc_traffic("k_gossip_select")
+    assert t is None or t > 0
+    assert bench.pmc_traffic("no_such_kernel") is None

@@ -63,3 +63,25 @@ def test_crash_converges_and_gossip_capacity_reports_overflow():
     with pytest.raises(SwimError) as ei:
         c.step(12)
     assert ei.value.code == -75  # SWIM_EOVERFLOW
+
+
+def test_c3_schedule_small_parity():
+    """The bench's C3 fault schedule (10 % simultaneous crash + a 16-member partition for 40
+    periods healed by SYNC, LAN defaults) at N = 1,024: the gossip storm it triggers (SYNC merges
+    re-spreading accepted SUSPECT records) must match the oracle bit for bit."""
+    import bench
+
+    cfg = bench.preset_config("lan")
+    n = 1024
+    a = SwimCluster(cfg, n, seed=1, gossip_capacity=1 << 17)
+    b = OracleCluster(cfg, n, seed=1)
+    for c in (a, b):
+        c.step(3)
+        bench.inject_faults(c, "c3", 3, 1, n=n)
+    for _ in range(12):
+        for c in (a, b):
+            c.step(5)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+    assert a.stats()["gossips_created"] > 10 * n  # the storm really happened
