@@ -190,7 +190,8 @@ typedef struct swim_xchg {
   uint64_t send_words;
   uint64_t send_counts[SWIM_MAX_WORLD];
   uint64_t recv_counts[SWIM_MAX_WORLD]; /* host: words received from each rank             */
-  uint64_t recv_stride;                 /* host, ALLGATHER: words per rank block in recv    */
+  uint64_t recv_stride;                 /* host, ALLGATHER: words per rank block in recv;
+                                           ALLTOALLV: words sent by all ranks together      */
 } swim_xchg;
 /* Device buffer sizes (u32 words) the host must allocate and attach before stepping. */
 int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv_words);

@@ -320,6 +320,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         h->pc = PC_R_PULL;
         break;
       case PC_R_NEED: {  // (2) receiver side: what each received pair's receiver still lacks
+        if (x->recv_stride == 0) {  // no shard registered a remote receiver: nothing to ask or ship
+          h->n_in_pairs = 0;
+          h->pc = PC_R_PULL;
+          break;
+        }
         uint64_t words = 0;
         for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
         const uint32_t n_in = (uint32_t)(words / 2);
