@@ -350,6 +350,8 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
 // in the active list. A word's infection rounds (64 B) are read only when its class is MIXED;
 // ALL/NONE words are decided by the class. A member with a non-empty window registers with each
 // chosen peer (in_cnt), so delivery can run receiver-side (k_gossip_pull).
+constexpr uint32_t SEL_BATCH = 4;  // list entries per lane per step in k_gossip_select
+
 __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
@@ -374,21 +376,21 @@ __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
     const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
     uint8_t* mminr = P.mmin + lrow(P, m) * W32;
     const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
-    // four list entries per lane per step, their holds words loaded together (bytes in flight)
-    for (uint32_t k0 = 0; k0 < n_act; k0 += 256u) {
-      uint32_t ev[4], wv[4];
+    // SEL_BATCH list entries per lane per step, their holds words loaded together (bytes in flight)
+    for (uint32_t k0 = 0; k0 < n_act; k0 += 64u * SEL_BATCH) {
+      uint32_t ev[SEL_BATCH], wv[SEL_BATCH];
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
+      for (uint32_t j = 0; j < SEL_BATCH; ++j) {
         const uint32_t k = k0 + 64u * j + lane;
         ev[j] = k < n_act ? P.act[k] : 0u;
       }
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
+      for (uint32_t j = 0; j < SEL_BATCH; ++j) {
         const uint32_t k = k0 + 64u * j + lane;
         wv[j] = k < n_act ? hbr[(w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
       }
 #pragma unroll 1
-      for (uint32_t j = 0; j < 4u; ++j) {
+      for (uint32_t j = 0; j < SEL_BATCH; ++j) {
       const uint32_t k = k0 + 64u * j + lane;
       if (k >= n_act) break;
       const uint32_t e = ev[j], word = wv[j];
