@@ -234,23 +234,33 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
     return false;
   }
   if (n) (void)hipMemcpyAsync(h->xsend, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
+  KP Q = P;
+  Q.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+  hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, 4u * n);
   HIPC_RC(h, rc, hipStreamSynchronize(s));
   xchg_clear(x, SWIM_X_ALLGATHER, h->world);
-  x->send_words = 4ull * n;
+  x->send_words = 4ull * n + h->GC / 32 + 2;
   return true;
 }
 
 int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   hipStream_t s = h->stream;
   const uint32_t* xr = reinterpret_cast<const uint32_t*>(h->xrecv);
-  uint32_t total = 0;
+  uint32_t total = 0, offs[SWIM_MAX_WORLD];
+  const uint64_t tail = h->GC / 32 + 2;  // wlast + bounds after each shard's gossips
   for (uint32_t q = 0; q < h->world; ++q) {
-    const uint32_t c = (uint32_t)(x->recv_counts[q] / 4);
+    const uint32_t c = (uint32_t)((x->recv_counts[q] - tail) / 4);
+    offs[q] = (uint32_t)(q * x->recv_stride + 4ull * c);
     if (c)
       hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(c, 256)), dim3(256), 0, s,
                          reinterpret_cast<const uint4*>(xr + q * x->recv_stride), c, total, h->ck[0], h->cv[0]);
     total += c;
   }
+  // liveness maxima first: the commit itself then raises the new words on every shard alike
+  HIPC(h, hipMemcpyAsync(h->d_xcounts, offs, 4ull * h->world, hipMemcpyHostToDevice, s));
+  KP Q = P;
+  Q.xrecv = xr;
+  hipLaunchKernelGGL(k_round_max_merge, dim3(64), dim3(256), 0, s, Q, h->d_xcounts, h->d_blx);
   return commit_sorted(h, P, total);
 }
 
@@ -279,20 +289,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
       case PC_R_MAX:  // phases 1..G: gossip rounds
         set_phase(h, P, 1 + h->q);
         h->pc = PC_R_SEL;
-        if (W > 1) {  // liveness + bounds over every shard
-          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-          hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, P);
-          HIPC(h, hipStreamSynchronize(s));
-          xchg_clear(x, SWIM_X_ALLREDUCE_MAX, W);
-          x->send_words = h->GC / 32 + 2;
-          return SWIM_OK;
-        }
         break;
       case PC_R_SEL:
-        if (W > 1) {
-          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-          hipLaunchKernelGGL(k_round_max_unpack, dim3(64), dim3(256), 0, s, P);
-          HIPC(h, hipMemcpyAsync(h->d_blx, P.xsend + h->GC / 32, 8, hipMemcpyDeviceToDevice, s));
+        if (W > 1) {  // liveness + bounds over every shard arrived with the last commit
           P.blx = h->d_blx;
           HIPC(h, hipMemsetAsync(P.ctl->xg_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         }
@@ -1038,8 +1037,8 @@ int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv
   // gossip commits: 4 words per staged gossip (x world when gathered); round maxima: W32 + 2
   const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
   const uint64_t rows = (uint64_t)h->scap * (h->N + 2ull);
-  const uint64_t stg = 4ull * h->base.stg_cap;
-  *send_words = std::max({win, rows, stg, W32 + 2});
+  const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2;  // commits carry the liveness maxima too
+  *send_words = std::max({win, rows, stg});
   *recv_words = std::max({(uint64_t)(h->N - nloc) * h->base.f * (2 + W32), rows, stg * h->world});
   return SWIM_OK;
 }

@@ -1058,10 +1058,12 @@ __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
 }
 
 // the all-reduce MAX operand of a round: per-word gossip liveness + the bit_length bounds
-__global__ void k_round_max_pack(KP P) {
+// Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
+// bit-length bounds after the words of its staged gossips: [gossips | wlast | bhi | 32 - blo]
+__global__ void k_round_max_pack(KP P, uint32_t off) {
   const uint32_t W32 = P.GC >> 5;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W32; i += gridDim.x * blockDim.x)
-    P.xsend[i] = P.wlast[i];
+    P.xsend[off + i] = P.wlast[i];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t blo = 32, bhi = 0;
     for (uint32_t b = 0; b < 32u; ++b)
@@ -1069,15 +1071,25 @@ __global__ void k_round_max_pack(KP P) {
         blo = b < blo ? b : blo;
         bhi = b;
       }
-    P.xsend[W32] = bhi;
-    P.xsend[W32 + 1] = 32u - blo;  // 0 when this shard has no alive member
+    P.xsend[off + W32] = bhi;
+    P.xsend[off + W32 + 1] = 32u - blo;  // 0 when this shard has no alive member
   }
 }
 
-__global__ void k_round_max_unpack(KP P) {
+// element-wise max over the shards' blocks (offsets in `offs`) into wlast and blx
+__global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
   const uint32_t W32 = P.GC >> 5;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W32; i += gridDim.x * blockDim.x)
-    P.wlast[i] = P.xsend[i];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < W32 + 2u; i += gridDim.x * blockDim.x) {
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < P.world; ++q) {
+      const uint32_t x = P.xrecv[offs[q] + i];
+      v = x > v ? x : v;
+    }
+    if (i < W32)
+      P.wlast[i] = v;
+    else
+      blx[i - W32] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
