@@ -44,7 +44,7 @@ struct swim_handle {
   int pc = 0;
   uint32_t q = 0;
   // sharding
-  uint32_t world = 1, rank = 0, xrec = 0;
+  uint32_t world = 1, rank = 0;
   void* xsend = nullptr;
   void* xrecv = nullptr;
   uint64_t xsend_words = 0, xrecv_words = 0;
@@ -492,8 +492,8 @@ int check_overflow(swim_handle* h) {
   if (ov) {
     char buf[160];
     std::snprintf(buf, sizeof buf,
-                  "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 dirty list, "
-                  "16 sync bucket)",
+                  "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 apply spill list, "
+                  "16 sync bucket, 32 invariant)",
                   ov);
     return fail(h, SWIM_EOVERFLOW, buf);
   }

@@ -56,10 +56,9 @@ enum Overflow : uint32_t {
   OV_EVENTS = 1u,
   OV_GOSSIP = 2u,
   OV_SYNC = 4u,
-  OV_DIRTY = 8u,
+  OV_SPILL = 8u,  // a receiver spilled more subjects in one round than its LDS spill list holds
   OV_BUCKET = 16u,
   OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
-  OV_HOLD_RANGE = 64u,  // a gossip was received more than 65534 rounds after its creation
 };
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
@@ -166,7 +165,6 @@ struct KP {
   const uint32_t* blx;  // global (max bit_length, 32 - min bit_length) after the round's all-reduce
   uint32_t* xsend;      // host-attached device buffers of the current exchange
   const uint32_t* xrecv;
-  uint32_t xrec_words;  // words per received record (SYNC rows: 2 + N)
   uint32_t nneed;       // words of a need bitmap over this round's active list
   uint32_t* rpairs;     // [(N-nloc)*f][2] received (sender, receiver) pairs of the round
   uint32_t* rneed;      // [pairs][W32/32] per pair: active words the receiver lacks something in

@@ -788,7 +788,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
               if (o < SPILL_CAP)
                 s_spl[o] = sr[j].x;
               else
-                atomicOr(&P.ctl->overflow, OV_DIRTY);
+                atomicOr(&P.ctl->overflow, OV_SPILL);
             }
           }
         }
