@@ -667,7 +667,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.in_list, (size_t)N * INCAP);
   ALLOC(P.in_ov, 2ull * N * c.gossip_fanout);
   ALLOC(P.alist, 2ull * N);
-  ALLOC(P.act, h->GC / 32);
+  ALLOC(P.act, h->GC / 32 + 8);  // + a quad of slack: k_gossip_select reads the list 16 B at a time
   ALLOC(P.held, N);
   ALLOC(P.due, N);
   ALLOC(P.events, std::max<uint32_t>(1, h->ecap));

@@ -309,30 +309,49 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
   }
   __syncthreads();
   const uint32_t lo = s_lo, hi = s_hi;
-  const uint32_t w_beg = lo >> 5, w_end = (hi + 31u) >> 5;
+  const uint32_t w_lo = lo >> 5, w_end = (hi + 31u) >> 5;
   const int32_t r = (int32_t)P.round;
   const int32_t spread_lo = (int32_t)(P.rm * s_blo), spread_hi = (int32_t)(P.rm * s_bhi);
   const int32_t sweep_lo = 2 * (spread_lo + 1), sweep_hi = 2 * (spread_hi + 1);
   const uint32_t W32 = P.GC >> 5;
+  // Words are listed by aligned quads: a quad with any active word contributes all four (the
+  // idle ones with class NONE/NONE, which every consumer skips), so list position 4q..4q+3 maps
+  // to four consecutive, 16-B-aligned holdings words and k_gossip_select reads them with one
+  // 16-B load. When the padded span would not fit the list (a live range of ~GC ids), only the
+  // active words are listed and the consumers fall back to per-word loads.
+  const uint32_t w_beg = w_lo & ~3u, q_end = (w_end + 3u) & ~3u;
+  const bool pad = q_end - w_beg <= W32;
   uint32_t base = 0;
-  for (uint32_t t0 = w_beg; t0 < w_end; t0 += blockDim.x) {
-    const uint32_t wi = t0 + threadIdx.x;
-    uint32_t e = 0;
-    bool on = false;
-    if (wi < w_end) {
-      const uint32_t ws = wi & (W32 - 1u);
-      const uint32_t id0 = (wi << 5) > lo ? (wi << 5) : lo;
-      const int32_t inf_lo = (int32_t)P.g_create[id0 & P.gmask];
-      const int32_t inf_hi = (int32_t)P.wlast[ws];
-      const int32_t amin = r - inf_hi, amax = r - inf_lo;  // holders' ages lie in [amin, amax]
-      const uint32_t wc = amin > spread_hi ? WC_NONE : (amax <= spread_lo ? WC_ALL : WC_MIXED);
-      const uint32_t sc = amax <= sweep_lo ? WC_NONE : (amin > sweep_hi ? WC_ALL : WC_MIXED);
-      on = wc != WC_NONE || sc != WC_NONE;
-      e = (wi - w_beg) | (wc << 26) | (sc << 28);
+  for (uint32_t t0 = w_beg; t0 < q_end; t0 += 4u * blockDim.x) {
+    const uint32_t wq = t0 + 4u * threadIdx.x;
+    uint32_t e[4], onm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      const uint32_t wi = wq + j;
+      uint32_t wc = WC_NONE, sc = WC_NONE;
+      if (wi >= w_lo && wi < w_end) {
+        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t id0 = (wi << 5) > lo ? (wi << 5) : lo;
+        const int32_t inf_lo = (int32_t)P.g_create[id0 & P.gmask];
+        const int32_t inf_hi = (int32_t)P.wlast[ws];
+        const int32_t amin = r - inf_hi, amax = r - inf_lo;  // holders' ages lie in [amin, amax]
+        wc = amin > spread_hi ? WC_NONE : (amax <= spread_lo ? WC_ALL : WC_MIXED);
+        sc = amax <= sweep_lo ? WC_NONE : (amin > sweep_hi ? WC_ALL : WC_MIXED);
+      }
+      if (wc != WC_NONE || sc != WC_NONE) onm |= 1u << j;
+      e[j] = (wi - w_beg) | (wc << 26) | (sc << 28);
     }
+    const uint32_t cnt = pad ? (onm ? 4u : 0u) : (uint32_t)__popc(onm);
     uint32_t total;
-    const uint32_t off = block_excl_scan1024(on ? 1u : 0u, &total, s_part);
-    if (on) P.act[base + off] = e;
+    const uint32_t off = block_excl_scan1024(cnt, &total, s_part);
+    if (pad) {
+      if (onm) *reinterpret_cast<uint4*>(P.act + base + off) = make_uint4(e[0], e[1], e[2], e[3]);
+    } else {
+      uint32_t o = base + off;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        if ((onm >> j) & 1u) P.act[o++] = e[j];
+    }
     base += total;
   }
   if (threadIdx.x == 0) {
@@ -350,9 +369,15 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
 // in the active list. A word's infection rounds (64 B) are read only when its class is MIXED;
 // ALL/NONE words are decided by the class. A member with a non-empty window registers with each
 // chosen peer (in_cnt), so delivery can run receiver-side (k_gossip_pull).
-constexpr uint32_t SEL_BATCH = 4;  // list entries per lane per step in k_gossip_select
+#ifndef SWIM_SEL_BATCH
+#define SWIM_SEL_BATCH 2
+#endif
+#ifndef SWIM_SEL_WAVES
+#define SWIM_SEL_WAVES 8
+#endif
+constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
-__global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
@@ -376,75 +401,135 @@ __global__ void __launch_bounds__(256, 6) k_gossip_select(KP P) {
     const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
     uint8_t* mminr = P.mmin + lrow(P, m) * W32;
     const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
-    // SEL_BATCH list entries per lane per step, their holds words loaded together (bytes in flight)
-    for (uint32_t k0 = 0; k0 < n_act; k0 += 64u * SEL_BATCH) {
-      uint32_t ev[SEL_BATCH], wv[SEL_BATCH];
+    // SEL_BATCH aligned quads of list entries per lane per step: one 16-B list load and (for a
+    // quad of consecutive aligned words, the padded layout of k_gossip_prep) one 16-B holdings
+    // load each, all issued together (bytes in flight). Words whose class the member's own age
+    // bounds settle are finished in a fully unrolled pass (no dynamically indexed register
+    // arrays, so nothing goes to scratch); the few left MIXED are finished one by one from a mask.
+    for (uint32_t k0 = 0; k0 < n_act; k0 += 256u * SEL_BATCH) {
+      uint32_t ev[4 * SEL_BATCH], wv[4 * SEL_BATCH];
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
-        const uint32_t k = k0 + 64u * j + lane;
-        ev[j] = k < n_act ? P.act[k] : 0u;
+        const uint32_t kq = k0 + 256u * j + 4u * lane;
+        const uint4 a = kq < n_act ? *reinterpret_cast<const uint4*>(P.act + kq) : make_uint4(0u, 0u, 0u, 0u);
+        ev[4 * j] = a.x;
+        ev[4 * j + 1] = a.y;
+        ev[4 * j + 2] = a.z;
+        ev[4 * j + 3] = a.w;
       }
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
-        const uint32_t k = k0 + 64u * j + lane;
-        wv[j] = k < n_act ? hbr[(w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
-      }
-#pragma unroll 1
-      for (uint32_t j = 0; j < SEL_BATCH; ++j) {
-      const uint32_t k = k0 + 64u * j + lane;
-      if (k >= n_act) break;
-      const uint32_t e = ev[j], word = wv[j];
-      const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
-      const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
-      const uint32_t ws = wi & (W32 - 1u);
-      const uint32_t held = word & range_mask(wi << 5, lo, hi);
-      uint32_t clear = 0, win = 0;
-      if (held) {
-        uint32_t wcm = wc, scm = sc;
-        if (wcm == WC_MIXED || scm == WC_MIXED) {
-          // this member's own age range in the word: [r - newest, r - oldest] (mod 2^8)
-          const uint32_t amin = (r - mmaxr[ws]) & 0xFFu, amax = (r - mminr[ws]) & 0xFFu;
-          if (wcm == WC_MIXED) wcm = amin > spread ? WC_NONE : (amax <= spread ? WC_ALL : WC_MIXED);
-          if (scm == WC_MIXED) scm = amax <= sweep ? WC_NONE : (amin > sweep ? WC_ALL : WC_MIXED);
-        }
-        if (wcm == WC_MIXED || scm == WC_MIXED) {
-          // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
-          ++hdw;
-          uint4 dv[2];
-          const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
-          dv[0] = dp[0];
-          dv[1] = dp[1];
-          const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dv);
-          uint32_t oldest_kept = 0;
-#pragma unroll 8
-          for (uint32_t b = 0; b < 32u; ++b) {
-            const uint32_t age = (r - (d32[b >> 2] >> ((b & 3u) * 8u))) & 0xFFu;
-            const uint32_t hbit = (held >> b) & 1u;
-            const uint32_t gone = hbit & (age > sweep ? 1u : 0u);
-            clear |= gone << b;  // sweepGossips
-            win |= (hbit & (age <= spread ? 1u : 0u)) << b;
-            if (hbit && !gone && age > oldest_kept) oldest_kept = age;
-          }
-          if (clear && (held & ~clear)) mminr[ws] = (uint8_t)(r - oldest_kept);
+        const uint32_t kq = k0 + 256u * j + 4u * lane;
+        const uint32_t o0 = ev[4 * j] & ACT_OFF_MASK;
+        const uint32_t ws0 = (w_beg + o0) & (W32 - 1u);
+        const bool quad = kq + 3u < n_act && (ws0 & 3u) == 0u && (ev[4 * j + 3] & ACT_OFF_MASK) == o0 + 3u;
+        if (quad) {
+          const uint4 h = *reinterpret_cast<const uint4*>(hbr + ws0);
+          wv[4 * j] = h.x;
+          wv[4 * j + 1] = h.y;
+          wv[4 * j + 2] = h.z;
+          wv[4 * j + 3] = h.w;
         } else {
+#pragma unroll
+          for (uint32_t i = 0; i < 4u; ++i)
+            wv[4 * j + i] = kq + i < n_act ? hbr[(w_beg + (ev[4 * j + i] & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
+        }
+      }
+      uint32_t mixm = 0;  // entries whose infection rounds must be read
+#pragma unroll 1
+      for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
+        // quad jq's values by select chains (no dynamically indexed register arrays: no scratch)
+        uint32_t eq[4], hq[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i) {
+          eq[i] = ev[i];
+          hq[i] = wv[i];
+#pragma unroll
+          for (uint32_t t = 1; t < SEL_BATCH; ++t)
+            if (jq == t) {
+              eq[i] = ev[4 * t + i];
+              hq[i] = wv[4 * t + i];
+            }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i) {
+        const uint32_t j = 4u * jq + i;
+        const uint32_t k = k0 + 256u * jq + 4u * lane + i;
+        const uint32_t e = eq[i], word = hq[i];
+        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+        const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
+        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t held = k < n_act ? word & range_mask(wi << 5, lo, hi) : 0u;
+        uint32_t clear = 0, win = 0;
+        if (held) {
+          uint32_t wcm = wc, scm = sc;
+          if (wcm == WC_MIXED || scm == WC_MIXED) {
+            // this member's own age range in the word: [r - newest, r - oldest] (mod 2^8)
+            const uint32_t amin = (r - mmaxr[ws]) & 0xFFu, amax = (r - mminr[ws]) & 0xFFu;
+            if (wcm == WC_MIXED) wcm = amin > spread ? WC_NONE : (amax <= spread ? WC_ALL : WC_MIXED);
+            if (scm == WC_MIXED) scm = amax <= sweep ? WC_NONE : (amin > sweep ? WC_ALL : WC_MIXED);
+          }
+          if (wcm == WC_MIXED || scm == WC_MIXED) {
+            mixm |= 1u << j;
+            continue;
+          }
           if (wcm == WC_ALL) win = held;
           if (scm == WC_ALL) clear = held;
+          if (clear) {
+            hbr[ws] = word & ~clear;
+            nclear += (uint32_t)__popc(clear);
+          }
         }
+        if (k < n_act && wc != WC_NONE) {
+          // a globally ALL word's window is the member's holdings after the sweep, which receivers
+          // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
+          if (wc == WC_MIXED) {
+            ++winw;
+            wbr[k] = win;
+          }
+          win_l |= win != 0u;
+          winbits += (uint32_t)__popc(win);
+        }
+        }
+      }
+      while (mixm) {
+        const uint32_t j = (uint32_t)__builtin_ctz(mixm);
+        mixm &= mixm - 1u;
+        const uint32_t k = k0 + 256u * (j >> 2) + 4u * lane + (j & 3u);
+        const uint32_t e = P.act[k];  // re-read (cache-resident) rather than index registers
+        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+        const uint32_t wc = (e >> 26) & 3u;
+        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t word = hbr[ws];
+        const uint32_t held = word & range_mask(wi << 5, lo, hi);
+        // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
+        ++hdw;
+        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
+        const uint4 d0 = dp[0], d1 = dp[1];
+        const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        uint32_t clear = 0, win = 0, oldest_kept = 0;
+#pragma unroll 4
+        for (uint32_t b = 0; b < 32u; ++b) {
+          const uint32_t age = (r - (d32[b >> 2] >> ((b & 3u) * 8u))) & 0xFFu;
+          const uint32_t hbit = (held >> b) & 1u;
+          const uint32_t gone = hbit & (age > sweep ? 1u : 0u);
+          clear |= gone << b;  // sweepGossips
+          win |= (hbit & (age <= spread ? 1u : 0u)) << b;
+          if (hbit && !gone && age > oldest_kept) oldest_kept = age;
+        }
+        if (clear && (held & ~clear)) mminr[ws] = (uint8_t)(r - oldest_kept);
         if (clear) {
           hbr[ws] = word & ~clear;
           nclear += (uint32_t)__popc(clear);
         }
-      }
-      if (wc != WC_NONE) {
-        // a globally ALL word's window is the member's holdings after the sweep, which receivers
-        // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
-        if (wc == WC_MIXED) {
-          ++winw;
-          wbr[k] = win;
+        if (wc != WC_NONE) {
+          if (wc == WC_MIXED) {
+            ++winw;
+            wbr[k] = win;
+          }
+          win_l |= win != 0u;
+          winbits += (uint32_t)__popc(win);
         }
-        win_l |= win != 0u;
-        winbits += (uint32_t)__popc(win);
-      }
       }
     }
   }

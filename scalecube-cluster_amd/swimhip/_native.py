@@ -11,7 +11,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)  # scalecube-cluster_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(HERE, "libswimhip.so")
+# SWIMHIP_LIB: an alternative build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("SWIMHIP_LIB") or os.path.join(HERE, "libswimhip.so")
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "swimhip.h")
 
 SWIM_OK = 0
