@@ -634,7 +634,10 @@ __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint3
 // NetworkEmulator.evaluateLoss draws one value per (sender, receiver, gossip) message and is drawn
 // only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
 // receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
-__global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
+#ifndef SWIM_PULL_WAVES
+#define SWIM_PULL_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
@@ -691,56 +694,104 @@ __global__ void __launch_bounds__(256) k_gossip_pull(KP P) {
       s_sid[threadIdx.x >> 6][lane] = sid;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      uint32_t e_n = lane < n_act ? P.act[lane] : 0u;  // next list entry in flight
-      for (uint32_t k = lane; k < n_act; k += 64u) {
-        const uint32_t e = e_n;
-        if (k + 64u < n_act) e_n = P.act[k + 64u];
-        const uint32_t wc = (e >> 26) & 3u;
-        if (wc == WC_NONE) continue;
-        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
-        const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t hw = hbr[ws];
-        ++words;
-        const uint32_t live = range_mask(wi << 5, lo, hi);
-        if ((hw & live) == live) continue;  // holds every live gossip of the word: nothing is new
-        const uint32_t prev = first_chunk ? 0u : nbr[k];
-        uint32_t u = 0;
-        for (uint32_t q0 = 0; q0 < cdeg; q0 += 4u) {
-          uint32_t wv[4], mv[4];
+      // lane takes an aligned quad of list entries (k_gossip_prep pads the list into quads of
+      // consecutive aligned words): the receiver's holdings, its receipts so far and each
+      // sender's window words then come in 16-B loads; other quads fall back to per-word loads
+      for (uint32_t kq = 4u * lane; kq < n_act; kq += 256u) {
+        const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
+        const uint32_t ea[4] = {a.x, a.y, a.z, a.w};
+        const uint32_t o0 = a.x & ACT_OFF_MASK;
+        const uint32_t ws0 = (w_beg + o0) & (W32 - 1u);
+        const bool quad = kq + 3u < n_act && (ws0 & 3u) == 0u && (a.w & ACT_OFF_MASK) == o0 + 3u;
+        uint32_t wcv[4], wsv[4], live[4], hw[4], prev[4], u[4];
+        uint32_t todo = 0, anyall = 0, anymix = 0;
+        uint4 h4 = make_uint4(0u, 0u, 0u, 0u);
+        if (quad) h4 = *reinterpret_cast<const uint4*>(hbr + ws0);
+        const uint32_t ha[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) {  // issue the window loads of 4 senders together
-            const uint32_t en = q0 + j < cdeg ? snd[q0 + j] : 0u;
-            mv[j] = q0 + j < cdeg ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
-            wv[j] = q0 + j >= cdeg ? 0u
-                    : (en & XREC)      ? remote_window(P, en & ~XREC, k)
-                    : wc == WC_ALL     ? P.hb[lrow(P, en) * W32 + ws] & live
-                                       : P.wb[lrow(P, en) * W32 + k];
-          }
+        for (uint32_t i = 0; i < 4u; ++i) {
+          const bool in = kq + i < n_act;
+          wcv[i] = in ? (ea[i] >> 26) & 3u : WC_NONE;
+          const uint32_t wi = w_beg + (ea[i] & ACT_OFF_MASK);
+          wsv[i] = wi & (W32 - 1u);
+          live[i] = range_mask(wi << 5, lo, hi);
+          hw[i] = quad ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
+          u[i] = 0u;
+          prev[i] = 0u;
+          if (wcv[i] == WC_NONE) continue;
+          ++words;
+          if ((hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
+          todo |= 1u << i;
+          anyall |= wcv[i] == WC_ALL ? 1u : 0u;
+          anymix |= wcv[i] == WC_MIXED ? 1u : 0u;
+        }
+        if (!todo) continue;
+        if (!first_chunk) {  // later chunks only add gossips earlier ones did not bring
+          const uint4 p4 = *reinterpret_cast<const uint4*>(nbr + kq);
+          prev[0] = p4.x;
+          prev[1] = p4.y;
+          prev[2] = p4.z;
+          prev[3] = p4.w;
+        }
+        for (uint32_t q0 = 0; q0 < cdeg; q0 += 2u) {
+          uint32_t wv[2][4], mv[2];
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) {
-            const uint32_t win = wv[j];
-            if (!win) continue;
-            ++probes;
-            if (!((reach >> (q0 + j)) & 1ull)) continue;
-            uint32_t cand = win & ~hw & ~u & ~prev;
-            if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
-              uint32_t need = cand;
-              cand = 0u;
-              while (need) {
-                const uint32_t b = (uint32_t)__builtin_ctz(need);
-                need &= need - 1u;
-                if (draw1(P.seed, K_GOSSIP, mv[j], p, P.g_hash[ws * 32u + b], P.tick) >= P.loss_thr)
-                  cand |= 1u << b;
-              }
+          for (uint32_t j = 0; j < 2u; ++j) {  // the window loads of 2 senders, issued together
+            const bool has = q0 + j < cdeg;
+            const uint32_t en = has ? snd[q0 + j] : 0u;
+            mv[j] = has ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
+            uint4 wa = make_uint4(0u, 0u, 0u, 0u), wm = make_uint4(0u, 0u, 0u, 0u);
+            if (has && !(en & XREC) && quad) {
+              if (anyall) wa = *reinterpret_cast<const uint4*>(P.hb + lrow(P, en) * W32 + ws0);
+              if (anymix) wm = *reinterpret_cast<const uint4*>(P.wb + lrow(P, en) * W32 + kq);
             }
-            u |= cand;
+            const uint32_t waa[4] = {wa.x, wa.y, wa.z, wa.w}, wma[4] = {wm.x, wm.y, wm.z, wm.w};
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+              uint32_t v = 0u;
+              if (has && ((todo >> i) & 1u)) {
+                if (en & XREC)
+                  v = remote_window(P, en & ~XREC, kq + i);
+                else if (quad)
+                  v = wcv[i] == WC_ALL ? waa[i] & live[i] : wma[i];
+                else
+                  v = wcv[i] == WC_ALL ? P.hb[lrow(P, en) * W32 + wsv[i]] & live[i]
+                                       : P.wb[lrow(P, en) * W32 + kq + i];
+              }
+              wv[j][i] = v;
+            }
           }
+#pragma unroll
+          for (uint32_t j = 0; j < 2u; ++j)
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+              const uint32_t win = wv[j][i];
+              if (!win) continue;
+              ++probes;
+              if (!((reach >> (q0 + j)) & 1ull)) continue;
+              uint32_t cand = win & ~hw[i] & ~u[i] & ~prev[i];
+              if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+                uint32_t need = cand;
+                cand = 0u;
+                while (need) {
+                  const uint32_t b = (uint32_t)__builtin_ctz(need);
+                  need &= need - 1u;
+                  if (draw1(P.seed, K_GOSSIP, mv[j], p, P.g_hash[wsv[i] * 32u + b], P.tick) >= P.loss_thr)
+                    cand |= 1u << b;
+                }
+              }
+              u[i] |= cand;
+            }
         }
-        if (u) {  // holdings are updated by k_gossip_apply, after every receiver has pulled
-          nbr[k] = prev | u;
-          receipts += (uint32_t)__popc(u);
-          if (nsw <= NSUM) atomicOr(&sum[k >> 5], 1u << (k & 31u));
-        }
+        uint32_t sbits = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i)
+          if (u[i]) {  // holdings are updated by k_gossip_apply, after every receiver has pulled
+            nbr[kq + i] = prev[i] | u[i];
+            receipts += (uint32_t)__popc(u[i]);
+            sbits |= 1u << ((kq + i) & 31u);
+          }
+        if (sbits && nsw <= NSUM) atomicOr(&sum[kq >> 5], sbits);
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
