@@ -837,6 +837,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   __shared__ uint32_t s_spl[SPILL_CAP];
   __shared__ uint32_t s_pres[PRES_WORDS];  // subjects in the table (N <= 65,536): row-order apply
   __shared__ uint32_t s_nspill;
+  __shared__ uint32_t s_part[16];
   const uint32_t r = P.round;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
@@ -931,16 +932,42 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       }
     };
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
-    for (uint32_t it0 = 0; it0 < n_items; it0 += 4u * blockDim.x) {
+    // The list positions with receipts, compacted from the summary into the table's unused tail:
+    // the table has 2^lg >= 2 * total slots and a receipt word holds >= 1 receipt, so when
+    // 2^lg < HCAP the <= total positions fit in HCAP - 2^lg >= 2^lg slots. Otherwise every summary
+    // bit is an item and threads test their own.
+    const bool compact = summ && lg < HCAP_LOG;
+    uint32_t* s_items = s_key + (1u << lg);
+    uint32_t n_comp = 0;
+    if (compact) {
+      for (uint32_t c0 = 0; c0 < nsw; c0 += blockDim.x) {
+        const uint32_t t = c0 + threadIdx.x;
+        uint32_t bits = t < nsw ? sumr[t] : 0u;
+        uint32_t tot;
+        uint32_t o = n_comp + block_excl_scan1024((uint32_t)__popc(bits), &tot, s_part);
+        while (bits) {
+          s_items[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
+          bits &= bits - 1u;
+        }
+        n_comp += tot;
+      }
+      __syncthreads();
+    }
+    const uint32_t n_it = compact ? n_comp : n_items;
+    for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * blockDim.x) {
       // four items per thread: their loads are issued together, stage by stage
       uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
       uint4 v0[4], v1[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
         const uint32_t it = it0 + j * blockDim.x + threadIdx.x;
-        // summary item = (summary word, bit): consecutive threads share one summary word
-        const bool ok = it < n_items && (!summ || ((sumr[it >> 5] >> (it & 31u)) & 1u));
-        kv[j] = ok ? it : NONE;
+        if (compact) {
+          kv[j] = it < n_it ? s_items[it] : NONE;
+        } else {
+          // summary item = (summary word, bit): consecutive threads share one summary word
+          const bool ok = it < n_items && (!summ || ((sumr[it >> 5] >> (it & 31u)) & 1u));
+          kv[j] = ok ? it : NONE;
+        }
       }
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) ev[j] = kv[j] != NONE ? P.act[kv[j]] : 0u;
