@@ -81,11 +81,16 @@ def kernel_bytes(name, d, n):
     return 0
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/gpu_pmc.sh: separate
-    FETCH_SIZE and WRITE_SIZE rocprofv3 passes over the same workload; FETCH_SIZE doubled per the
-    gfx950 note in MI355X_MICROARCH.md), or None when no summary covers it."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def pmc_traffic(kernel, workload="c3", world=1):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload on one GPU
+    (tools/gpu_pmc.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes over the same workload;
+    FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md): profiles/pmc_traffic.json for
+    the default C3 run, profiles/pmc_traffic_<workload>.json for the others. None when no summary
+    covers the kernel, the workload, or a sharded run (per-launch traffic changes with the shard)."""
+    if world != 1:
+        return None
+    name = "pmc_traffic.json" if workload == "c3" else f"pmc_traffic_{workload}.json"
+    path = os.path.join(REPO, "profiles", name)
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -281,7 +286,7 @@ def main():
                    "gossip_ring_slots": w["gcap"]},
         "periods_to_dead": periods_to_dead,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom, args.workload, world),
                      "bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3, "launches": launches},
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",

@@ -37,3 +37,10 @@ def test_pmc_traffic_reads_committed_summary():
     t = bench.pmc_traffic("k_gossip_select")
     assert t is None or t > 0
     assert bench.pmc_traffic("no_such_kernel") is None
+
+
+def test_pmc_traffic_is_per_workload_and_single_gpu():
+    # the committed summary is of the default C3 run on one GPU: no other workload, no shard
+    if bench.pmc_traffic("k_gossip_select") is not None:
+        assert bench.pmc_traffic("k_gossip_select", "c3", 2) is None
+    assert bench.pmc_traffic("k_gossip_select", "no_such_workload") is None
