@@ -223,6 +223,25 @@ __device__ __forceinline__ uint32_t range_mask(uint32_t id0, uint32_t lo, uint32
   return m;
 }
 
+// Four infection rounds per dword (byte b = word bit 4q + b). Byte-wise (r - d) mod 2^8: the high
+// bit of every byte is set before the subtraction so no borrow crosses a byte, then fixed up.
+__device__ __forceinline__ uint32_t bytes_sub(uint32_t r, uint32_t d) {
+  const uint32_t R = (r & 0xFFu) * 0x01010101u, H = 0x80808080u;
+  return ((R | H) - (d & ~H)) ^ ((R ^ ~d) & H);
+}
+
+// 4-bit mask: bit b set iff byte b of a > t (t < 2^15). Bytes go to 16-bit lanes, where
+// v + 0x8000 - (t + 1) reaches bit 15 iff v > t and never carries into the next lane.
+__device__ __forceinline__ uint32_t bytes_gt(uint32_t a, uint32_t t) {
+  const uint32_t K = (0x8000u - (t + 1u)) * 0x00010001u;
+  const uint32_t gl = ((a & 0x00FF00FFu) + K) & 0x80008000u;         // bytes 0, 2
+  const uint32_t gh = (((a >> 8) & 0x00FF00FFu) + K) & 0x80008000u;  // bytes 1, 3
+  return ((gl >> 15) & 1u) | ((gh >> 14) & 2u) | ((gl >> 29) & 4u) | ((gh >> 28) & 8u);
+}
+
+// 4-bit mask -> byte mask (0xFF per set bit): the four shifted copies do not overlap
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) * 0xFFu; }
+
 // receiver p gets sender entry e this round (a local member id, or XREC | received record)
 __device__ __forceinline__ void register_sender(const KP& P, uint32_t p, uint32_t e) {
   const uint32_t slot = atomicAdd(&P.in_cnt[p], 1u);
@@ -507,15 +526,26 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
         const uint4 d0 = dp[0], d1 = dp[1];
         const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-        uint32_t clear = 0, win = 0, oldest_kept = 0;
-#pragma unroll 4
-        for (uint32_t b = 0; b < 32u; ++b) {
-          const uint32_t age = (r - (d32[b >> 2] >> ((b & 3u) * 8u))) & 0xFFu;
-          const uint32_t hbit = (held >> b) & 1u;
-          const uint32_t gone = hbit & (age > sweep ? 1u : 0u);
-          clear |= gone << b;  // sweepGossips
-          win |= (hbit & (age <= spread ? 1u : 0u)) << b;
-          if (hbit && !gone && age > oldest_kept) oldest_kept = age;
+        // four ages per dword at once (byte-wise r - round, then 16-bit-lane threshold tests)
+        uint32_t over_sweep = 0, over_spread = 0;
+        uint32_t ages[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8u; ++q) {
+          const uint32_t a = bytes_sub(r, d32[q]);
+          ages[q] = a;
+          over_sweep |= bytes_gt(a, sweep) << (4u * q);
+          over_spread |= bytes_gt(a, spread) << (4u * q);
+        }
+        const uint32_t clear = held & over_sweep;  // sweepGossips
+        const uint32_t win = held & ~over_spread;
+        uint32_t oldest_kept = 0;
+        const uint32_t kept = held & ~clear;
+        if (clear && kept) {
+#pragma unroll
+          for (uint32_t q = 0; q < 8u; ++q) {
+            const uint32_t a = ages[q] & nibble_bytes((kept >> (4u * q)) & 0xFu);
+            oldest_kept = max(oldest_kept, max(max(a & 0xFFu, (a >> 8) & 0xFFu), max((a >> 16) & 0xFFu, a >> 24)));
+          }
         }
         if (clear && (held & ~clear)) mminr[ws] = (uint8_t)(r - oldest_kept);
         if (clear) {
@@ -879,13 +909,13 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
         if (!nb16) continue;
         uint4 v = q == 0 ? v0 : v1;
-        uint32_t* v32 = reinterpret_cast<uint32_t*>(&v);
-#pragma unroll
-        for (uint32_t b = 0; b < 16u; ++b)
-          if ((nb16 >> b) & 1u) {
-            const uint32_t sh = (b & 3u) * 8u;
-            v32[b >> 2] = (v32[b >> 2] & ~(0xFFu << sh)) | (((r + 1u) & 0xFFu) << sh);
-          }
+        const uint32_t rb = ((r + 1u) & 0xFFu) * 0x01010101u;
+        const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
+        const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
+        v.x = (v.x & ~m0) | (rb & m0);
+        v.y = (v.y & ~m1) | (rb & m1);
+        v.z = (v.z & ~m2) | (rb & m2);
+        v.w = (v.w & ~m3) | (rb & m3);
         dp[q] = v;
       }
       // records ascend within a run, so the run's highest receipt carries its lattice max
