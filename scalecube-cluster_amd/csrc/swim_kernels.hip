@@ -843,13 +843,22 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   add_stat(P, ST_G_PULLW, words);
 }
 
-constexpr uint32_t HCAP_LOG = 13;
-constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 64 KiB of keys + values
+#ifndef SWIM_APPLY_HLOG
+#define SWIM_APPLY_HLOG 14
+#endif
+#ifndef SWIM_APPLY_THREADS
+#define SWIM_APPLY_THREADS 1024
+#endif
+#ifndef SWIM_APPLY_BLOCKS
+#define SWIM_APPLY_BLOCKS 256
+#endif
+constexpr uint32_t HCAP_LOG = SWIM_APPLY_HLOG;
+constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 128 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
 constexpr uint32_t SPILL_CAP = 1024;       // spilled subjects per receiver and round (LDS list)
 constexpr uint32_t PRES_WORDS = 2048;     // subject-presence bitmap for N <= 65,536
-constexpr uint32_t APPLY_THREADS = 512;
-constexpr uint32_t APPLY_BLOCKS = 512;     // persistent: 2 workgroups per CU (LDS-bound)
+constexpr uint32_t APPLY_THREADS = SWIM_APPLY_THREADS;
+constexpr uint32_t APPLY_BLOCKS = SWIM_APPLY_BLOCKS;  // persistent: one 16-wave workgroup per CU (LDS-bound)
 
 // Membership apply of a round's first receipts: onGossipReq's new-gossip branch
 // (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
