@@ -139,6 +139,11 @@ typedef struct swim_stats {
   uint64_t gossip_hd_words;   /* active words whose infection rounds k_gossip_select read  */
   uint64_t gossip_window_words; /* window words written by k_gossip_select (x members)    */
   uint64_t gossip_pull_words; /* active window words examined by k_gossip_pull (x receivers) */
+  /* GossipState.infectedFrom (GossipProtocolImpl.java:181,248); 0 in the oracle
+   * except infected_suppressed */
+  uint64_t infected_pruned_pairs; /* (sender, peer) pairs whose window was pruned              */
+  uint64_t infected_records;  /* deliveries recorded in full                                  */
+  uint64_t infected_suppressed; /* GossipRequests not sent: peer in infectedFrom (alive peers) */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -154,8 +159,12 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp);
 /* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
  * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */
 int swim_set_partition(swim_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1);
-/* Directed link block a->b (NetworkEmulator.blockOutbound(Address...) :105-119). */
+/* Directed outbound block src->dst (NetworkEmulator.blockOutbound(Address...) :105-119): the
+ * sender's send fails immediately (tryFailOutbound :166-180). */
 int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked);
+/* Inbound block at dst of messages from src (NetworkEmulator.blockInbound :255-269): dst's
+ * transport silently drops them (NetworkEmulatorTransport.java:64-68,73-77); the send succeeds. */
+int swim_block_inbound(swim_handle* h, uint32_t dst, uint32_t src, int blocked);
 /* Crash = transport.stop() (MembershipProtocolTest.java:991-1000): the member stops
  * sending, receiving, answering and firing timers, from the next period on. */
 int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
@@ -218,6 +227,9 @@ const char* swim_last_error(swim_handle* h);
 int swim_kat_is_overrides(const uint32_t* r1, const uint32_t* r0, uint8_t* out, uint64_t n);
 /* Device Philox4x32-10 draws (counter = {a,b,c,tick}, key = seed ^ kind) for RNG parity. */
 int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint32_t* out, uint64_t n);
+/* All four output words (out4[4i .. 4i+3]); with kind = 0 the key is {seed lo, seed hi}, so the
+ * Random123 philox4x32_10 known-answer vectors apply directly (tests/test_philox_kat.py). */
+int swim_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint32_t* out4, uint64_t n);
 
 /* Debug: the gossips a member holds, as (gossip hash, infection round) pairs. */
 int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,

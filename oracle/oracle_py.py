@@ -42,6 +42,8 @@ def load_oracle():
         lib.oracle_is_overrides.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         lib.oracle_philox.restype = ctypes.c_uint32
         lib.oracle_philox.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [ctypes.c_uint32] * 4
+        lib.oracle_philox4.restype = None
+        lib.oracle_philox4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, P, P]
         lib.oracle_cluster_math.restype = ctypes.c_int64
         lib.oracle_cluster_math.argtypes = [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
         lib.oracle_perm.restype = ctypes.c_uint32
@@ -61,6 +63,13 @@ def is_overrides(r1: int, r0: int) -> bool:
 
 def philox(seed: int, kind: int, a: int, b: int, c: int, tick: int) -> int:
     return load_oracle().oracle_philox(seed, kind, a, b, c, tick)
+
+
+def philox4(seed: int, kind: int, a: int, b: int, c: int, tick: int):
+    ctr = (ctypes.c_uint32 * 4)(a, b, c, tick)
+    out = (ctypes.c_uint32 * 4)()
+    load_oracle().oracle_philox4(seed, kind, ctr, out)
+    return list(out)
 
 
 def cluster_math(which: int, mult: int, n: int, fanout: int = 0) -> int:

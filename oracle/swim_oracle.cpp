@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <new>
 #include <unordered_map>
@@ -164,15 +165,33 @@ struct Gossip {  // Gossip.java:7-49 + GossipRequest payload (MembershipRecord)
   int32_t holders;  // members whose gossips map currently holds it
 };
 
-// GossipProtocolImpl.gossips (GPI:49): gossipId -> GossipState.infectionPeriod
-// (GossipState.java:14). Gossip ids (origin, seq) are also numbered globally in creation order
-// (gid); each member's map is a direct-mapped table keyed by gid that stores the full key, so
-// find/put/erase are exact map operations (a collision with a live entry grows every table).
+// GossipProtocolImpl.gossips (GPI:49): gossipId -> GossipState (infectionPeriod,
+// GossipState.java:14). Gossip ids (origin, seq) are numbered globally in creation order (gid);
+// a member's map is a bitset over the id ring (slot = gid mod rc, rc at least twice the live id
+// range, so live ids never share a slot) plus the infection round per slot, and the held ids in
+// order of infection round, which is non-decreasing (every new state gets the gossip module's
+// next round): the send window is a suffix of that order and the sweep a prefix.
 struct GossipMap {
-  std::vector<uint32_t> key;  // gid, or EMPTY
-  std::vector<int64_t> inf;
+  std::vector<uint64_t> held;                        // rc bits
+  std::vector<int64_t> inf;                          // rc slots
+  std::deque<std::pair<uint32_t, int64_t>> order;    // (gid, infectionPeriod), oldest first
 };
-constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+
+// GossipState.infected (GossipState.java:17; addToInfected GossipProtocolImpl.java:181): the
+// members a gossip was received from during its current GossipState. Kept per receiver as the
+// message batches each sender delivered: {round t, the gossips sent in t (a bitset over gid
+// words from w0)}. Member p is in infected(g) iff a batch from p of a round t >= the round the
+// current state of g was created (infectionPeriod - 1) carries g and that message was not lost —
+// exactly the set the reference accumulates (a fresh state starts empty, every later delivery
+// adds its sender). Loss draws of messages the receiver already held are evaluated only when a
+// suppression query needs them (the draw is a pure function of the message). A batch of round t
+// can only matter while the receiver may still send those gossips: rounds <= t + 1 + spread.
+struct Batch {
+  int64_t t;
+  uint32_t tick;
+  uint32_t w0;
+  std::vector<uint64_t> bits;
+};
 
 struct Member {
   std::vector<uint32_t> table;          // MPI:87 membershipTable (+ MPI:88 members: cell != 0)
@@ -182,6 +201,7 @@ struct Member {
   uint32_t fd_epoch = 0, fd_cursor = 0; // FDI:49-50 pingMembers order + pingMemberIndex
   uint32_t g_epoch = 0, g_cursor = 0;   // GPI:52-53 remoteMembers order + remoteMembersIndex
   GossipMap gossips;                    // GPI:49 gossips
+  std::unordered_map<uint32_t, std::vector<Batch>> recv;  // sender -> batches (infected sets)
   uint32_t gossip_seq = 0;              // GPI:48 gossipCounter
   uint32_t sync_fd = 0xFFFFFFFFu;       // FD-triggered SYNC target of this period (MPI:385-397)
   bool alive = true;
@@ -203,11 +223,13 @@ struct oracle_handle {
   uint32_t loss_bp = 0;
   std::vector<uint8_t> group;
   uint64_t part_t0 = 0, part_t1 = 0;
-  std::vector<uint8_t> link;  // directed block bitmap, lazily allocated
+  std::vector<uint8_t> link;    // outbound block src->dst (send error), lazily allocated
+  std::vector<uint8_t> inlink;  // inbound block at dst of messages from src (silent drop)
   std::vector<Member> m;
   std::vector<Gossip> registry;  // by gid
   uint32_t gbase = 0;            // every gid below is held by nobody
-  uint32_t rc = 64;              // capacity of each member's GossipMap (power of two)
+  uint32_t rc = 256;             // slots of each member's GossipMap (power of two)
+  int32_t hzn = 0;               // gossipPeriodsToSpread(N) + 1: rounds a batch can matter
   std::vector<swim_event> events;
   swim_stats st;
   std::vector<uint32_t> pres, last_removed;
@@ -221,19 +243,41 @@ inline uint32_t ghash(uint32_t origin, uint32_t seq) { return fmix32(origin ^ fm
 
 inline uint32_t tick_of(const oracle_handle* h, uint32_t phase) { return (uint32_t)(h->period * h->TPP + phase); }
 
-// NetworkEmulatorTransport.send/requestResponse (NET:44-70) + NetworkEmulator.evaluateLoss
-// (NE:348-351) + crash (transport stopped) + partition cut: is message src->dst delivered?
-bool delivered(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
+inline bool bit_set(const std::vector<uint8_t>& bm, uint64_t bit) {
+  return !bm.empty() && (bm[bit >> 3] & (1u << (bit & 7)));
+}
+
+// The sender side of NetworkEmulatorTransport.send/requestResponse (NET:44-70): tryFailOutbound
+// (NE:166-180) fails the send immediately — a NETWORK_BREAK error the sender sees — on a
+// loss draw (NE:348-351, nextInt(100) < lossPercent) or a blocked destination (loss 100 %,
+// NE:105-119; the partition cut is a blockOutbound on both sides). A stopped transport
+// (crash) neither sends nor accepts connections, which the sender also sees as an error.
+bool out_ok(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
   if (!h->m[src].alive || !h->m[dst].alive) return false;
   if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[src] != h->group[dst]) return false;
-  if (!h->link.empty()) {
-    uint64_t bit = (uint64_t)src * h->N + dst;
-    if (h->link[bit >> 3] & (1u << (bit & 7))) return false;
-  }
+  if (bit_set(h->link, (uint64_t)src * h->N + dst)) return false;
   if (h->loss_bp == 0) return true;      // NE:349 lossPercent > 0
   if (h->loss_bp >= 10000) return false; // NE:350 lossPercent >= 100
   uint32_t thr = (uint32_t)(((uint64_t)h->loss_bp << 32) / 10000u);
   return draw(h->seed, kind, src, dst, c, tick) >= thr;  // NE:350 nextInt(100) < loss => lost
+}
+
+// The receiver side: NET:73-77 (listen) and NET:64-68 (responses) drop a message whose sender
+// the receiver blocks inbound (NE:255-269), silently — the sender saw a successful send.
+bool in_ok(const oracle_handle* h, uint32_t dst, uint32_t src) {
+  return !bit_set(h->inlink, (uint64_t)dst * h->N + src);
+}
+
+// Everything of delivered() but the loss draw: both transports up, no partition cut, no block.
+bool link_ok(const oracle_handle* h, uint32_t src, uint32_t dst) {
+  if (!h->m[src].alive || !h->m[dst].alive) return false;
+  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[src] != h->group[dst]) return false;
+  return !bit_set(h->link, (uint64_t)src * h->N + dst) && in_ok(h, dst, src);
+}
+
+// Is message src->dst delivered to dst's protocol handlers?
+bool delivered(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
+  return out_ok(h, kind, src, dst, c, tick) && in_ok(h, dst, src);
 }
 
 void perm_keys(const oracle_handle* h, uint32_t kind, uint32_t member, uint32_t epoch, uint32_t* k) {
@@ -258,50 +302,59 @@ void emit_event(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t type, ui
   h->events.push_back(e);
 }
 
+inline bool gossip_held(const oracle_handle* h, const Member& me, uint32_t gid) {
+  const uint32_t sl = gid & (h->rc - 1);
+  return (me.gossips.held[sl >> 6] >> (sl & 63)) & 1u;
+}
+
+// infectionPeriod of a held gossip of the live id range, or -1
 int64_t gossip_find(const oracle_handle* h, const Member& me, uint32_t gid) {
-  const uint32_t s = gid & (h->rc - 1);
-  return me.gossips.key[s] == gid ? me.gossips.inf[s] : -1;
+  return gossip_held(h, me, gid) ? me.gossips.inf[gid & (h->rc - 1)] : -1;
 }
 
-void gossip_erase(oracle_handle* h, Member& me, uint32_t gid) {
-  const uint32_t s = gid & (h->rc - 1);
-  if (me.gossips.key[s] != gid) return;
-  me.gossips.key[s] = EMPTY;
-  h->registry[gid].holders--;
+// the held bits of absolute id word w (ids 64w .. 64w+63); the ring has no aliasing words
+inline uint64_t held_word(const oracle_handle* h, const Member& me, uint32_t w) {
+  return me.gossips.held[w & ((h->rc >> 6) - 1)];
 }
 
-void gossip_grow(oracle_handle* h) {
-  h->rc *= 2;
+// Grow the ring until it holds twice the live id range plus a word of slack on each side.
+void gossip_reserve(oracle_handle* h, uint32_t gend) {
+  if (2ull * (gend - h->gbase) + 256 <= h->rc) return;
+  uint32_t nrc = h->rc;
+  while (2ull * (gend - h->gbase) + 256 > nrc) nrc *= 2;
   for (auto& mm : h->m) {
-    GossipMap nm;
-    nm.key.assign(h->rc, EMPTY);
-    nm.inf.assign(h->rc, 0);
-    for (size_t s = 0; s < mm.gossips.key.size(); ++s) {
-      const uint32_t g = mm.gossips.key[s];
-      if (g == EMPTY) continue;
-      nm.key[g & (h->rc - 1)] = g;
-      nm.inf[g & (h->rc - 1)] = mm.gossips.inf[s];
+    GossipMap& g = mm.gossips;
+    std::vector<uint64_t> nh(nrc / 64, 0);
+    std::vector<int64_t> ni(nrc, 0);
+    for (const auto& e : g.order) {
+      const uint32_t sl = e.first & (nrc - 1);
+      nh[sl >> 6] |= 1ull << (sl & 63);
+      ni[sl] = e.second;
     }
-    mm.gossips = std::move(nm);
+    g.held.swap(nh);
+    g.inf.swap(ni);
   }
+  h->rc = nrc;
 }
 
+// gossips.put(id, new GossipState(gossip, inf)) (GossipProtocolImpl.java:166-167,177-178) for a
+// gossip the member does not hold
 void gossip_put(oracle_handle* h, Member& me, uint32_t gid, int64_t inf) {
-  for (;;) {
-    const uint32_t s = gid & (h->rc - 1);
-    const uint32_t k = me.gossips.key[s];
-    if (k == gid) {
-      me.gossips.inf[s] = inf;
-      return;
-    }
-    if (k == EMPTY) {
-      me.gossips.key[s] = gid;
-      me.gossips.inf[s] = inf;
-      h->registry[gid].holders++;
-      return;
-    }
-    gossip_grow(h);  // another live gossip owns the slot
-  }
+  gossip_reserve(h, gid + 1);
+  const uint32_t sl = gid & (h->rc - 1);
+  me.gossips.held[sl >> 6] |= 1ull << (sl & 63);
+  me.gossips.inf[sl] = inf;
+  me.gossips.order.push_back({gid, inf});
+  h->registry[gid].holders++;
+}
+
+// gossips.remove(id) of the oldest held gossip (sweepGossips, GossipProtocolImpl.java:297-298)
+void gossip_pop_oldest(oracle_handle* h, Member& me) {
+  const uint32_t gid = me.gossips.order.front().first;
+  const uint32_t sl = gid & (h->rc - 1);
+  me.gossips.held[sl >> 6] &= ~(1ull << (sl & 63));
+  me.gossips.order.pop_front();
+  h->registry[gid].holders--;
 }
 
 // GossipProtocolImpl.spread -> createAndPutGossip (GPI:124-128,163-169,211-213): the new
@@ -453,19 +506,28 @@ void do_ping(oracle_handle* h, uint32_t i) {
     } else {
       h->st.fd_ping_req++;
       uint32_t unsent = 0, sent = 0;
-      bool any_ok = false;
+      uint32_t first = 0xFFFFFFFFu;  // proxy whose forwarded ack reaches i's transport first
       for (uint32_t p : proxies) {
-        if (!delivered(h, K_PING_REQ, i, p, j, tick)) {  // emulator send error: immediate SUSPECT
+        if (!out_ok(h, K_PING_REQ, i, p, j, tick)) {  // tryFailOutbound: immediate error -> SUSPECT
           ++unsent;
           continue;
         }
         ++sent;
-        if (delivered(h, K_PROXY_PING, p, j, i, tick) && delivered(h, K_PROXY_ACK, j, p, i, tick) &&
-            delivered(h, K_FWD_ACK, p, i, j, tick))
-          any_ok = true;
+        // onPingReq (FDI:255-277) -> transit PING -> onPing at j -> ACK to the proxy ->
+        // onTransitPingAck (FDI:283-305) forwards it to i. Each hop is a send that the next
+        // receiver's inbound filter may drop; the last hop reaches i's TransportImpl.
+        if (first == 0xFFFFFFFFu && in_ok(h, p, i) && delivered(h, K_PROXY_PING, p, j, i, tick) &&
+            delivered(h, K_PROXY_ACK, j, p, i, tick) && out_ok(h, K_FWD_ACK, p, i, j, tick))
+          first = p;
       }
+      // TransportImpl.requestResponse matches responses by correlation id only (:236-238) and
+      // every PING_REQ of this probe carries the same cid (FDI:174-178), so the first forwarded
+      // ack (canonically: the first proxy in selection order whose relay got through) is taken
+      // by every pending subscription; NET:64-68 then checks i's inbound filter against that
+      // ack's sender (the proxy): blocked -> Mono.never() -> every subscription times out.
+      const bool ok = first != 0xFFFFFFFFu && in_ok(h, i, first);
       for (uint32_t u = 0; u < unsent; ++u) evs.push_back(SWIM_SUSPECT);
-      for (uint32_t s = 0; s < sent; ++s) evs.push_back(any_ok ? SWIM_ALIVE : SWIM_SUSPECT);  // FDI:190-207
+      for (uint32_t s = 0; s < sent; ++s) evs.push_back(ok ? SWIM_ALIVE : SWIM_SUSPECT);  // FDI:190-207
     }
   }
   for (uint32_t ev : evs) {  // publishPingResult (FDI:365-368) -> MPI:376
@@ -520,59 +582,118 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   const int32_t rm = h->cfg.gossip_repeat_mult;
   while (h->gbase < h->registry.size() && h->registry[h->gbase].holders == 0) h->gbase++;
   const uint32_t gend = (uint32_t)h->registry.size();
-  // GPI:144-146 "gossips.isEmpty()" is decided on the start-of-round state of every member:
-  // a gossip swept at the end of round r (r-1 <= inf + sweep < r) still counts, even if a
-  // delivery later in round r re-infects the member with it.
+  const uint32_t wlo = h->gbase >> 6, whi = (gend + 63) >> 6, nw = whi - wlo;
+  const uint32_t thr = (uint32_t)(((uint64_t)h->loss_bp << 32) / 10000u);
+  // NetworkEmulator.evaluateLoss of one GossipRequest (NE:348-351), the sender side of out_ok
+  auto not_lost = [&](uint32_t src, uint32_t dst, uint32_t gid, uint32_t tk) {
+    if (h->loss_bp == 0) return true;
+    if (h->loss_bp >= 10000) return false;
+    return draw(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk) >= thr;
+  };
+  // GPI:144-146 "gossips.isEmpty()" on the start-of-round state of every member
   std::vector<uint8_t> nonempty(h->N, 0);
+  for (uint32_t s = 0; s < h->N; ++s) nonempty[s] = h->m[s].alive && !h->m[s].gossips.order.empty();
+  // sweepGossips (GPI:281-304) at the end of each doSpreadGossip(r). A swept gossip is never in
+  // its holder's window (spread < sweep), so sweeping first changes no send of round r; it only
+  // makes round-r deliveries of it start a new GossipState, as they do in the reference.
   for (uint32_t s = 0; s < h->N; ++s) {
-    const Member& me = h->m[s];
+    Member& me = h->m[s];
     if (!me.alive) continue;
     const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);  // GPI:283-284
-    for (uint32_t gid = h->gbase; gid < gend && !nonempty[s]; ++gid) {
-      const int64_t inf = gossip_find(h, me, gid);
-      if (inf >= 0 && inf <= r && r - 1 <= inf + sweep) nonempty[s] = 1;
-    }
+    while (!me.gossips.order.empty() && r > me.gossips.order.front().second + sweep) gossip_pop_oldest(h, me);
   }
-  std::vector<uint32_t> window;
+  // Every member's doSpreadGossip(r) runs on the start-of-round state (its gossips, their
+  // infected sets, its peers); the messages are handled by the receivers' onGossipReq after
+  // all of them, with currentPeriod = r + 1.
+  struct Delivery {
+    uint32_t to, gid;
+  };
+  struct Sent {
+    uint32_t to, from;
+    Batch b;
+  };
+  std::vector<Delivery> deliveries;
+  std::vector<Sent> sent;
+  std::vector<std::pair<uint32_t, int64_t>> window;  // (gid, infectionPeriod)
+  std::vector<uint64_t> W(nw), S(nw);
   for (uint32_t s = 0; s < h->N; ++s) {
     Member& me = h->m[s];
-    if (!me.alive || !nonempty[s]) continue;  // GPI:144-146 (no peer selection either)
+    if (!nonempty[s]) continue;  // GPI:144-146 (no peer selection either)
     const int32_t spread = periods_to_spread(rm, (int32_t)me.others + 1);  // GPI:243-244
+    // selectGossipsToSend's age filter (GPI:247): a suffix of the infection order
     window.clear();
-    for (uint32_t gid = h->gbase; gid < gend; ++gid) {
-      const int64_t inf = gossip_find(h, me, gid);
-      if (inf >= 0 && inf <= r && r <= inf + spread) window.push_back(gid);  // GPI:247
+    std::fill(W.begin(), W.end(), 0ull);
+    for (auto it = me.gossips.order.rbegin(); it != me.gossips.order.rend() && it->second + spread >= r; ++it) {
+      if (it->second > r) continue;
+      window.push_back(*it);
+      W[(it->first >> 6) - wlo] |= 1ull << (it->first & 63);
     }
     std::vector<uint32_t> peers = select_gossip_members(h, s);  // GPI:150
+    if (window.empty()) continue;
     for (uint32_t p : peers) {
-      // GossipState.infected (GPI:248) only prunes sends to members that already hold the
-      // gossip; redundant deliveries are no-ops, so they are not simulated.
       Member& pm = h->m[p];
-      if (!pm.alive) continue;  // stopped transport: every message to it is lost
-      const int32_t psweep = periods_to_sweep(rm, (int32_t)pm.others + 1);
-      for (uint32_t gid : window) {
-        const int64_t pinf = gossip_find(h, pm, gid);
-        const bool has = pinf >= 0;
-        h->st.gossip_sends++;  // one GossipRequest message per gossip and peer (GPI:225-239)
-        if (has && r <= pinf + psweep) continue;  // receiver holds it (maybe since this round)
-        const Gossip& g = h->registry[gid];
-        if (!delivered(h, K_GOSSIP, s, p, g.hash, tick)) continue;
-        gossip_put(h, pm, gid, r + 1);  // GPI:172,176-179: infectionPeriod = receiver's next round
-        h->st.gossip_first_receipts++;
-        auto& slot = h->inbox[p][g.subject];
-        slot = std::max(slot, g.record);
+      // !isInfected(member.id()) (GPI:248): the window gossips p delivered to s during their
+      // current state
+      std::fill(S.begin(), S.end(), 0ull);
+      uint64_t nsupp = 0;
+      const auto fit = me.recv.find(p);
+      if (fit != me.recv.end())
+        for (const auto& wg : window) {
+          const uint32_t g = wg.first;
+          for (const Batch& bt : fit->second) {
+            if (bt.t < wg.second - 1 || (g >> 6) < bt.w0 || (g >> 6) - bt.w0 >= bt.bits.size()) continue;
+            if (!((bt.bits[(g >> 6) - bt.w0] >> (g & 63)) & 1u) || !not_lost(p, s, g, bt.tick)) continue;
+            S[(g >> 6) - wlo] |= 1ull << (g & 63);
+            ++nsupp;
+            break;
+          }
+        }
+      uint64_t nsend = 0;
+      for (uint32_t k = 0; k < nw; ++k) nsend += (uint64_t)__builtin_popcountll(W[k] & ~S[k]);
+      // one GossipRequest message per gossip and peer (GPI:225-239), counted for alive peers
+      if (pm.alive) {
+        h->st.gossip_sends += nsend;
+        h->st.infected_suppressed += nsupp;
       }
+      // the link part of delivered(): both alive, no partition cut, no outbound / inbound block
+      if (!nsend || !pm.alive || h->loss_bp >= 10000 || !link_ok(h, s, p)) continue;
+      Sent st{p, s, Batch{r, tick, 0, {}}};
+      uint32_t k0 = 0, k1 = nw;
+      while (k0 < k1 && !(W[k0] & ~S[k0])) ++k0;
+      while (k1 > k0 && !(W[k1 - 1] & ~S[k1 - 1])) --k1;
+      st.b.w0 = wlo + k0;
+      for (uint32_t k = k0; k < k1; ++k) {
+        const uint64_t eff = W[k] & ~S[k];
+        st.b.bits.push_back(eff);
+        // first receipts: messages p lacks the gossip of, each with its own loss draw
+        for (uint64_t cand = eff & ~held_word(h, pm, wlo + k); cand; cand &= cand - 1) {
+          const uint32_t g = ((wlo + k) << 6) + (uint32_t)__builtin_ctzll(cand);
+          if (not_lost(s, p, g, tick)) deliveries.push_back({p, g});
+        }
+      }
+      sent.push_back(std::move(st));
     }
   }
-  // sweepGossips (GPI:281-304), physical removal after every member's sends.
-  for (uint32_t s = 0; s < h->N; ++s) {
-    Member& me = h->m[s];
-    if (!me.alive) continue;
-    const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);
-    for (uint32_t gid = h->gbase; gid < gend; ++gid) {
-      const int64_t inf = gossip_find(h, me, gid);
-      if (inf >= 0 && r > inf + sweep) gossip_erase(h, me, gid);
-    }
+  // onGossipReq (GPI:171-183): a new id starts a GossipState with infectionPeriod = r + 1
+  for (const Delivery& d : deliveries) {
+    Member& pm = h->m[d.to];
+    if (gossip_held(h, pm, d.gid)) continue;  // an earlier message of this round brought it
+    gossip_put(h, pm, d.gid, r + 1);
+    h->st.gossip_first_receipts++;
+    const Gossip& g = h->registry[d.gid];
+    auto& slot = h->inbox[d.to][g.subject];  // sink.next -> onMembershipGossip, batched
+    slot = std::max(slot, g.record);
+  }
+  // ... and addToInfected(from) for every message (GPI:181)
+  for (Sent& st : sent) h->m[st.to].recv[st.from].push_back(std::move(st.b));
+  if (q + 1 == h->G) {  // batches that can no longer suppress a send
+    const int64_t keep = r + 1 - h->hzn;
+    for (auto& mm : h->m)
+      for (auto it = mm.recv.begin(); it != mm.recv.end();) {
+        auto& v = it->second;
+        v.erase(std::remove_if(v.begin(), v.end(), [&](const Batch& x) { return x.t < keep; }), v.end());
+        it = v.empty() ? mm.recv.erase(it) : std::next(it);
+      }
   }
   // membership apply of the first receipts (MPI:407-414 -> updateMembership MEMBERSHIP_GOSSIP)
   for (uint32_t p = 0; p < h->N; ++p) {
@@ -739,6 +860,8 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
   h->G = (uint32_t)std::max(1, cfg->ping_interval_ms / cfg->gossip_interval_ms);
   h->S = (uint32_t)std::max(1, cfg->sync_interval_ms / cfg->ping_interval_ms);
   h->TPP = h->G + 4;
+  h->sweepmax = periods_to_sweep(cfg->gossip_repeat_mult, (int32_t)cfg->n_members) + 1;  // others + 1 <= N
+  h->hzn = periods_to_spread(cfg->gossip_repeat_mult, (int32_t)cfg->n_members) + 1;
   h->seed = cfg->seed;
   h->group.assign(h->N, 0);
   std::memset(&h->st, 0, sizeof h->st);
@@ -747,7 +870,7 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
     for (uint32_t i = 0; i < h->N; ++i) {
       h->m[i].table.assign(h->N, SWIM_PACK(0, SWIM_ALIVE));  // converged start, all ALIVE inc 0
       h->m[i].others = h->N - 1;
-      h->m[i].gossips.key.assign(h->rc, EMPTY);
+      h->m[i].gossips.held.assign(h->rc / 64, 0);
       h->m[i].gossips.inf.assign(h->rc, 0);
     }
     h->inbox.resize(h->N);
@@ -791,6 +914,17 @@ int oracle_block_link(oracle_handle* h, uint32_t src, uint32_t dst, int blocked)
   return SWIM_OK;
 }
 
+int oracle_block_inbound(oracle_handle* h, uint32_t dst, uint32_t src, int blocked) {
+  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
+  if (h->inlink.empty()) h->inlink.assign(((uint64_t)h->N * h->N + 7) / 8, 0);
+  uint64_t bit = (uint64_t)dst * h->N + src;
+  if (blocked)
+    h->inlink[bit >> 3] |= (uint8_t)(1u << (bit & 7));
+  else
+    h->inlink[bit >> 3] &= (uint8_t)~(1u << (bit & 7));
+  return SWIM_OK;
+}
+
 int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n) {
   if (!h || (n && !ids)) return SWIM_EINVAL;
   for (uint32_t k = 0; k < n; ++k) {
@@ -800,8 +934,8 @@ int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n) {
     if (!me.alive) continue;
     me.alive = false;
     me.timers.clear();  // its scheduler is gone
-    for (size_t sl = 0; sl < me.gossips.key.size(); ++sl)
-      if (me.gossips.key[sl] != EMPTY) gossip_erase(h, me, me.gossips.key[sl]);
+    while (!me.gossips.order.empty()) gossip_pop_oldest(h, me);
+    me.recv.clear();
     for (uint32_t j = 0; j < h->N; ++j)
       if (j != c && me.table[j] != SWIM_ABSENT) h->pres[j]--;
   }
@@ -912,6 +1046,11 @@ int oracle_is_overrides(uint32_t r1, uint32_t r0) { return is_overrides(r1, r0) 
 
 uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick) {
   return draw(seed, kind, a, b, c, tick);
+}
+
+void oracle_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out4) {
+  const U4 v = draw4(seed, kind, abct[0], abct[1], abct[2], abct[3]);
+  for (int i = 0; i < 4; ++i) out4[i] = v.v[i];
 }
 
 int64_t oracle_cluster_math(int which, int32_t mult, int32_t n, int32_t fanout) {

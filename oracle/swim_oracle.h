@@ -32,6 +32,7 @@ int oracle_destroy(oracle_handle* h);
 int oracle_set_loss(oracle_handle* h, uint32_t loss_bp);
 int oracle_set_partition(oracle_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1);
 int oracle_block_link(oracle_handle* h, uint32_t src, uint32_t dst, int blocked);
+int oracle_block_inbound(oracle_handle* h, uint32_t dst, uint32_t src, int blocked);
 int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_step(oracle_handle* h, uint32_t periods);
 int oracle_drain_events(oracle_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);
@@ -49,6 +50,7 @@ int oracle_debug_member_state(oracle_handle* h, uint32_t* out6n, uint32_t n);
 /* Pure helpers (known-answer tests). */
 int oracle_is_overrides(uint32_t r1, uint32_t r0);
 uint32_t oracle_philox(uint64_t seed, uint32_t kind, uint32_t a, uint32_t b, uint32_t c, uint32_t tick);
+void oracle_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out4);
 /* ClusterMath (ClusterMath.java): which = 0 ceilLog2, 1 gossipPeriodsToSpread,
  * 2 gossipPeriodsToSweep, 3 suspicionTimeout (periods), 4 maxMessagesPerGossipPerNode. */
 int64_t oracle_cluster_math(int which, int32_t mult, int32_t n, int32_t fanout);

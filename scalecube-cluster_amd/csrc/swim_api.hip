@@ -297,6 +297,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_pairwin, dim3(256), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
         if (W > 1) {  // (1) registrations with receivers on other shards
           Ctl c;
@@ -379,6 +380,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
                                h->n_in_pairs);
         }
         timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_record, dim3(256), dim3(256), 0, s, P); });
         timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
         timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_R_C;
@@ -493,7 +495,7 @@ int check_overflow(swim_handle* h) {
     char buf[160];
     std::snprintf(buf, sizeof buf,
                   "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 apply spill list, "
-                  "16 sync bucket, 32 invariant)",
+                  "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping)",
                   ov);
     return fail(h, SWIM_EOVERFLOW, buf);
   }
@@ -568,9 +570,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // inf + sweep + 1 (sweepGossips runs after that round's sends, GossipProtocolImpl.java:150-153),
   // and sweep <= 2 * (rm * bitlen(N) + 1); expiry = inf + sweepmax bounds every holder.
   P.sweepmax = 2u * (P.rm * bitlen(N) + 1u) + 1u;
-  if (P.sweepmax + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
-    std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u rounds > 254)\n", P.rm, N,
-                 P.sweepmax);
+  // infectedFrom horizon: a delivery of round t can suppress sends up to round
+  // t + 1 + gossipPeriodsToSpread
+  P.hzn = P.rm * bitlen(N) + 1u;
+  if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
+    std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
+                 P.rm, N, P.sweepmax, P.hzn);
     free_all(h);
     delete h;
     return SWIM_EINVAL;
@@ -589,6 +594,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.loss_mode = 0;
   P.loss_thr = 0;
   P.link = nullptr;
+  P.inlink = nullptr;
 
   const size_t NN = (size_t)P.nloc * N;  // this shard's rows
   const size_t NL = P.nloc;
@@ -682,6 +688,26 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
+  {  // infectedFrom bookkeeping: in-history rings, delivery records, pruned pairs
+    const uint64_t f = (uint64_t)c.gossip_fanout, W32 = h->GC / 32;
+    // deliveries recorded per round: those whose receiver may select the sender within the
+    // horizon (may_select's reach at a full view), x2 for margin
+    const uint64_t reach = std::min<uint64_t>(N, (uint64_t)(P.hzn + 1) * f * 2 + 64 + 64);
+    const uint64_t rec_round = std::max<uint64_t>(64, 2 * (uint64_t)P.nloc * f * reach / N);
+    P.rcap = pow2ceil(std::max<uint64_t>(4096, rec_round * (P.hzn + 1)));
+    P.bcap = pow2ceil(std::min<uint64_t>(1ull << 30, std::max<uint64_t>(1 << 16, P.rcap * std::max<uint64_t>(1, W32 / 4))));
+    P.spcap = (uint32_t)std::max<uint64_t>(4096, std::min<uint64_t>((uint64_t)P.nloc * f, 65536));
+    P.pwcap = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1 << 16, (uint64_t)P.spcap * (W32 + 4)));
+  }
+  ALLOC(P.ih, NL * IHCAP);
+  ALLOC(P.ih_head, N);
+  ALLOC(P.rec_hdr, P.rcap);
+  ALLOC(P.rec_len, P.rcap);
+  ALLOC(P.rec_body, P.bcap);
+  ALLOC(P.sp_list, P.spcap);
+  ALLOC(P.sp_recs, (size_t)P.spcap * MAXREC);
+  ALLOC(P.pw, P.pwcap);
+  ALLOC(P.rp_list, P.spcap);
   ALLOC(P.ctl, 1);
   ALLOC(P.stat_shards, (size_t)STAT_SHARDS * STAT_STRIDE);
   ALLOC(h->d_digest, 2);
@@ -724,6 +750,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
   {  // every member of this shard starts with others = N - 1
     const uint32_t all = P.nloc;
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);
@@ -773,29 +800,39 @@ int swim_set_partition(swim_handle* h, const uint8_t* group, uint32_t n, uint64_
   return SWIM_OK;
 }
 
-int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked) {
-  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
-  KP& P = h->base;
+namespace {
+// flip one bit of a lazily allocated N x N bitmap on the device
+int set_bitmap_bit(swim_handle* h, const uint8_t** field, uint64_t bit, int on) {
   const size_t bytes = ((size_t)h->N * h->N + 7) / 8;
-  if (!P.link) {
+  if (!*field) {
     uint8_t* l = nullptr;
     int rc = dalloc(h, &l, bytes);
     if (rc) return rc;
     HIPC(h, hipMemsetAsync(l, 0, bytes, h->stream));
-    P.link = l;
+    *field = l;
   }
-  const uint64_t bit = (uint64_t)src * h->N + dst;
   uint8_t byte = 0;
-  uint8_t* dp = const_cast<uint8_t*>(P.link) + (bit >> 3);
+  uint8_t* dp = const_cast<uint8_t*>(*field) + (bit >> 3);
   HIPC(h, hipMemcpyAsync(&byte, dp, 1, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
-  if (blocked)
+  if (on)
     byte |= (uint8_t)(1u << (bit & 7));
   else
     byte &= (uint8_t) ~(1u << (bit & 7));
   HIPC(h, hipMemcpyAsync(dp, &byte, 1, hipMemcpyHostToDevice, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
+}
+}  // namespace
+
+int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked) {
+  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
+  return set_bitmap_bit(h, &h->base.link, (uint64_t)src * h->N + dst, blocked);
+}
+
+int swim_block_inbound(swim_handle* h, uint32_t dst, uint32_t src, int blocked) {
+  if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
+  return set_bitmap_bit(h, &h->base.inlink, (uint64_t)dst * h->N + src, blocked);
 }
 
 int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
@@ -925,7 +962,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->fd_alive_events = stats[ST_FD_ALIVE_EV];
   out->gossips_created = stats[ST_GOSSIPS_CREATED];
   out->gossip_first_receipts = stats[ST_GOSSIP_RECEIPTS];
-  out->gossip_sends = stats[ST_GOSSIP_SENDS];
+  out->gossip_sends = stats[ST_GOSSIP_SENDS] - stats[ST_GOSSIP_SUPP];
   out->syncs_sent = stats[ST_SYNCS_SENT];
   out->syncs_delivered = stats[ST_SYNCS_DELIVERED];
   out->sync_acks_delivered = stats[ST_ACKS_DELIVERED];
@@ -944,6 +981,9 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->gossip_hd_words = stats[ST_G_HDREAD];
   out->gossip_window_words = stats[ST_G_WINW];
   out->gossip_pull_words = stats[ST_G_PULLW];
+  out->infected_pruned_pairs = stats[ST_IF_PAIRS];
+  out->infected_records = stats[ST_IF_RECORDS];
+  out->infected_suppressed = stats[ST_GOSSIP_SUPP];
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];
@@ -984,6 +1024,22 @@ int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t
   if (rc == SWIM_OK) {
     hipLaunchKernelGGL(k_kat_philox, dim3(blocks_for(n, 256)), dim3(256), 0, 0, seed, kind, din, dout, n);
     if (hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = SWIM_EHIP;
+  }
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
+}
+
+int swim_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out4, uint64_t n) {
+  if (!abct || !out4) return SWIM_EINVAL;
+  if (n == 0) return SWIM_OK;
+  uint32_t *din = nullptr, *dout = nullptr;
+  if (hipMalloc(&din, n * 16) != hipSuccess || hipMalloc(&dout, n * 16) != hipSuccess) return SWIM_EHIP;
+  int rc = SWIM_OK;
+  if (hipMemcpy(din, abct, n * 16, hipMemcpyHostToDevice) != hipSuccess) rc = SWIM_EHIP;
+  if (rc == SWIM_OK) {
+    hipLaunchKernelGGL(k_kat_philox4, dim3(blocks_for(n, 256)), dim3(256), 0, 0, seed, kind, din, dout, n);
+    if (hipMemcpy(out4, dout, n * 16, hipMemcpyDeviceToHost) != hipSuccess) rc = SWIM_EHIP;
   }
   (void)hipFree(din);
   (void)hipFree(dout);

@@ -49,6 +49,9 @@ enum StatIdx : int {
   ST_G_HDREAD,
   ST_G_WINW,
   ST_G_PULLW,
+  ST_GOSSIP_SUPP,  // GossipRequests not sent because the peer is in infectedFrom (GPI:248)
+  ST_IF_PAIRS,     // (sender, peer) pairs whose window was pruned by infectedFrom records
+  ST_IF_RECORDS,   // deliveries recorded as infectedFrom sets
   ST_COUNT
 };
 
@@ -59,6 +62,8 @@ enum Overflow : uint32_t {
   OV_SPILL = 8u,  // a receiver spilled more subjects in one round than its LDS spill list holds
   OV_BUCKET = 16u,
   OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
+  OV_IFROM = 64u,  // infectedFrom bookkeeping out of capacity or a delivery predicted never to
+                   // matter did: results would no longer be exact
 };
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
@@ -83,6 +88,11 @@ struct Ctl {
   uint32_t n_inov;      // entries of in_ov this round
   uint32_t pad[2];
   uint32_t bl_hist[32]; // alive members per bit_length(others + 1) (spread/sweep bounds)
+  // infectedFrom bookkeeping: monotone counters of the record pools, and the
+  // pools' fill at the start of each round (mod 256), so an allocation can check that it does
+  // not overwrite a record still inside the horizon
+  uint32_t rec_cnt, body_cnt, sp_cnt, rp_cnt, pw_used, pad2[3];
+  uint32_t rs_rec[256], rs_body[256];
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
 };
@@ -108,7 +118,8 @@ struct KP {
   uint32_t loss_mode; // 0 none, 1 probabilistic, 2 all lost
   uint32_t part_active;
   const uint8_t* group;
-  const uint8_t* link;  // directed block bitmap or nullptr
+  const uint8_t* link;    // outbound block bitmap [src][dst] (send error) or nullptr
+  const uint8_t* inlink;  // inbound block bitmap [dst][src] (silent drop at dst) or nullptr
   // state
   uint32_t* view;
   uint32_t* dl;
@@ -177,6 +188,19 @@ struct KP {
   uint32_t* xs_pend;    // [world][2*nloc] SYNC requests bound for each remote shard
   uint32_t* rs_ref;     // [2N] receiver side: record index of remote request q
   uint32_t* ack_ref;    // [2N] requester side: record index of the SYNC_ACK of remote request q
+  // GossipState.infectedFrom (GossipState.java:17, GossipProtocolImpl.java:181,248), DESIGN.md §3.9
+  uint32_t hzn;        // rounds a delivery can still suppress a send: gossipPeriodsToSpread(N) + 1
+  uint4* ih;           // [nloc][IHCAP] in-history ring: {sender, round, record or NONE, 0}
+  uint32_t* ih_head;   // [N] entries ever appended
+  uint4* rec_hdr;      // [RCAP] delivery records: {deliverer, owner (receiver), round, body offset}
+  uint32_t* rec_len;   // [RCAP] body entries
+  uint2* rec_body;     // [BCAP] {unwrapped bitmap word, gossips of the word delivered}
+  uint32_t rcap, bcap; // powers of two
+  uint4* sp_list;      // [SPCAP] this round's pruned pairs: {sender, peer, records, window offset}
+  uint32_t* sp_recs;   // [SPCAP][MAXREC] their records
+  uint32_t* pw;        // [PWCAP] per pruned pair, its window over this round's active list
+  uint4* rp_list;      // [SPCAP] this round's recorded deliveries: {in_list entry, receiver, record, sender}
+  uint32_t spcap, pwcap;
   Ctl* ctl;
   unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
@@ -189,28 +213,44 @@ constexpr uint32_t REMOTE = 0xFFFFFFFEu;   // req_stage of a request staged on a
 constexpr uint32_t XREC = 0x80000000u;     // in_list entry: a received window record, not a local row
 constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
 constexpr uint32_t NSUM = 1024;  // receipt-summary words per receiver: active lists up to 32,768 words
+constexpr uint32_t SPAIR = 0x40000000u;  // in_list entry: a pruned pair (window in pw), not a member id
+constexpr uint32_t IHCAP = 256;  // in-history entries per member (~f per round over the horizon)
+constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
 
-// partition cut and directed link blocks only (no liveness, no loss draw)
+__device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {
+  return bm && (bm[bit >> 3] & (1u << (bit & 7)));
+}
+
+// Partition cut and directed blocks only (no liveness, no loss draw): can a message src -> dst
+// reach dst's handlers? An outbound block (NetworkEmulator.blockOutbound, :105-119) fails the
+// send; an inbound block at dst (blockInbound, :255-269) drops it silently
+// (NetworkEmulatorTransport.java:73-77). For one-way messages both just lose the message.
 __device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t dst) {
   if (P.part_active && P.group[src] != P.group[dst]) return false;
-  if (P.link) {
-    const uint64_t bit = (uint64_t)src * P.N + dst;
-    if (P.link[bit >> 3] & (1u << (bit & 7))) return false;
-  }
-  return true;
+  if (bit_at(P.link, (uint64_t)src * P.N + dst)) return false;
+  return !bit_at(P.inlink, (uint64_t)dst * P.N + src);
+}
+
+// Sender side (tryFailOutbound, NetworkEmulator.java:166-180): false = the send fails at once
+// (loss draw, blocked destination / partition cut, stopped transport on either end).
+__device__ __forceinline__ bool out_ok(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
+                                       uint32_t tick) {
+  if (!P.alive[src] || !P.alive[dst]) return false;
+  if (P.part_active && P.group[src] != P.group[dst]) return false;
+  if (bit_at(P.link, (uint64_t)src * P.N + dst)) return false;
+  if (P.loss_mode == 0) return true;
+  if (P.loss_mode == 2) return false;
+  return draw1(P.seed, kind, src, dst, c, tick) >= P.loss_thr;
+}
+
+// Receiver side: dst's inbound filter on the message's sender (NetworkEmulatorTransport.java:64-68,73-77).
+__device__ __forceinline__ bool in_ok(const KP& P, uint32_t dst, uint32_t src) {
+  return !bit_at(P.inlink, (uint64_t)dst * P.N + src);
 }
 
 __device__ __forceinline__ bool delivered(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
                                           uint32_t tick) {
-  if (!P.alive[src] || !P.alive[dst]) return false;
-  if (P.part_active && P.group[src] != P.group[dst]) return false;
-  if (P.link) {
-    const uint64_t bit = (uint64_t)src * P.N + dst;
-    if (P.link[bit >> 3] & (1u << (bit & 7))) return false;
-  }
-  if (P.loss_mode == 0) return true;
-  if (P.loss_mode == 2) return false;
-  return draw1(P.seed, kind, src, dst, c, tick) >= P.loss_thr;
+  return out_ok(P, kind, src, dst, c, tick) && in_ok(P, dst, src);
 }
 
 __device__ __forceinline__ uint32_t susp_periods(const KP& P, uint32_t others) { return P.mult * bitlen(others + 1u); }

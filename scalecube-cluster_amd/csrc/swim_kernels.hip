@@ -166,19 +166,21 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
         nB = 1;  // FailureDetectorImpl.java:163-165
       } else {
         preq = 1;
-        bool any_ok = false;
+        uint32_t first = NONE;  // the proxy whose forwarded ack reaches i's transport first
         for (uint32_t q = 0; q < np; ++q) {
           const uint32_t p = proxies[q];
-          if (!delivered(P, K_PING_REQ, i, p, j, P.tick)) {
+          if (!out_ok(P, K_PING_REQ, i, p, j, P.tick)) {
             ++nA;  // NetworkEmulator send error -> immediate SUSPECT
             continue;
           }
           ++nB;
-          if (delivered(P, K_PROXY_PING, p, j, i, P.tick) && delivered(P, K_PROXY_ACK, j, p, i, P.tick) &&
-              delivered(P, K_FWD_ACK, p, i, j, P.tick))
-            any_ok = true;  // first transit ack completes every pending subscription (cid-only match)
+          if (first == NONE && in_ok(P, p, i) && delivered(P, K_PROXY_PING, p, j, i, P.tick) &&
+              delivered(P, K_PROXY_ACK, j, p, i, P.tick) && out_ok(P, K_FWD_ACK, p, i, j, P.tick))
+            first = p;
         }
-        stB = any_ok ? SWIM_ALIVE : SWIM_SUSPECT;
+        // cid-only matching (TransportImpl.java:236-238): that ack completes every pending
+        // subscription, then i's inbound filter on its sender decides (NetworkEmulatorTransport.java:64-68)
+        stB = (first != NONE && in_ok(P, i, first)) ? SWIM_ALIVE : SWIM_SUSPECT;
       }
     }
     // publishPingResult -> onFailureDetectorEvent, sequentially (MembershipProtocolImpl.java:376-404)
@@ -275,6 +277,66 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* to
   return base + x - v;
 }
 
+// ---- GossipState.infectedFrom (GossipState.java:17; GossipProtocolImpl.java:181,248) -------
+// A member never sends gossip g to a peer it received g from during its current GossipState of
+// g. Storing every (member, gossip, sender) triple is out of reach in a storm (~150 senders per
+// held gossip), so the device keeps exactly the part that can matter:
+//   * every member's in-history: the senders that delivered to it in the last hzn rounds;
+//   * for a delivery whose receiver may select its sender as a gossip peer within hzn rounds
+//     (may_select, conservative), a record of the delivered gossips;
+//   * when a member does select such a peer, its window for that peer is pruned by the records
+//     (k_gossip_pairwin); a selected peer in the in-history without a record (a prediction
+//     that failed) raises OV_IFROM instead of silently diverging.
+// hzn = gossipPeriodsToSpread(N) + 1: a record made in round t can only suppress sends in rounds
+// t+1 .. t+1+spread, the last rounds the receiver can still have those gossips in its window.
+__device__ __forceinline__ bool may_select(const KP& P, uint32_t p, uint32_t s) {
+  const uint32_t others = P.cnt[p];
+  if (others < P.f + 64u) return true;  // small views: "select all" is never far away
+  const uint32_t N = P.N;
+  const uint64_t kappa = (2ull * N + others) / (others + 1ull);  // >= 2 positions per present member
+  const uint64_t reach = (uint64_t)(P.hzn + 1u) * P.f * kappa + 64u;
+  if (reach >= N) return true;
+  const uint32_t half = perm_half_bits(N);
+  const uint32_t ep = P.g_epoch[p], cur = P.g_cursor[p];
+  const uint32_t pos = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep));
+  if (pos >= cur && pos - cur < reach) return true;
+  if (cur + reach > N) {  // the cursor may wrap into the next shuffle within the horizon
+    const uint32_t pos1 = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u));
+    if (pos1 < cur + reach - N) return true;
+  }
+  return false;
+}
+
+// position of word offset o (from w_beg) in this round's active list, or NONE (sorted ascending)
+__device__ __forceinline__ uint32_t act_find(const KP& P, uint32_t o, uint32_t n_act) {
+  uint32_t lo = 0, hi = n_act;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((P.act[mid] & ACT_OFF_MASK) < o)
+      lo = mid + 1u;
+    else
+      hi = mid;
+  }
+  return (lo < n_act && (P.act[lo] & ACT_OFF_MASK) == o) ? lo : NONE;
+}
+
+__device__ __forceinline__ uint32_t bytes_sub(uint32_t r, uint32_t d);
+__device__ __forceinline__ uint32_t bytes_gt(uint32_t a, uint32_t t);
+
+// bits of word ws whose current GossipState at member m began no later than round t (a record
+// of round t about them still applies): infection round inf, state created in round inf - 1
+// (or committed for round inf), so (t + 1 - inf) mod 2^8 <= 255 - hzn (swim_create checks that
+// sweepmax + hzn < 256, so the two cases cannot alias)
+__device__ __forceinline__ uint32_t state_since(const KP& P, uint32_t m, uint32_t ws, uint32_t t) {
+  const uint4* dp = reinterpret_cast<const uint4*>(P.hd + lrow(P, m) * P.GC + (size_t)ws * 32u);
+  const uint4 d0 = dp[0], d1 = dp[1];
+  const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+  uint32_t late = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 8u; ++q) late |= bytes_gt(bytes_sub(t + 1u, d32[q]), 255u - P.hzn) << (4u * q);
+  return ~late;
+}
+
 // One workgroup, once per round, before any member acts. Advances the oldest-live pointer (a
 // gossip is dead once every holder has swept it: the last holder got it by wlast) and lists the
 // ACTIVE bitmap words: those where some holder's send window (age <= spread) may be non-empty or
@@ -307,6 +369,11 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     c->glo = lo;
     c->n_alist = 0;
     c->n_inov = 0;
+    c->sp_cnt = 0;
+    c->rp_cnt = 0;
+    c->pw_used = 0;
+    c->rs_rec[P.round & 255u] = c->rec_cnt;
+    c->rs_body[P.round & 255u] = c->body_cnt;
     c->scan_lo = lo;
     c->scan_hi = hi;
     uint32_t blo = 32, bhi = 0;
@@ -398,6 +465,8 @@ constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step 
 
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
+  __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
+  __shared__ uint32_t s_rec[4][MAXF][MAXREC];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t m = P.row0 + blockIdx.x * 4u + w;
@@ -633,15 +702,61 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   // because receivers that already hold a whole word never look at the senders' windows
   const uint32_t alive_peers = (uint32_t)__popcll(__ballot(reg && lane < np && P.alive[s_peers[w][lane]]));
   winbits = wave_sum(winbits);
+  uint32_t entry = m;  // what peer `lane` registers: m, or a pruned pair
+  if (reg) {
+    // GossipState.isInfected (GPI:248): the peers that delivered to m within the horizon, from
+    // m's in-history (newest first, rounds ascending in append order)
+    if (lane < MAXF) s_nrec[w][lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const uint32_t head = P.ih_head[m];
+    const uint32_t nvalid = head < IHCAP ? head : IHCAP;
+    const uint4* ring = P.ih + lrow(P, m) * IHCAP;
+    for (uint32_t b0 = 0; b0 < nvalid; b0 += 64u) {
+      const uint32_t j = b0 + lane;
+      bool young = false;
+      if (j < nvalid) {
+        const uint4 e = ring[(head - 1u - j) & (IHCAP - 1u)];
+        young = e.y + P.hzn >= r;
+        if (young)
+          for (uint32_t q = 0; q < np; ++q)
+            if (s_peers[w][q] == e.x) {
+              if (e.z == NONE) {  // a delivery predicted never to be sent back: cannot stay exact
+                atomicOr(&P.ctl->overflow, OV_IFROM);
+              } else {
+                const uint32_t c = atomicAdd(&s_nrec[w][q], 1u);
+                if (c < MAXREC)
+                  s_rec[w][q][c] = e.z;
+                else
+                  atomicOr(&P.ctl->overflow, OV_IFROM);
+              }
+            }
+      }
+      if (!__any(young)) break;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < np && s_nrec[w][lane]) {  // this pair's window gets pruned (k_gossip_pairwin)
+      const uint32_t nr = s_nrec[w][lane] < MAXREC ? s_nrec[w][lane] : MAXREC;
+      const uint32_t sp = atomicAdd(&P.ctl->sp_cnt, 1u);
+      if (sp < P.spcap) {
+        P.sp_list[sp] = make_uint4(m, s_peers[w][lane], nr, 0u);
+        for (uint32_t c = 0; c < nr; ++c) P.sp_recs[(size_t)sp * MAXREC + c] = s_rec[w][lane][c];
+        entry = SPAIR | sp;
+      } else {
+        atomicOr(&P.ctl->overflow, OV_IFROM);
+      }
+    }
+  }
   if (reg && lane < np) {
     const uint32_t p = s_peers[w][lane];
     if (is_local(P, p)) {
-      register_sender(P, p, m);
+      register_sender(P, p, entry);
     } else {  // the window travels to p's shard (k_gossip_pack / k_gossip_unpack)
       const uint32_t dst = p / P.nloc;
       const uint32_t o = atomicAdd(&P.ctl->xg_cnt[dst], 1u);
       uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + o);
-      e[0] = m;
+      e[0] = entry;
       e[1] = p;
     }
   }
@@ -655,6 +770,131 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
 }
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
+
+// member m's start-of-round send window at active-list position k, as k_gossip_pull reads it
+__device__ __forceinline__ uint32_t own_window(const KP& P, uint32_t m, uint32_t k, uint32_t w_beg, uint32_t lo,
+                                               uint32_t hi) {
+  const uint32_t ea = P.act[k];
+  const uint32_t wc = (ea >> 26) & 3u;
+  if (wc == WC_NONE) return 0u;
+  const uint32_t W32 = P.GC >> 5;
+  const uint32_t wi = w_beg + (ea & ACT_OFF_MASK);
+  if (wc == WC_ALL) return P.hb[lrow(P, m) * W32 + (wi & (W32 - 1u))] & range_mask(wi << 5, lo, hi);
+  return P.wb[lrow(P, m) * W32 + k];
+}
+
+// One wave per pruned pair (sender m, peer x) of this round: m's window, minus every gossip x
+// delivered to m (a record of round t) during m's current GossipState of it
+// (selectGossipsToSend's !isInfected filter, GossipProtocolImpl.java:245-250). The pruned
+// window goes to pw, where k_gossip_pull (or the shard exchange) reads it instead of wb/hb.
+__global__ void __launch_bounds__(256) k_gossip_pairwin(KP P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t n4 = (n_act + 3u) & ~3u;  // 16-B aligned windows (k_gossip_pull reads quads)
+  const uint32_t W32 = P.GC >> 5;
+  uint32_t removed_alive = 0, pairs = 0;
+  for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+    const uint4 sp = P.sp_list[i];
+    const uint32_t m = sp.x, x = sp.y;
+    uint32_t off = 0;
+    if (lane == 0) off = atomicAdd(&P.ctl->pw_used, n4);
+    off = __shfl(off, 0, 64);
+    if (off + n4 > P.pwcap || off + n4 < off) {
+      if (lane == 0) atomicOr(&P.ctl->overflow, OV_IFROM);
+      continue;
+    }
+    if (lane == 0) P.sp_list[i].w = off;
+    uint32_t* pwr = P.pw + off;
+    for (uint32_t k = lane; k < n4; k += 64u) pwr[k] = k < n_act ? own_window(P, m, k, w_beg, lo, hi) : 0u;
+    __threadfence();  // the plain stores reach L2 before the atomics below
+    uint32_t removed = 0;
+    for (uint32_t j = 0; j < sp.z; ++j) {
+      const uint32_t rec = P.sp_recs[(size_t)i * MAXREC + j];
+      const uint4 hdr = P.rec_hdr[rec & (P.rcap - 1u)];
+      const uint32_t len = P.rec_len[rec & (P.rcap - 1u)];
+      for (uint32_t e = lane; e < len; e += 64u) {
+        const uint2 ent = P.rec_body[(hdr.w + e) & (P.bcap - 1u)];
+        if (ent.x < w_beg) continue;  // every holder has swept the word
+        const uint32_t k = act_find(P, ent.x - w_beg, n_act);
+        if (k == NONE || ((P.act[k] >> 26) & 3u) == WC_NONE) continue;  // nobody's window
+        const uint32_t supp = ent.y & state_since(P, m, ent.x & (W32 - 1u), hdr.z);
+        if (supp) removed += (uint32_t)__popc(atomicAnd(&pwr[k], ~supp) & supp);
+      }
+    }
+    if (P.alive[x]) removed_alive += removed;  // the send counter covers alive peers only
+    pairs += lane == 0 ? 1u : 0u;
+  }
+  add_stat(P, ST_GOSSIP_SUPP, removed_alive);
+  add_stat(P, ST_IF_PAIRS, pairs);
+}
+
+// word k of a delivery record: what sender entry `sreg` delivered to p this round at active
+// position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull)
+__device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, uint32_t sid, uint32_t p, uint32_t k,
+                                                   uint32_t w_beg, uint32_t lo, uint32_t hi, uint32_t* wi_out) {
+  const uint32_t ea = P.act[k];
+  const uint32_t W32 = P.GC >> 5;
+  const uint32_t wi = w_beg + (ea & ACT_OFF_MASK);
+  *wi_out = wi;
+  if (((ea >> 26) & 3u) == WC_NONE) return 0u;
+  uint32_t v;
+  if (sreg & XREC)
+    v = remote_window(P, sreg & ~XREC, k);
+  else if (sreg & SPAIR)
+    v = P.pw[P.sp_list[sreg & ~SPAIR].w + k];
+  else
+    v = own_window(P, sreg, k, w_beg, lo, hi);
+  if (v && P.loss_mode == 1u) {
+    uint32_t need = v;
+    v = 0u;
+    while (need) {
+      const uint32_t b = (uint32_t)__builtin_ctz(need);
+      need &= need - 1u;
+      if (draw1(P.seed, K_GOSSIP, sid, p, P.g_hash[(wi & (W32 - 1u)) * 32u + b], P.tick) >= P.loss_thr) v |= 1u << b;
+    }
+  }
+  return v;
+}
+
+// One wave per recorded delivery of this round (chosen in k_gossip_pull): the receiver's
+// addToInfected(sender) for every gossip delivered (GossipProtocolImpl.java:181), stored sparse as
+// (word, bits) in the record pool. Runs before k_gossip_apply changes any holdings.
+__global__ void __launch_bounds__(256) k_gossip_record(KP P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n = P.ctl->rp_cnt < P.spcap ? P.ctl->rp_cnt : P.spcap;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  const uint32_t r = P.round;
+  uint32_t nrec = 0;
+  for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+    const uint4 rp = P.rp_list[i];  // {in_list entry, receiver, record, sender id}
+    uint32_t cnt = 0, wi;
+    for (uint32_t k = lane; k < n_act; k += 64u) cnt += delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi) ? 1u : 0u;
+    const uint32_t total = wave_sum(cnt);
+    uint32_t off = 0;
+    if (lane == 0) off = atomicAdd(&P.ctl->body_cnt, total);
+    off = __shfl(off, 0, 64);
+    // the records still inside the horizon start at rs_body of round r - hzn
+    if (off + total - P.ctl->rs_body[(r - P.hzn) & 255u] > P.bcap) {
+      if (lane == 0) atomicOr(&P.ctl->overflow, OV_IFROM);
+      continue;
+    }
+    uint32_t base = 0;
+    for (uint32_t k0 = 0; k0 < n_act; k0 += 64u) {
+      const uint32_t k = k0 + lane;
+      const uint32_t v = k < n_act ? delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi) : 0u;
+      const unsigned long long b = __ballot(v != 0u);
+      if (v) P.rec_body[(off + base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))) & (P.bcap - 1u)] = make_uint2(wi, v);
+      base += (uint32_t)__popcll(b);
+    }
+    if (lane == 0) {
+      P.rec_hdr[rp.z & (P.rcap - 1u)].w = off;
+      P.rec_len[rp.z & (P.rcap - 1u)] = total;
+    }
+    nrec += lane == 0 ? 1u : 0u;
+  }
+  add_stat(P, ST_IF_RECORDS, nrec);
+}
 
 // One wave per receiver p: spreadGossipsTo (GossipProtocolImpl.java:215-251) seen from the
 // receiving side. Every sender that picked p sends each gossip of its start-of-round window as
@@ -671,6 +911,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
+  __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
@@ -688,6 +929,9 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
+    uint32_t ihh = P.ih_head[p];  // in-history appends of this receiver (wave-uniform)
+    uint4* ring = P.ih + lrow(P, p) * IHCAP;
+    const uint32_t r = P.round;
     for (uint32_t done = 0; done < deg;) {
       const bool first_chunk = done == 0;  // later chunks only add gossips earlier ones did not bring
       // next chunk of senders: lane q holds sender q
@@ -716,12 +960,46 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       done += cdeg;
       // an entry is a local sender's member id, or XREC | index of a pair received from the
       // sender's shard (its window words arrive sparse, see k_gossip_need)
-      const uint32_t sid = lane < cdeg ? ((sreg & XREC) ? P.rpairs[2 * (sreg & ~XREC)] : sreg) : 0u;
+      uint32_t sid = 0, pwo = 0;
+      if (lane < cdeg) {
+        if (sreg & XREC) {
+          sid = P.rpairs[2 * (sreg & ~XREC)];
+        } else if (sreg & SPAIR) {
+          const uint4 sp = P.sp_list[sreg & ~SPAIR];
+          sid = sp.x;
+          pwo = sp.w;
+        } else {
+          sid = sreg;
+        }
+      }
       const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sid, p);
       const unsigned long long reach = __ballot(ok_l);
+      {  // infectedFrom: every sender whose messages can arrive joins p's in-history; a delivery
+         // p may send gossips back to within the horizon is recorded (k_gossip_record)
+        uint32_t rec = NONE;
+        if (ok_l && may_select(P, p, sid)) {
+          rec = atomicAdd(&P.ctl->rec_cnt, 1u);
+          const uint32_t o = atomicAdd(&P.ctl->rp_cnt, 1u);
+          if (rec + 1u - P.ctl->rs_rec[(r - P.hzn) & 255u] > P.rcap || o >= P.spcap) {
+            atomicOr(&P.ctl->overflow, OV_IFROM);
+          } else {
+            P.rec_hdr[rec & (P.rcap - 1u)] = make_uint4(sid, p, r, 0u);
+            P.rec_len[rec & (P.rcap - 1u)] = 0u;
+            P.rp_list[o] = make_uint4(sreg, p, rec, sid);
+          }
+        }
+        if (ok_l) {
+          const uint32_t pos = ihh + (uint32_t)__popcll(reach & ((1ull << lane) - 1ull));
+          uint4* slot = ring + (pos & (IHCAP - 1u));
+          if (pos >= IHCAP && (*slot).y + P.hzn >= r) atomicOr(&P.ctl->overflow, OV_IFROM);
+          *slot = make_uint4(sid, r, rec, 0u);
+        }
+        ihh += (uint32_t)__popcll(reach);
+      }
       uint32_t* snd = s_snd[threadIdx.x >> 6];
       snd[lane] = sreg;
       s_sid[threadIdx.x >> 6][lane] = sid;
+      s_pwo[threadIdx.x >> 6][lane] = pwo;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       // lane takes an aligned quad of list entries (k_gossip_prep pads the list into quads of
@@ -771,7 +1049,10 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
             const uint32_t en = has ? snd[q0 + j] : 0u;
             mv[j] = has ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
             uint4 wa = make_uint4(0u, 0u, 0u, 0u), wm = make_uint4(0u, 0u, 0u, 0u);
-            if (has && !(en & XREC) && quad) {
+            if (has && (en & SPAIR)) {  // pruned pair: its window was written to pw
+              const uint32_t* pwr = P.pw + s_pwo[threadIdx.x >> 6][q0 + j];
+              wm = *reinterpret_cast<const uint4*>(pwr + kq);  // act-indexed, padded to quads
+            } else if (has && !(en & XREC) && quad) {
               if (anyall) wa = *reinterpret_cast<const uint4*>(P.hb + lrow(P, en) * W32 + ws0);
               if (anymix) wm = *reinterpret_cast<const uint4*>(P.wb + lrow(P, en) * W32 + kq);
             }
@@ -782,6 +1063,8 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
               if (has && ((todo >> i) & 1u)) {
                 if (en & XREC)
                   v = remote_window(P, en & ~XREC, kq + i);
+                else if (en & SPAIR)
+                  v = wma[i];
                 else if (quad)
                   v = wcv[i] == WC_ALL ? waa[i] & live[i] : wma[i];
                 else
@@ -825,6 +1108,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
+    if (lane == 0) P.ih_head[p] = ihh;
     const uint32_t total = wave_sum(receipts);
     if (lane == 0 && total) {
       const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);
@@ -1095,7 +1379,7 @@ __global__ void k_gossip_pack_pairs(KP P, uint32_t n_rec) {
   uint32_t dst, i;
   if (g < n_rec && xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) {
     const uint32_t* e = P.xg_pend + 2 * ((size_t)dst * P.nloc * P.f + i);
-    P.xsend[2 * g] = e[0];
+    P.xsend[2 * g] = (e[0] & SPAIR) ? P.sp_list[e[0] & ~SPAIR].x : e[0];
     P.xsend[2 * g + 1] = e[1];
   }
 }
@@ -1125,6 +1409,9 @@ __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uin
       P.rpairs[2 * i + 1] = p;
     }
     const uint32_t* hbr = P.hb + lrow(P, p) * W32;
+    // a delivery p will record (infectedFrom, k_gossip_record) needs the whole window
+    const bool all = P.alive[p] && P.loss_mode != 2u && link_open(P, P.xrecv[2 * i], p) &&
+                     may_select(P, p, P.xrecv[2 * i]);
     uint32_t cnt[4], pre[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4u; ++j) {
@@ -1138,7 +1425,7 @@ __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uin
           if (((e >> 26) & 3u) == WC_NONE) continue;
           const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
           const uint32_t live = range_mask(wi << 5, lo, hi);
-          if ((hbr[wi & (W32 - 1u)] & live) != live) bits |= 1u << b;
+          if (all || (hbr[wi & (W32 - 1u)] & live) != live) bits |= 1u << b;
         }
       if (t < nneed) {
         P.rneed[(size_t)i * nneed + t] = bits;
@@ -1175,7 +1462,9 @@ __global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pai
   for (uint32_t g = blockIdx.x; g < n_pairs; g += gridDim.x) {
     uint32_t dst, i;
     if (!xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) break;
-    const uint32_t m = P.xg_pend[2 * ((size_t)dst * P.nloc * P.f + i)];
+    const uint32_t ent = P.xg_pend[2 * ((size_t)dst * P.nloc * P.f + i)];
+    const uint32_t m = (ent & SPAIR) ? P.sp_list[ent & ~SPAIR].x : ent;
+    const uint32_t* pwr = (ent & SPAIR) ? P.pw + P.sp_list[ent & ~SPAIR].w : nullptr;  // pruned window
     const uint32_t* wbr = P.wb + lrow(P, m) * W32;
     const uint32_t* hbr = P.hb + lrow(P, m) * W32;
     uint32_t nv[4], cnt[4], pre[4];
@@ -1197,7 +1486,7 @@ __global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pai
         const uint32_t k = 32u * (4u * threadIdx.x + j) + b;
         const uint32_t e = P.act[k];
         const uint32_t wc = (e >> 26) & 3u, wi = w_beg + (e & ACT_OFF_MASK);
-        out[o++] = wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi) : wbr[k];
+        out[o++] = pwr ? pwr[k] : (wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi) : wbr[k]);
       }
     }
   }
@@ -1671,6 +1960,17 @@ __global__ void k_digest(const uint32_t* view, const uint32_t* dl, uint32_t N, u
 __global__ void k_kat_overrides(const uint32_t* r1, const uint32_t* r0, uint8_t* out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = is_overrides(r1[i], r0[i]) ? 1 : 0;
+}
+
+__global__ void k_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const u32x4 v = draw4(seed, kind, abct[4 * i], abct[4 * i + 1], abct[4 * i + 2], abct[4 * i + 3]);
+    out[4 * i] = v.x;
+    out[4 * i + 1] = v.y;
+    out[4 * i + 2] = v.z;
+    out[4 * i + 3] = v.w;
+  }
 }
 
 __global__ void k_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out, uint64_t n) {

@@ -127,6 +127,24 @@ __host__ __device__ __forceinline__ uint32_t perm_apply(uint32_t x, uint32_t n, 
   return x;
 }
 
+// inverse of perm_apply: the position of member y in the keyed shuffle. The cycle walk of the
+// forward map only passes through values >= n, so walking the inverse rounds back from y stops
+// exactly at the position that maps to y.
+__host__ __device__ __forceinline__ uint32_t perm_inverse(uint32_t y, uint32_t n, uint32_t half, const PermKey& key) {
+  const uint32_t mask = (1u << half) - 1u;
+  do {
+    uint32_t L = y >> half, R = y & mask;
+#pragma unroll
+    for (int r = 3; r >= 0; --r) {
+      const uint32_t pl = R ^ (fmix32(L ^ key.k[r]) & mask);
+      R = L;
+      L = pl;
+    }
+    y = (L << half) | R;
+  } while (y >= n);
+  return y;
+}
+
 // ClusterMath.ceilLog2 (ClusterMath.java:133-135): 32 - numberOfLeadingZeros(num)
 __host__ __device__ __forceinline__ uint32_t bitlen(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 0u; }
 

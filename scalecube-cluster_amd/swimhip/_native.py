@@ -101,6 +101,9 @@ STAT_FIELDS = [
     "gossip_hd_words",
     "gossip_window_words",
     "gossip_pull_words",
+    "infected_pruned_pairs",
+    "infected_records",
+    "infected_suppressed",
 ]
 
 
@@ -143,6 +146,7 @@ def api_table(prefix: str):
         (prefix + "set_loss", _I, [_P, _U32]),
         (prefix + "set_partition", _I, [_P, _pU8, _U32, _U64, _U64]),
         (prefix + "block_link", _I, [_P, _U32, _U32, _I]),
+        (prefix + "block_inbound", _I, [_P, _U32, _U32, _I]),
         (prefix + "crash", _I, [_P, _pU32, _U32]),
         (prefix + "step", _I, [_P, _U32]),
         (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
@@ -160,6 +164,7 @@ SWIM_ONLY = [
     ("swim_last_error", ctypes.c_char_p, [_P]),
     ("swim_kat_is_overrides", _I, [_pU32, _pU32, _pU8, _U64]),
     ("swim_kat_philox", _I, [_U64, _U32, _pU32, _pU32, _U64]),
+    ("swim_kat_philox4", _I, [_U64, _U32, _pU32, _pU32, _U64]),
     ("swim_debug_holdings", _I, [_P, _U32, _pU32, _pU32, _U32, _pU32]),
     ("swim_debug_member_state", _I, [_P, _pU32, _U32]),
     ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),

@@ -134,7 +134,8 @@ class SwimCluster:
         self._call("set_partition", self._h, g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), self.n, t0, t1)
 
     def block_outbound(self, src: int, dsts, blocked: bool = True):
-        """NetworkEmulator.blockOutbound(Address...) (NetworkEmulator.java:105-119)."""
+        """NetworkEmulator.blockOutbound(Address...) (NetworkEmulator.java:105-119): a send from
+        src to a blocked destination fails immediately (tryFailOutbound, :166-180)."""
         for d in dsts:
             self._call("block_link", self._h, int(src), int(d), 1 if blocked else 0)
 
@@ -142,9 +143,14 @@ class SwimCluster:
         self.block_outbound(src, dsts, blocked=False)
 
     def block_inbound(self, dst: int, srcs, blocked: bool = True):
-        """NetworkEmulator.blockInbound (NetworkEmulator.java:255-269): drops by sender."""
+        """NetworkEmulator.blockInbound (NetworkEmulator.java:255-269): dst silently drops every
+        message whose sender is in srcs (NetworkEmulatorTransport.java:66-68,73-77); the sender's
+        send succeeds, unlike an outbound block."""
         for s in srcs:
-            self._call("block_link", self._h, int(s), int(dst), 1 if blocked else 0)
+            self._call("block_inbound", self._h, int(dst), int(s), 1 if blocked else 0)
+
+    def unblock_inbound(self, dst: int, srcs):
+        self.block_inbound(dst, srcs, blocked=False)
 
     def crash(self, ids):
         ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))

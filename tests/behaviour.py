@@ -229,6 +229,119 @@ def mp_long_partition_then_removed(make):
     assert_suspected(c, D)
 
 
+# -- MembershipProtocolTest, inbound-only blocks (:681-918) --------------------------------
+# (testNodeJoinClusterWithNoInbound / ...ThenInboundRecover, :597-679, start members that join
+# through INITIAL_SYNC; the simulator's members start converged, so those two are not restated.)
+def seeds_a_config(n):
+    """The inbound tests wire b and c with seed a only (createMembership(x, [a.address()]))."""
+    return membership_test_config(n).membership(lambda o: o.seedMembers([A]))
+
+
+def block_all_inbound(c, dst):
+    """NetworkEmulator.blockAllInbound (:237-242) of member dst."""
+    c.block_inbound(dst, [x for x in range(c.n) if x != dst])
+
+
+def unblock_all_inbound(c, dst):
+    c.unblock_inbound(dst, [x for x in range(c.n) if x != dst])
+
+
+def removed_by(c):
+    out = {}
+    for e in c.events():
+        if e.isRemoved():
+            out.setdefault(e.observer, set()).add(e.member)
+    return out
+
+
+def mp_partition_no_inbound_then_removed(make, recover=False):
+    """testNetworkPartitionDueNoInboundThenRemoved (:681-720): c drops every inbound message; a
+    and b remove c, c removes a and b, and nobody stays suspected. With recover=True,
+    testNetworkPartitionDueNoInboundUntilRemovedThenInboundRecover (:722-775): after unblocking,
+    SYNC to the seed brings all three back."""
+    c = make(seeds_a_config(3), 3, 31 if not recover else 32)
+    c.step(seconds(3))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+    c.events()
+    block_all_inbound(c, C)
+    c.step(await_suspicion(3))
+    assert_trusted(c, A, B)
+    assert_suspected(c, A)
+    assert_trusted(c, B, A)
+    assert_suspected(c, B)
+    assert_trusted(c, C)
+    assert_suspected(c, C)
+    rem = removed_by(c)
+    assert rem.get(A) == {C} and rem.get(B) == {C} and rem.get(C) == {A, B}, rem
+    if recover:
+        unblock_all_inbound(c, C)
+        c.step(seconds(3))
+        for m in (A, B, C):
+            assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+            assert_suspected(c, m)
+
+
+def mp_partition_no_inbound_then_recover(make):
+    mp_partition_no_inbound_then_removed(make, recover=True)
+
+
+def mp_between_two_members(make, mode):
+    """testNetworkPartitionBetweenTwoMembersDueNoInbound / NoOutbound / NoTrafficAtAll
+    (:777-851): c blocks b's inbound, outbound or both; ping-req through a keeps everyone
+    trusted for a whole suspicion timeout."""
+    c = make(seeds_a_config(3), 3, {"in": 33, "out": 34, "both": 35}[mode])
+    c.step(seconds(3))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+    if mode in ("in", "both"):
+        c.block_inbound(C, [B])
+    if mode in ("out", "both"):
+        c.block_outbound(C, [B])
+    c.step(await_suspicion(3))
+    for m in (A, B, C):
+        assert_trusted(c, m, *[x for x in (A, B, C) if x != m])
+
+
+def mp_between_two_members_no_inbound(make):
+    mp_between_two_members(make, "in")
+
+
+def mp_between_two_members_no_outbound(make):
+    mp_between_two_members(make, "out")
+
+
+def mp_between_two_members_no_traffic(make):
+    mp_between_two_members(make, "both")
+
+
+def mp_partition_many_no_inbound_then_recover(make):
+    """testNetworkPartitionManyDueNoInboundThenRemovedThenRecover (:853-918): all four drop all
+    inbound, suspect then remove each other, then recover once unblocked."""
+    c = make(membership_test_config(4), 4, 36)
+    c.step(seconds(1))
+    for m in (A, B, C, D):
+        assert_trusted(c, m, *[x for x in (A, B, C, D) if x != m])
+        assert_suspected(c, m)
+    c.events()
+    for m in (A, B, C, D):
+        block_all_inbound(c, m)
+    c.step(seconds(2))
+    for m in (A, B, C, D):
+        assert_trusted(c, m)
+        assert_suspected(c, m, *[x for x in (A, B, C, D) if x != m])
+    c.step(await_suspicion(4))
+    rem = removed_by(c)
+    for m in (A, B, C, D):
+        assert rem.get(m) == {x for x in (A, B, C, D) if x != m}, rem
+    for m in (A, B, C, D):
+        unblock_all_inbound(c, m)
+    c.step(seconds(3))
+    for m in (A, B, C, D):
+        assert_trusted(c, m, *[x for x in (A, B, C, D) if x != m])
+        assert_suspected(c, m)
+
+
 def gossip_dissemination_bound(make):
     """GossipProtocolTest (:48-64, :154-161) restated on membership gossip: the SUSPECT gossip
     about a crashed member reaches every alive member within gossipTimeoutToSweep rounds, with
@@ -255,5 +368,7 @@ ALL = [
     fd_trusted, fd_suspected, fd_trusted_despite_bad_network,
     mp_initial_phase_ok, mp_partition_no_outbound_then_recover, mp_member_lost_network_then_recover,
     mp_partition_twice_then_recover, mp_network_lost_on_all_nodes_then_recover, mp_long_partition_then_removed,
+    mp_partition_no_inbound_then_removed, mp_partition_no_inbound_then_recover, mp_between_two_members_no_inbound,
+    mp_between_two_members_no_outbound, mp_between_two_members_no_traffic, mp_partition_many_no_inbound_then_recover,
     gossip_dissemination_bound,
 ]

@@ -14,7 +14,7 @@ PARITY_KEYS = [
     "period", "fd_probes", "fd_direct_ok", "fd_ping_req", "fd_suspect_events", "fd_alive_events",
     "gossips_created", "gossip_first_receipts", "gossip_sends", "syncs_sent", "syncs_delivered",
     "sync_acks_delivered", "records_accepted", "events_added", "events_removed", "suspicion_timeouts",
-    "refutations", "not_converged",
+    "refutations", "not_converged", "infected_suppressed",
 ]
 
 
@@ -75,6 +75,38 @@ def _links(c):
         yield
 
 
+def _asym_partition(c, k, t0, length, after, loss):
+    # A small group {0..k-1} cut off past the suspicion timeout, with message loss: the small
+    # side's view sizes (and with them gossipPeriodsToSpread / ToSweep, ClusterMath.java:99-113)
+    # drop below the large side's, so a sender can still spread a gossip that the peer it got it
+    # from has already swept. GossipState.infectedFrom (GossipProtocolImpl.java:181,248) keeps it
+    # from re-infecting that peer; the round-1 oracle, which ignored infectedFrom, diverged here
+    # (first at period 22: 13,176 vs 13,174 first receipts).
+    c.set_loss(loss)
+    c.partition((np.arange(c.n) >= k).astype(np.uint8), t0, t0 + length)
+    for _ in range(t0 + length + after):
+        c.step(1)
+        yield
+
+
+def _inbound(c):
+    # NetworkEmulator.blockInbound (NetworkEmulator.java:255-269): member 3 drops everything
+    # (blockAllInbound) for 20 periods, member 5 drops member 6's messages, member 9 drops
+    # member 0's; an inbound block lets the sender's send succeed, so ping-req subscriptions stay
+    # pending instead of failing at once (FailureDetectorImpl.java:183-208).
+    c.block_inbound(3, [x for x in range(c.n) if x != 3])
+    c.block_inbound(5, [6])
+    c.block_inbound(9, [0])
+    c.block_outbound(11, [12])
+    for _ in range(20):
+        c.step(1)
+        yield
+    c.unblock_inbound(3, [x for x in range(c.n) if x != 3])
+    for _ in range(12):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -87,6 +119,12 @@ SCENARIOS = {
         64, 5, lambda c: _partition_heal(c, 2, 30, 25)),
     "local48_links": (ClusterConfig.defaultLocalConfig(), 48, 6, _links),
     "lan1024_loss5_crash10": (ClusterConfig.defaultLanConfig(), 1024, 7, lambda c: _lan_loss(c, 10, 30, 5.0)),
+    "local32_asym_partition_loss20": (
+        ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers(list(range(32))).syncInterval(2000)),
+        32, 0, lambda c: _asym_partition(c, 6, 2, 25, 20, 20.0)),
+    "local24_inbound_blocks": (
+        ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers([0, 1]).syncInterval(2000)),
+        24, 8, _inbound),
 }
 
 
