@@ -78,6 +78,15 @@ def kernel_bytes(name, d, n):
         return 4 * d["sweep_cells"]
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
         return 24 * d["fd_probes"]
+    # infectedFrom bookkeeping: in-history ring entries (16 B per registration,
+    # ~gossip_probes / words per registration is not tracked, so per probe), pruned windows and
+    # dense delivery records (a window word read + a word written per active position)
+    if name == "k_gossip_inhist":  # in_list entry + ring entry per registered sender
+        return 20 * d["fd_probes"] * 3
+    if name == "k_gossip_pairwin":
+        return 12 * d["infected_pruned_pairs"] * max(1, d["gossip_scanned"] // max(1, d["fd_probes"]))
+    if name == "k_gossip_record":
+        return 12 * d["infected_records"] * max(1, d["gossip_scanned"] // max(1, d["fd_probes"]))
     return 0
 
 
@@ -291,7 +300,8 @@ def main():
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
-                                   "gossip_pull_words", "gossip_probes", "events_removed")},
+                                   "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
+                                   "infected_suppressed", "infected_pruned_pairs", "infected_records")},
     }
     c.close()
     if rank == 0 and not args.no_cpu_baseline:

@@ -240,8 +240,9 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
 int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n);
 
 /* Kernel timing for the bench: the last step's per-kernel-class device time (ms, HIP events
- * on the handle's stream). idx: 0 fd, 1 gossip_send, 2 gossip_apply, 3 suspicion, 4 sync_merge,
- * 5 sync_ack. Returns accumulated time since the last reset. */
+ * on the handle's stream). idx: 0 fd, 1 gossip_pull, 2 gossip_apply, 3 suspicion, 4 sync_merge,
+ * 5 sync_ack, 6 sync_snapshot, 7 bookkeeping, 8 gossip_select, 9 gossip_inhist, 10 gossip_pairwin
+ * (fill + prune), 11 gossip_record. Returns accumulated time since the last reset. */
 int swim_kernel_time(swim_handle* h, uint32_t idx, double* ms, uint64_t* launches);
 int swim_kernel_time_reset(swim_handle* h, int enable);
 

@@ -175,6 +175,12 @@ struct GossipMap {
   std::vector<uint64_t> held;                        // rc bits
   std::vector<int64_t> inf;                          // rc slots
   std::deque<std::pair<uint32_t, int64_t>> order;    // (gid, infectionPeriod), oldest first
+  // selectGossipsToSend's age filter as a bitset (rc bits): the window is the run of `order`
+  // with infectionPeriod in [r - spread, r], positions [w_lo, w_end) counted from the first
+  // entry ever held (`popped` entries have left the front), kept up to date round by round
+  std::vector<uint64_t> win;
+  uint64_t popped = 0, w_lo = 0, w_end = 0;
+  int32_t w_spread = -1;
 };
 
 // GossipState.infected (GossipState.java:17; addToInfected GossipProtocolImpl.java:181): the
@@ -234,7 +240,7 @@ struct oracle_handle {
   swim_stats st;
   std::vector<uint32_t> pres, last_removed;
   // pending gossip-delivered records per receiver: subject -> lattice max
-  std::vector<std::map<uint32_t, uint32_t>> inbox;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> inbox;
 };
 
 namespace {
@@ -324,23 +330,25 @@ void gossip_reserve(oracle_handle* h, uint32_t gend) {
   while (2ull * (gend - h->gbase) + 256 > nrc) nrc *= 2;
   for (auto& mm : h->m) {
     GossipMap& g = mm.gossips;
-    std::vector<uint64_t> nh(nrc / 64, 0);
+    std::vector<uint64_t> nh(nrc / 64, 0), nw(nrc / 64, 0);
     std::vector<int64_t> ni(nrc, 0);
-    for (const auto& e : g.order) {
+    for (size_t k = 0; k < g.order.size(); ++k) {
+      const auto& e = g.order[k];
       const uint32_t sl = e.first & (nrc - 1);
       nh[sl >> 6] |= 1ull << (sl & 63);
       ni[sl] = e.second;
+      if (g.popped + k >= g.w_lo && g.popped + k < g.w_end) nw[sl >> 6] |= 1ull << (sl & 63);
     }
     g.held.swap(nh);
     g.inf.swap(ni);
+    g.win.swap(nw);
   }
   h->rc = nrc;
 }
 
 // gossips.put(id, new GossipState(gossip, inf)) (GossipProtocolImpl.java:166-167,177-178) for a
-// gossip the member does not hold
+// gossip the member does not hold (the ring already has room for gid)
 void gossip_put(oracle_handle* h, Member& me, uint32_t gid, int64_t inf) {
-  gossip_reserve(h, gid + 1);
   const uint32_t sl = gid & (h->rc - 1);
   me.gossips.held[sl >> 6] |= 1ull << (sl & 63);
   me.gossips.inf[sl] = inf;
@@ -350,11 +358,35 @@ void gossip_put(oracle_handle* h, Member& me, uint32_t gid, int64_t inf) {
 
 // gossips.remove(id) of the oldest held gossip (sweepGossips, GossipProtocolImpl.java:297-298)
 void gossip_pop_oldest(oracle_handle* h, Member& me) {
-  const uint32_t gid = me.gossips.order.front().first;
+  GossipMap& g = me.gossips;
+  const uint32_t gid = g.order.front().first;
   const uint32_t sl = gid & (h->rc - 1);
-  me.gossips.held[sl >> 6] &= ~(1ull << (sl & 63));
-  me.gossips.order.pop_front();
+  g.held[sl >> 6] &= ~(1ull << (sl & 63));
+  if (g.popped >= g.w_lo && g.popped < g.w_end) {  // still in the window bitset
+    g.win[sl >> 6] &= ~(1ull << (sl & 63));
+    g.w_lo = g.popped + 1;
+  }
+  g.order.pop_front();
+  g.popped++;
+  g.w_lo = std::max(g.w_lo, g.popped);
+  g.w_end = std::max(g.w_end, g.w_lo);
   h->registry[gid].holders--;
+}
+
+// Bring the window bitset to round r: gossips with infectionPeriod in [r - spread, r] (GPI:247).
+void window_update(oracle_handle* h, GossipMap& g, int64_t r, int32_t spread) {
+  auto flip = [&](uint64_t pos) {
+    const uint32_t sl = g.order[pos - g.popped].first & (h->rc - 1);
+    g.win[sl >> 6] ^= 1ull << (sl & 63);
+  };
+  if (spread != g.w_spread) {  // view size changed ClusterMath's spread: rebuild
+    for (uint64_t k = g.w_lo; k < g.w_end; ++k) flip(k);
+    g.w_lo = g.w_end = g.popped;
+    g.w_spread = spread;
+  }
+  const uint64_t end = g.popped + g.order.size();
+  while (g.w_end < end && g.order[g.w_end - g.popped].second <= r) flip(g.w_end++);
+  while (g.w_lo < g.w_end && g.order[g.w_lo - g.popped].second + spread < r) flip(g.w_lo++);
 }
 
 // GossipProtocolImpl.spread -> createAndPutGossip (GPI:124-128,163-169,211-213): the new
@@ -364,6 +396,7 @@ void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t
   uint32_t seq = o.gossip_seq++;
   const uint32_t gid = (uint32_t)h->registry.size();
   h->registry.push_back(Gossip{origin, seq, subject, record, ghash(origin, seq), create_round, 0});
+  gossip_reserve(h, gid + 1);
   gossip_put(h, o, gid, create_round);
   h->st.gossips_created++;
 }
@@ -614,22 +647,17 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   };
   std::vector<Delivery> deliveries;
   std::vector<Sent> sent;
-  std::vector<std::pair<uint32_t, int64_t>> window;  // (gid, infectionPeriod)
   std::vector<uint64_t> W(nw), S(nw);
   for (uint32_t s = 0; s < h->N; ++s) {
     Member& me = h->m[s];
     if (!nonempty[s]) continue;  // GPI:144-146 (no peer selection either)
     const int32_t spread = periods_to_spread(rm, (int32_t)me.others + 1);  // GPI:243-244
-    // selectGossipsToSend's age filter (GPI:247): a suffix of the infection order
-    window.clear();
-    std::fill(W.begin(), W.end(), 0ull);
-    for (auto it = me.gossips.order.rbegin(); it != me.gossips.order.rend() && it->second + spread >= r; ++it) {
-      if (it->second > r) continue;
-      window.push_back(*it);
-      W[(it->first >> 6) - wlo] |= 1ull << (it->first & 63);
-    }
+    // selectGossipsToSend's age filter (GPI:247)
+    window_update(h, me.gossips, r, spread);
+    const uint32_t rw = (h->rc >> 6) - 1;
+    for (uint32_t k = 0; k < nw; ++k) W[k] = me.gossips.win[(wlo + k) & rw];
     std::vector<uint32_t> peers = select_gossip_members(h, s);  // GPI:150
-    if (window.empty()) continue;
+    if (me.gossips.w_lo == me.gossips.w_end) continue;
     for (uint32_t p : peers) {
       Member& pm = h->m[p];
       // !isInfected(member.id()) (GPI:248): the window gossips p delivered to s during their
@@ -638,16 +666,18 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       uint64_t nsupp = 0;
       const auto fit = me.recv.find(p);
       if (fit != me.recv.end())
-        for (const auto& wg : window) {
-          const uint32_t g = wg.first;
-          for (const Batch& bt : fit->second) {
-            if (bt.t < wg.second - 1 || (g >> 6) < bt.w0 || (g >> 6) - bt.w0 >= bt.bits.size()) continue;
-            if (!((bt.bits[(g >> 6) - bt.w0] >> (g & 63)) & 1u) || !not_lost(p, s, g, bt.tick)) continue;
-            S[(g >> 6) - wlo] |= 1ull << (g & 63);
-            ++nsupp;
-            break;
+        for (const Batch& bt : fit->second)
+          for (uint32_t j = 0; j < bt.bits.size(); ++j) {
+            const uint32_t w = bt.w0 + j;
+            if (w < wlo || w >= whi) continue;
+            for (uint64_t c = bt.bits[j] & W[w - wlo] & ~S[w - wlo]; c; c &= c - 1) {
+              const uint32_t g = (w << 6) + (uint32_t)__builtin_ctzll(c);
+              // the batch counts for the current GossipState only (created in round inf - 1)
+              if (bt.t < me.gossips.inf[g & (h->rc - 1)] - 1 || !not_lost(p, s, g, bt.tick)) continue;
+              S[w - wlo] |= 1ull << (g & 63);
+              ++nsupp;
+            }
           }
-        }
       uint64_t nsend = 0;
       for (uint32_t k = 0; k < nw; ++k) nsend += (uint64_t)__builtin_popcountll(W[k] & ~S[k]);
       // one GossipRequest message per gossip and peer (GPI:225-239), counted for alive peers
@@ -681,8 +711,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     gossip_put(h, pm, d.gid, r + 1);
     h->st.gossip_first_receipts++;
     const Gossip& g = h->registry[d.gid];
-    auto& slot = h->inbox[d.to][g.subject];  // sink.next -> onMembershipGossip, batched
-    slot = std::max(slot, g.record);
+    h->inbox[d.to].push_back({g.subject, g.record});  // sink.next -> onMembershipGossip, batched
   }
   // ... and addToInfected(from) for every message (GPI:181)
   for (Sent& st : sent) h->m[st.to].recv[st.from].push_back(std::move(st.b));
@@ -699,7 +728,18 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   for (uint32_t p = 0; p < h->N; ++p) {
     if (h->inbox[p].empty()) continue;
     const uint32_t snap = h->m[p].others;
-    for (auto& kv : h->inbox[p])
+    // the lattice max per subject, subjects in ascending order
+    auto& in = h->inbox[p];
+    std::sort(in.begin(), in.end());
+    size_t o = 0;
+    for (size_t k = 0; k < in.size(); ++k) {
+      if (o && in[o - 1].first == in[k].first)
+        in[o - 1].second = in[k].second;  // sorted: the later record is the larger
+      else
+        in[o++] = in[k];
+    }
+    in.resize(o);
+    for (auto& kv : in)
       update_membership(h, p, kv.first, kv.second, SWIM_R_MEMBERSHIP_GOSSIP, phase, 0, tick, snap, r + 1);
     h->inbox[p].clear();
   }
@@ -871,6 +911,7 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
       h->m[i].table.assign(h->N, SWIM_PACK(0, SWIM_ALIVE));  // converged start, all ALIVE inc 0
       h->m[i].others = h->N - 1;
       h->m[i].gossips.held.assign(h->rc / 64, 0);
+      h->m[i].gossips.win.assign(h->rc / 64, 0);
       h->m[i].gossips.inf.assign(h->rc, 0);
     }
     h->inbox.resize(h->N);

@@ -22,7 +22,7 @@ using namespace swim;
 
 namespace {
 
-constexpr int NCLASS = 9;  // timing classes, see swim_kernel_time
+constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 
 uint32_t pow2ceil(uint64_t v) {
   uint64_t p = 1;
@@ -185,6 +185,7 @@ void set_phase(swim_handle* h, KP& P, uint32_t phase) {
   } else if (phase <= G) {
     P.round = t * G + phase - 1;
     P.create_round = t * G + phase;
+    P.act = P.act_ring + (size_t)(P.round & 255u) * P.astride;  // this round's active list
   } else {
     P.round = (t + 1) * G;
     P.create_round = (t + 1) * G;
@@ -297,7 +298,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_pairwin, dim3(256), dim3(256), 0, s, P); });
+        timed(h, 10, [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 10, [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
         if (W > 1) {  // (1) registrations with receivers on other shards
           Ctl c;
@@ -379,8 +381,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(h->n_in_pairs, 256)), dim3(256), 0, s, P,
                                h->n_in_pairs);
         }
+        timed(h, 9, [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_record, dim3(256), dim3(256), 0, s, P); });
+        timed(h, 11, [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
         timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_R_C;
@@ -673,7 +676,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.in_list, (size_t)N * INCAP);
   ALLOC(P.in_ov, 2ull * N * c.gossip_fanout);
   ALLOC(P.alist, 2ull * N);
-  ALLOC(P.act, h->GC / 32 + 8);  // + a quad of slack: k_gossip_select reads the list 16 B at a time
+  P.astride = h->GC / 32 + 8;  // + a quad of slack: k_gossip_select reads the list 16 B at a time
+  ALLOC(P.act_ring, 256ull * P.astride);
+  P.act = P.act_ring;
+  ALLOC(P.actpos, h->GC / 32);
   ALLOC(P.held, N);
   ALLOC(P.due, N);
   ALLOC(P.events, std::max<uint32_t>(1, h->ecap));
@@ -695,7 +701,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     const uint64_t reach = std::min<uint64_t>(N, (uint64_t)(P.hzn + 1) * f * 2 + 64 + 64);
     const uint64_t rec_round = std::max<uint64_t>(64, 2 * (uint64_t)P.nloc * f * reach / N);
     P.rcap = pow2ceil(std::max<uint64_t>(4096, rec_round * (P.hzn + 1)));
-    P.bcap = pow2ceil(std::min<uint64_t>(1ull << 30, std::max<uint64_t>(1 << 16, P.rcap * std::max<uint64_t>(1, W32 / 4))));
+    P.bcap = pow2ceil(std::min<uint64_t>(1ull << 30, std::max<uint64_t>(1 << 16, P.rcap * std::max<uint64_t>(1, W32 / 2))));
     P.spcap = (uint32_t)std::max<uint64_t>(4096, std::min<uint64_t>((uint64_t)P.nloc * f, 65536));
     P.pwcap = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1 << 16, (uint64_t)P.spcap * (W32 + 4)));
   }
@@ -751,6 +757,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
+  hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
+                     NONE);
   {  // every member of this shard starts with others = N - 1
     const uint32_t all = P.nloc;
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);

@@ -93,6 +93,7 @@ struct Ctl {
   // not overwrite a record still inside the horizon
   uint32_t rec_cnt, body_cnt, sp_cnt, rp_cnt, pw_used, pad2[3];
   uint32_t rs_rec[256], rs_body[256];
+  uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
 };
@@ -154,7 +155,10 @@ struct KP {
   uint32_t* in_list;  // [N][INCAP] the first INCAP of them
   uint32_t* in_ov;    // [N*f][2] (receiver, sender) pairs beyond INCAP
   uint32_t* alist;    // [N] receivers with first receipts this round
-  uint32_t* act;      // [GC/32] active words of this round (k_gossip_prep)
+  uint32_t* act;      // [GC/32] active words of this round (k_gossip_prep): its slot of act_ring
+  uint32_t* act_ring; // [256][astride] the active lists of the last 256 rounds (infectedFrom records)
+  uint32_t astride;
+  uint2* actpos;      // [GC/32] per ring word: {round it was last listed, its list position}
   uint32_t* held;     // [N] live gossips each member holds (GossipProtocolImpl.gossips.size())
   uint32_t* due;
   swim_event* events;
@@ -193,8 +197,8 @@ struct KP {
   uint4* ih;           // [nloc][IHCAP] in-history ring: {sender, round, record or NONE, 0}
   uint32_t* ih_head;   // [N] entries ever appended
   uint4* rec_hdr;      // [RCAP] delivery records: {deliverer, owner (receiver), round, body offset}
-  uint32_t* rec_len;   // [RCAP] body entries
-  uint2* rec_body;     // [BCAP] {unwrapped bitmap word, gossips of the word delivered}
+  uint32_t* rec_len;   // [RCAP] body words (the active list length of that round)
+  uint32_t* rec_body;  // [BCAP] per position of that round's active list: the gossips delivered
   uint32_t rcap, bcap; // powers of two
   uint4* sp_list;      // [SPCAP] this round's pruned pairs: {sender, peer, records, window offset}
   uint32_t* sp_recs;   // [SPCAP][MAXREC] their records
@@ -216,6 +220,7 @@ constexpr uint32_t NSUM = 1024;  // receipt-summary words per receiver: active l
 constexpr uint32_t SPAIR = 0x40000000u;  // in_list entry: a pruned pair (window in pw), not a member id
 constexpr uint32_t IHCAP = 256;  // in-history entries per member (~f per round over the horizon)
 constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
+constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {
   return bm && (bm[bit >> 3] & (1u << (bit & 7)));

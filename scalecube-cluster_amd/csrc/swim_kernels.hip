@@ -285,7 +285,7 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* to
 //   * for a delivery whose receiver may select its sender as a gossip peer within hzn rounds
 //     (may_select, conservative), a record of the delivered gossips;
 //   * when a member does select such a peer, its window for that peer is pruned by the records
-//     (k_gossip_pairwin); a selected peer in the in-history without a record (a prediction
+//     (k_gossip_pairfill, k_gossip_pairprune); a selected peer in the in-history without a record (a prediction
 //     that failed) raises OV_IFROM instead of silently diverging.
 // hzn = gossipPeriodsToSpread(N) + 1: a record made in round t can only suppress sends in rounds
 // t+1 .. t+1+spread, the last rounds the receiver can still have those gossips in its window.
@@ -298,26 +298,34 @@ __device__ __forceinline__ bool may_select(const KP& P, uint32_t p, uint32_t s) 
   if (reach >= N) return true;
   const uint32_t half = perm_half_bits(N);
   const uint32_t ep = P.g_epoch[p], cur = P.g_cursor[p];
-  const uint32_t pos = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep));
-  if (pos >= cur && pos - cur < reach) return true;
-  if (cur + reach > N) {  // the cursor may wrap into the next shuffle within the horizon
-    const uint32_t pos1 = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u));
-    if (pos1 < cur + reach - N) return true;
+  const PermKey k0 = perm_key(P.seed, K_GOSSIP_PERM, p, ep);
+  uint32_t pos = perm_inverse(s, N, half, k0);
+  bool wrap = false;
+  PermKey k1;
+  if (!(pos >= cur && pos - cur < reach)) {
+    if (cur + reach <= N) return false;
+    // the cursor may wrap into the next shuffle within the horizon
+    k1 = perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u);
+    pos = perm_inverse(s, N, half, k1);
+    if (pos >= cur + reach - N) return false;
+    wrap = true;
   }
-  return false;
-}
-
-// position of word offset o (from w_beg) in this round's active list, or NONE (sorted ascending)
-__device__ __forceinline__ uint32_t act_find(const KP& P, uint32_t o, uint32_t n_act) {
-  uint32_t lo = 0, hi = n_act;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if ((P.act[mid] & ACT_OFF_MASK) < o)
-      lo = mid + 1u;
-    else
-      hi = mid;
+  // Exact refinement: selectGossipMembers takes the first f present members from the cursor each
+  // round, so s comes up once the present members ahead of it are used up. Members removed in
+  // the meantime only bring it closer: a quarter of margin (a misprediction raises OV_IFROM).
+  const uint32_t* row = P.view + lrow(P, p) * N;
+  uint32_t ahead = 0;
+  const uint32_t end0 = wrap ? N : pos;
+  for (uint32_t x = cur; x < end0; ++x) {
+    const uint32_t m = perm_apply(x, N, half, k0);
+    ahead += (m != p && row[m] != 0u) ? 1u : 0u;
   }
-  return (lo < n_act && (P.act[lo] & ACT_OFF_MASK) == o) ? lo : NONE;
+  if (wrap)
+    for (uint32_t x = 0; x < pos; ++x) {
+      const uint32_t m = perm_apply(x, N, half, k1);
+      ahead += (m != p && row[m] != 0u) ? 1u : 0u;
+    }
+  return ahead < (P.f * P.hzn * 5u) / 4u + 16u;
 }
 
 __device__ __forceinline__ uint32_t bytes_sub(uint32_t r, uint32_t d);
@@ -431,18 +439,27 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     uint32_t total;
     const uint32_t off = block_excl_scan1024(cnt, &total, s_part);
     if (pad) {
-      if (onm) *reinterpret_cast<uint4*>(P.act + base + off) = make_uint4(e[0], e[1], e[2], e[3]);
+      if (onm) {
+        *reinterpret_cast<uint4*>(P.act + base + off) = make_uint4(e[0], e[1], e[2], e[3]);
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j)  // word -> list position, for infectedFrom records
+          P.actpos[(wq + j) & (W32 - 1u)] = make_uint2(P.round, base + off + j);
+      }
     } else {
       uint32_t o = base + off;
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j)
-        if ((onm >> j) & 1u) P.act[o++] = e[j];
+        if ((onm >> j) & 1u) {
+          P.actpos[(wq + j) & (W32 - 1u)] = make_uint2(P.round, o);
+          P.act[o++] = e[j];
+        }
     }
     base += total;
   }
   if (threadIdx.x == 0) {
     c->n_act = base;
     c->w_beg = w_beg;
+    c->wbeg_hist[P.round & 255u] = w_beg;
   }
 }
 
@@ -736,11 +753,13 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (lane < np && s_nrec[w][lane]) {  // this pair's window gets pruned (k_gossip_pairwin)
+    if (lane < np && s_nrec[w][lane]) {  // this pair's window gets pruned (k_gossip_pairprune)
       const uint32_t nr = s_nrec[w][lane] < MAXREC ? s_nrec[w][lane] : MAXREC;
       const uint32_t sp = atomicAdd(&P.ctl->sp_cnt, 1u);
-      if (sp < P.spcap) {
-        P.sp_list[sp] = make_uint4(m, s_peers[w][lane], nr, 0u);
+      const uint32_t n4 = (n_act + 3u) & ~3u;  // act-indexed window, padded to quads for k_gossip_pull
+      const uint32_t off = atomicAdd(&P.ctl->pw_used, n4);
+      if (sp < P.spcap && off + n4 <= P.pwcap && off + n4 >= off) {
+        P.sp_list[sp] = make_uint4(m, s_peers[w][lane], nr, off);
         for (uint32_t c = 0; c < nr; ++c) P.sp_recs[(size_t)sp * MAXREC + c] = s_rec[w][lane][c];
         entry = SPAIR | sp;
       } else {
@@ -783,50 +802,60 @@ __device__ __forceinline__ uint32_t own_window(const KP& P, uint32_t m, uint32_t
   return P.wb[lrow(P, m) * W32 + k];
 }
 
-// One wave per pruned pair (sender m, peer x) of this round: m's window, minus every gossip x
-// delivered to m (a record of round t) during m's current GossipState of it
-// (selectGossipsToSend's !isInfected filter, GossipProtocolImpl.java:245-250). The pruned
-// window goes to pw, where k_gossip_pull (or the shard exchange) reads it instead of wb/hb.
-__global__ void __launch_bounds__(256) k_gossip_pairwin(KP P) {
+// Pruned pairs (sender m, peer x) of this round: m's window minus every gossip x delivered to m
+// (a record of round t) during m's current GossipState of it (selectGossipsToSend's
+// !isInfected filter, GossipProtocolImpl.java:245-250). k_gossip_pairfill copies m's window into
+// the pair's pw slot, k_gossip_pairprune clears the recorded gossips; k_gossip_pull (or the shard
+// exchange) then reads pw instead of wb/hb. Work is split in PCHUNK-position pieces, one wave each.
+__global__ void __launch_bounds__(256) k_gossip_pairfill(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
-  const uint32_t n4 = (n_act + 3u) & ~3u;  // 16-B aligned windows (k_gossip_pull reads quads)
+  const uint32_t n4 = (n_act + 3u) & ~3u;
+  const uint32_t nch = (n4 + PCHUNK - 1u) / PCHUNK;
+  for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {
+    const uint4 sp = P.sp_list[u / nch];
+    const uint32_t k1 = min(n4, (u % nch + 1u) * PCHUNK);
+    for (uint32_t k = (u % nch) * PCHUNK + lane; k < k1; k += 64u)
+      P.pw[sp.w + k] = k < n_act ? own_window(P, sp.x, k, w_beg, lo, hi) : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
-  uint32_t removed_alive = 0, pairs = 0;
-  for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+  const uint32_t nch = (P.astride + PCHUNK - 1u) / PCHUNK;  // chunks of the longest record
+  uint32_t removed_alive = 0;
+  for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * MAXREC * nch; u += gridDim.x * 4u) {
+    const uint32_t i = u / (MAXREC * nch), j = (u / nch) % MAXREC, c = u % nch;
     const uint4 sp = P.sp_list[i];
-    const uint32_t m = sp.x, x = sp.y;
-    uint32_t off = 0;
-    if (lane == 0) off = atomicAdd(&P.ctl->pw_used, n4);
-    off = __shfl(off, 0, 64);
-    if (off + n4 > P.pwcap || off + n4 < off) {
-      if (lane == 0) atomicOr(&P.ctl->overflow, OV_IFROM);
-      continue;
-    }
-    if (lane == 0) P.sp_list[i].w = off;
-    uint32_t* pwr = P.pw + off;
-    for (uint32_t k = lane; k < n4; k += 64u) pwr[k] = k < n_act ? own_window(P, m, k, w_beg, lo, hi) : 0u;
-    __threadfence();  // the plain stores reach L2 before the atomics below
+    if (j >= sp.z) continue;
+    const uint32_t rec = P.sp_recs[(size_t)i * MAXREC + j];
+    const uint4 hdr = P.rec_hdr[rec & (P.rcap - 1u)];
+    const uint32_t len = P.rec_len[rec & (P.rcap - 1u)];
+    if (c * PCHUNK >= len) continue;
+    const uint32_t t = hdr.z, wbt = P.ctl->wbeg_hist[t & 255u];
+    const uint32_t* act_t = P.act_ring + (size_t)(t & 255u) * P.astride;
     uint32_t removed = 0;
-    for (uint32_t j = 0; j < sp.z; ++j) {
-      const uint32_t rec = P.sp_recs[(size_t)i * MAXREC + j];
-      const uint4 hdr = P.rec_hdr[rec & (P.rcap - 1u)];
-      const uint32_t len = P.rec_len[rec & (P.rcap - 1u)];
-      for (uint32_t e = lane; e < len; e += 64u) {
-        const uint2 ent = P.rec_body[(hdr.w + e) & (P.bcap - 1u)];
-        if (ent.x < w_beg) continue;  // every holder has swept the word
-        const uint32_t k = act_find(P, ent.x - w_beg, n_act);
-        if (k == NONE || ((P.act[k] >> 26) & 3u) == WC_NONE) continue;  // nobody's window
-        const uint32_t supp = ent.y & state_since(P, m, ent.x & (W32 - 1u), hdr.z);
-        if (supp) removed += (uint32_t)__popc(atomicAnd(&pwr[k], ~supp) & supp);
-      }
+    const uint32_t q1 = min(len, (c + 1u) * PCHUNK);
+    for (uint32_t q = c * PCHUNK + lane; q < q1; q += 64u) {
+      const uint32_t bits = P.rec_body[(hdr.w + q) & (P.bcap - 1u)];
+      if (!bits) continue;
+      const uint32_t wi = wbt + (act_t[q] & ACT_OFF_MASK);
+      if (wi < w_beg) continue;  // every holder has swept the word
+      const uint2 ap = P.actpos[wi & (W32 - 1u)];  // listed this round, as this very word?
+      if (ap.x != P.round || ap.y >= n_act) continue;
+      const uint32_t ea = P.act[ap.y];
+      if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
+      const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t);
+      if (supp) removed += (uint32_t)__popc(atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
-    if (P.alive[x]) removed_alive += removed;  // the send counter covers alive peers only
-    pairs += lane == 0 ? 1u : 0u;
+    if (P.alive[sp.y]) removed_alive += removed;  // the send counter covers alive peers only
   }
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
-  add_stat(P, ST_IF_PAIRS, pairs);
+  add_stat(P, ST_IF_PAIRS, (blockIdx.x == 0 && threadIdx.x == 0) ? n : 0u);
 }
 
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
@@ -857,42 +886,103 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
   return v;
 }
 
-// One wave per recorded delivery of this round (chosen in k_gossip_pull): the receiver's
-// addToInfected(sender) for every gossip delivered (GossipProtocolImpl.java:181), stored sparse as
-// (word, bits) in the record pool. Runs before k_gossip_apply changes any holdings.
+// Recorded deliveries of this round (chosen in k_gossip_inhist): the receiver's
+// addToInfected(sender) for every gossip delivered (GossipProtocolImpl.java:181), one word per
+// position of this round's active list (kept in act_ring for the record's lifetime). Runs before
+// k_gossip_apply changes any holdings; PCHUNK positions per wave.
 __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->rp_cnt < P.spcap ? P.ctl->rp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
-  const uint32_t r = P.round;
-  uint32_t nrec = 0;
-  for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
-    const uint4 rp = P.rp_list[i];  // {in_list entry, receiver, record, sender id}
-    uint32_t cnt = 0, wi;
-    for (uint32_t k = lane; k < n_act; k += 64u) cnt += delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi) ? 1u : 0u;
-    const uint32_t total = wave_sum(cnt);
-    uint32_t off = 0;
-    if (lane == 0) off = atomicAdd(&P.ctl->body_cnt, total);
-    off = __shfl(off, 0, 64);
-    // the records still inside the horizon start at rs_body of round r - hzn
-    if (off + total - P.ctl->rs_body[(r - P.hzn) & 255u] > P.bcap) {
-      if (lane == 0) atomicOr(&P.ctl->overflow, OV_IFROM);
-      continue;
-    }
-    uint32_t base = 0;
-    for (uint32_t k0 = 0; k0 < n_act; k0 += 64u) {
-      const uint32_t k = k0 + lane;
-      const uint32_t v = k < n_act ? delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi) : 0u;
-      const unsigned long long b = __ballot(v != 0u);
-      if (v) P.rec_body[(off + base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))) & (P.bcap - 1u)] = make_uint2(wi, v);
-      base += (uint32_t)__popcll(b);
-    }
-    if (lane == 0) {
-      P.rec_hdr[rp.z & (P.rcap - 1u)].w = off;
-      P.rec_len[rp.z & (P.rcap - 1u)] = total;
-    }
-    nrec += lane == 0 ? 1u : 0u;
+  const uint32_t nch = (n_act + PCHUNK - 1u) / PCHUNK;
+  for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {
+    const uint4 rp = P.rp_list[u / nch];  // {in_list entry, receiver, record, sender id}
+    const uint32_t off = P.rec_hdr[rp.z & (P.rcap - 1u)].w;
+    const uint32_t k1 = min(n_act, (u % nch + 1u) * PCHUNK);
+    uint32_t wi;
+    for (uint32_t k = (u % nch) * PCHUNK + lane; k < k1; k += 64u)
+      P.rec_body[(off + k) & (P.bcap - 1u)] = delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi);
   }
+}
+
+// One wave per receiver p, after every member's selection of the round: each sender whose
+// messages can reach p joins p's in-history (round, record); a delivery p may answer with gossips
+// of its own within the horizon (may_select on p's post-selection cursor) gets a record, which
+// k_gossip_record fills after k_gossip_pull (GossipState.addToInfected, GPI:181).
+__global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (p >= P.row0 + P.nloc) return;  // whole wave
+  const uint32_t deg = P.in_cnt[p];
+  if (!deg || !P.alive[p] || P.loss_mode == 2u) return;  // nothing can be delivered
+  const uint32_t r = P.round, n_act = P.ctl->n_act;
+  uint32_t ihh = P.ih_head[p];
+  uint4* ring = P.ih + lrow(P, p) * IHCAP;
+  const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
+  uint32_t ov_pos = 0;
+  uint32_t nrec = 0;
+  for (uint32_t done = 0; done < deg;) {
+    uint32_t sreg = 0, cdeg = 0;
+    if (done == 0) {
+      cdeg = deg < INCAP ? deg : INCAP;
+      if (lane < cdeg) sreg = P.in_list[(size_t)p * INCAP + lane];
+    } else {
+      while (cdeg == 0 && ov_pos < n_ov) {  // receivers picked by more than INCAP senders (rare)
+        const uint32_t o = ov_pos + lane;
+        const bool mine = o < n_ov && P.in_ov[2 * o] == p;
+        const unsigned long long b = __ballot(mine);
+        if (mine) sreg = P.in_ov[2 * o + 1];  // lanes of a chunk need not be dense here
+        cdeg = (uint32_t)__popcll(b);
+        if (cdeg) {
+          const uint32_t rank = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+          uint32_t v = 0;
+          for (uint32_t t = 0; t < 64u; ++t) {
+            const uint32_t x = __shfl(sreg, (int)t, 64), rk = __shfl(rank, (int)t, 64);
+            if (((b >> t) & 1ull) && lane == rk) v = x;
+          }
+          sreg = v;
+        }
+        ov_pos += 64u;
+      }
+      if (cdeg == 0) break;
+    }
+    done += cdeg;
+    uint32_t sid = 0;
+    if (lane < cdeg) {
+      if (sreg & XREC)
+        sid = P.rpairs[2 * (sreg & ~XREC)];
+      else if (sreg & SPAIR)
+        sid = P.sp_list[sreg & ~SPAIR].x;
+      else
+        sid = sreg;
+    }
+    const bool ok_l = lane < cdeg && link_open(P, sid, p);
+    const unsigned long long reach = __ballot(ok_l);
+    uint32_t rec = NONE;
+    if (ok_l && may_select(P, p, sid)) {
+      rec = atomicAdd(&P.ctl->rec_cnt, 1u);
+      const uint32_t o = atomicAdd(&P.ctl->rp_cnt, 1u);
+      const uint32_t body = atomicAdd(&P.ctl->body_cnt, n_act);
+      // the records still inside the horizon start at rs_rec / rs_body of round r - hzn
+      if (rec + 1u - P.ctl->rs_rec[(r - P.hzn) & 255u] > P.rcap ||
+          body + n_act - P.ctl->rs_body[(r - P.hzn) & 255u] > P.bcap || o >= P.spcap) {
+        atomicOr(&P.ctl->overflow, OV_IFROM);
+      } else {
+        P.rec_hdr[rec & (P.rcap - 1u)] = make_uint4(sid, p, r, body);
+        P.rec_len[rec & (P.rcap - 1u)] = n_act;
+        P.rp_list[o] = make_uint4(sreg, p, rec, sid);
+        ++nrec;
+      }
+    }
+    if (ok_l) {
+      const uint32_t pos = ihh + (uint32_t)__popcll(reach & ((1ull << lane) - 1ull));
+      uint4* slot = ring + (pos & (IHCAP - 1u));
+      if (pos >= IHCAP && (*slot).y + P.hzn >= r) atomicOr(&P.ctl->overflow, OV_IFROM);
+      *slot = make_uint4(sid, r, rec, 0u);
+    }
+    ihh += (uint32_t)__popcll(reach);
+  }
+  if (lane == 0) P.ih_head[p] = ihh;
   add_stat(P, ST_IF_RECORDS, nrec);
 }
 
@@ -929,9 +1019,6 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
-    uint32_t ihh = P.ih_head[p];  // in-history appends of this receiver (wave-uniform)
-    uint4* ring = P.ih + lrow(P, p) * IHCAP;
-    const uint32_t r = P.round;
     for (uint32_t done = 0; done < deg;) {
       const bool first_chunk = done == 0;  // later chunks only add gossips earlier ones did not bring
       // next chunk of senders: lane q holds sender q
@@ -974,28 +1061,6 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       }
       const bool ok_l = lane < cdeg && P.loss_mode != 2u && link_open(P, sid, p);
       const unsigned long long reach = __ballot(ok_l);
-      {  // infectedFrom: every sender whose messages can arrive joins p's in-history; a delivery
-         // p may send gossips back to within the horizon is recorded (k_gossip_record)
-        uint32_t rec = NONE;
-        if (ok_l && may_select(P, p, sid)) {
-          rec = atomicAdd(&P.ctl->rec_cnt, 1u);
-          const uint32_t o = atomicAdd(&P.ctl->rp_cnt, 1u);
-          if (rec + 1u - P.ctl->rs_rec[(r - P.hzn) & 255u] > P.rcap || o >= P.spcap) {
-            atomicOr(&P.ctl->overflow, OV_IFROM);
-          } else {
-            P.rec_hdr[rec & (P.rcap - 1u)] = make_uint4(sid, p, r, 0u);
-            P.rec_len[rec & (P.rcap - 1u)] = 0u;
-            P.rp_list[o] = make_uint4(sreg, p, rec, sid);
-          }
-        }
-        if (ok_l) {
-          const uint32_t pos = ihh + (uint32_t)__popcll(reach & ((1ull << lane) - 1ull));
-          uint4* slot = ring + (pos & (IHCAP - 1u));
-          if (pos >= IHCAP && (*slot).y + P.hzn >= r) atomicOr(&P.ctl->overflow, OV_IFROM);
-          *slot = make_uint4(sid, r, rec, 0u);
-        }
-        ihh += (uint32_t)__popcll(reach);
-      }
       uint32_t* snd = s_snd[threadIdx.x >> 6];
       snd[lane] = sreg;
       s_sid[threadIdx.x >> 6][lane] = sid;
@@ -1108,7 +1173,6 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       }
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
-    if (lane == 0) P.ih_head[p] = ihh;
     const uint32_t total = wave_sum(receipts);
     if (lane == 0 && total) {
       const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);

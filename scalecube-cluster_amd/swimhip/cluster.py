@@ -243,7 +243,8 @@ class SwimCluster:
 
     # -- bench helpers (HIP library only) ---------------------------------------------------
     KERNEL_CLASSES = ["k_fd", "k_gossip_pull", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
-                      "k_sync_snapshot", "bookkeeping", "k_gossip_select"]
+                      "k_sync_snapshot", "bookkeeping", "k_gossip_select", "k_gossip_inhist", "k_gossip_pairwin",
+                      "k_gossip_record"]
 
     def step_async(self, periods: int = 1):
         self._call("step_async", self._h, int(periods))

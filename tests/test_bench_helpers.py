@@ -27,7 +27,8 @@ def test_kernel_bytes_covers_every_timed_class():
     from swimhip import SwimCluster
 
     d = {k: 1 for k in ("merge_cells", "ack_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
-                        "gossip_pull_words", "gossip_probes", "gossip_first_receipts", "sweep_cells", "fd_probes")}
+                        "gossip_pull_words", "gossip_probes", "gossip_first_receipts", "sweep_cells", "fd_probes",
+                        "infected_pruned_pairs", "infected_records")}
     for name in SwimCluster.KERNEL_CLASSES:
         if name != "bookkeeping":
             assert bench.kernel_bytes(name, d, 1) > 0, name

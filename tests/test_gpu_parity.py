@@ -33,11 +33,14 @@ def test_philox_device_matches_oracle():
         assert out[:256].tolist() == ref
 
 
-def test_c2_shape_4096_digest_parity():
-    """BASELINE config 2 shape (4,096 dense, 5 % loss, fanout 3, 1 % crash), 12 periods."""
+def test_c2_shape_4096_full_parity():
+    """BASELINE config 2 shape (4,096 dense, 5 % loss, fanout 3, 1 % crash), 12 periods: every
+    membership table, every suspicion deadline, the ordered MembershipEvent stream and the
+    protocol counters equal the oracle's every 4 periods."""
     cfg = ClusterConfig.defaultLanConfig()
     n = 4096
-    a, b = SwimCluster(cfg, n, seed=2024), OracleCluster(cfg, n, seed=2024)
+    a = SwimCluster(cfg, n, seed=2024, event_capacity=1 << 22)
+    b = OracleCluster(cfg, n, seed=2024, event_capacity=1 << 22)
     crashed = scenarios.crash_ids(n, 41, 2024)
     for c in (a, b):
         c.set_loss(5.0)
@@ -49,6 +52,10 @@ def test_c2_shape_4096_digest_parity():
         assert a.digest() == b.digest()
         sa, sb = a.stats(), b.stats()
         assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+        assert [e.key() for e in a.events()] == [e.key() for e in b.events()]
+        for i in range(n):
+            assert np.array_equal(a.view(i), b.view(i)), f"view row {i}"
+            assert np.array_equal(a.deadlines(i), b.deadlines(i)), f"deadline row {i}"
 
 
 def test_crash_converges_and_gossip_capacity_reports_overflow():
