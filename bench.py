@@ -72,8 +72,11 @@ def kernel_bytes(name, d, n):
         return 4 * d["gossip_scanned"] + 32 * d["gossip_hd_words"] + 4 * d["gossip_window_words"]  # + window
     if name == "k_gossip_pull":  # receiver holds word r/w + receipts word per active window word, one
         return 12 * d["gossip_pull_words"] + 4 * d["gossip_probes"]  # sender window word per probe
-    if name == "k_gossip_apply":  # per receipt: infection round (2 B) + ring record (8 B)
-        return 10 * d["gossip_first_receipts"]
+    if name == "k_gossip_apply":
+        # per receipt word: receipts r/w (8 B: read, clear), holdings r/w (8), newest/oldest round (1),
+        # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4);
+        # per subject run one ring record (8 B); per subject the table cell and its deadline (8 B)
+        return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
     if name == "k_susp_sweep":  # stream a deadline column
         return 4 * d["sweep_cells"]
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
@@ -90,22 +93,35 @@ def kernel_bytes(name, d, n):
     return 0
 
 
-def pmc_traffic(kernel, workload="c3", world=1):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload on one GPU
-    (tools/gpu_pmc.sh: separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes over the same workload;
-    FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md): profiles/pmc_traffic.json for
-    the default C3 run, profiles/pmc_traffic_<workload>.json for the others. None when no summary
-    covers the kernel, the workload, or a sharded run (per-launch traffic changes with the shard)."""
-    if world != 1:
+def pmc_traffic(kernel, workload="c3", world=1, steps=None, warmup=None):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of exactly this run: the same
+    workload, --steps and --warmup on one GPU (tools/gpu_pmc.sh: separate FETCH_SIZE and WRITE_SIZE
+    rocprofv3 passes over `bench.py --steps S --warmup W`; FETCH_SIZE doubled per the gfx950 note
+    in MI355X_MICROARCH.md): profiles/pmc_traffic_<workload>_s<S>_w<W>.json. None when no summary
+    covers that window or kernel, or for a sharded run (per-launch traffic changes with the shard)."""
+    if world != 1 or steps is None or warmup is None:
         return None
-    name = "pmc_traffic.json" if workload == "c3" else f"pmc_traffic_{workload}.json"
-    path = os.path.join(REPO, "profiles", name)
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{workload}_s{steps}_w{warmup}.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
     k = d.get(kernel)
     return None if k is None else k["fetch_bytes_x2"] + k["write_bytes"]
+
+
+def roofline_of(name, ktimes, d, world):
+    """achieved GB/s = algorithmic bytes per launch (kernel_bytes) / average launch time (HIP events
+    on the handle's stream), for one kernel class over a measured window."""
+    ms, launches = ktimes.get(name, (0.0, 0))
+    byts = kernel_bytes(name, d, 0)
+    if not launches or not ms or not byts:
+        return None
+    avg_s = ms / 1e3 / launches
+    per_launch = byts / world / launches  # work counters are cluster-wide, launches per shard
+    achieved = per_launch / avg_s / 1e9
+    return {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": per_launch,
+            "avg_launch_ms": avg_s * 1e3, "launches": launches}
 
 
 def log(msg):
@@ -254,15 +270,18 @@ def main():
 
     # dominant kernel + roofline over the timed region
     dom = max((k for k in ktimes if k != "bookkeeping"), key=lambda k: ktimes[k][0])
-    ms, launches = ktimes[dom]
-    byts = kernel_bytes(dom, d, n)
-    avg_s = ms / 1e3 / max(1, launches)
-    per_launch = byts / world / max(1, launches)  # work counters are cluster-wide, launches per shard
-    achieved = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    rl = roofline_of(dom, ktimes, d, world) or {"achieved": 0.0, "frac": 0.0, "bytes_per_launch": 0.0,
+                                                 "avg_launch_ms": 0.0, "launches": 0}
+    fracs = {k: round(v["frac"], 4) for k in ktimes if k != "bookkeeping"
+             for v in [roofline_of(k, ktimes, d, world)] if v}
 
-    # periods to DEAD convergence (untimed): every alive observer removed every crashed member
+    # periods to DEAD convergence (untimed): every alive observer removed every crashed member;
+    # the kernels are timed here too, for the suspicion sweep (no timeout fires in the timed region)
     periods_to_dead = None
+    conv = None
     if crashed and args.converge:
+        sc0 = c.stats()
+        c.kernel_timing(True)
         extra = 0
         while extra < args.converge:
             st = c.stats()
@@ -274,6 +293,11 @@ def main():
         pres, last = c.presence()
         if c.stats()["not_converged"] == 0:
             periods_to_dead = int(max(last[crashed])) - 1 - crash_period
+        kt2 = c.kernel_times()
+        dc = {k: v - sc0[k] for k, v in c.stats().items()}
+        conv = {k: round(v["frac"], 4) for k in ("k_susp_sweep", "k_sync_merge", "k_sync_ack")
+                for v in [roofline_of(k, kt2, dc, world)] if v}
+        c.kernel_timing(False)
 
     value = n * args.steps / elapsed  # the one cluster's member-periods (all shards together)
     out = {
@@ -294,14 +318,18 @@ def main():
                    "crashed": len(crashed), "loss_pct": w["loss"], "partition_periods": w["part"],
                    "gossip_ring_slots": w["gcap"]},
         "periods_to_dead": periods_to_dead,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom, args.workload, world),
-                     "bytes_per_launch": per_launch, "avg_launch_ms": avg_s * 1e3, "launches": launches},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": rl["frac"], "traffic": pmc_traffic(dom, args.workload, world, args.steps, args.warmup),
+                     "bytes_per_launch": rl["bytes_per_launch"], "avg_launch_ms": rl["avg_launch_ms"],
+                     "launches": rl["launches"]},
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
+        "kernels_frac": fracs,
+        "converge_kernels_frac": conv,
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
-                                   "infected_suppressed", "infected_pruned_pairs", "infected_records")},
+                                   "infected_suppressed", "infected_pruned_pairs", "infected_records",
+                                   "apply_words", "apply_runs", "apply_subjects")},
     }
     c.close()
     if rank == 0 and not args.no_cpu_baseline:

@@ -144,6 +144,10 @@ typedef struct swim_stats {
   uint64_t infected_pruned_pairs; /* (sender, peer) pairs whose window was pruned              */
   uint64_t infected_records;  /* deliveries recorded in full                                  */
   uint64_t infected_suppressed; /* GossipRequests not sent: peer in infectedFrom (alive peers) */
+  /* k_gossip_apply's work, for its HBM byte model; 0 in the oracle */
+  uint64_t apply_words;       /* receipt words folded into holdings / infection rounds        */
+  uint64_t apply_runs;        /* subject-run representatives read from the ring               */
+  uint64_t apply_subjects;    /* updateMembership calls (one per subject per receiver)        */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -168,6 +172,12 @@ int swim_block_inbound(swim_handle* h, uint32_t dst, uint32_t src, int blocked);
 /* Crash = transport.stop() (MembershipProtocolTest.java:991-1000): the member stops
  * sending, receiving, answering and firing timers, from the next period on. */
 int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
+
+/* Graceful leave = Cluster.shutdown() (ClusterImpl.java:370-408): each member's own record
+ * becomes DEAD and is spread as a gossip (MembershipProtocolImpl.leaveCluster :203-212); the member
+ * keeps running until its own sweep drops that gossip (spread() completes at sweep,
+ * GossipProtocolImpl.java:299-302), then stops at the end of that gossip round. Unsharded handles. */
+int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n);
 
 /* Advance `periods` protocol periods (FD, G gossip rounds, suspicion
  * timeouts, SYNC/SYNC_ACK). Asynchronous to the host only inside the call. */

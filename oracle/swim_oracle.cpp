@@ -211,6 +211,11 @@ struct Member {
   uint32_t gossip_seq = 0;              // GPI:48 gossipCounter
   uint32_t sync_fd = 0xFFFFFFFFu;       // FD-triggered SYNC target of this period (MPI:385-397)
   bool alive = true;
+  // graceful leave (MPI:203-212): the gossip of its own DEAD record; the member shuts down once
+  // its own sweep drops it (GossipProtocolImpl.spread completes at sweep, :299-302, and
+  // ClusterImpl.doShutdown then disposes and stops the transport, ClusterImpl.java:376-388)
+  bool leaving = false, stop = false;
+  uint32_t leave_gid = 0;
 };
 
 struct SyncReq {
@@ -371,6 +376,18 @@ void gossip_pop_oldest(oracle_handle* h, Member& me) {
   g.w_lo = std::max(g.w_lo, g.popped);
   g.w_end = std::max(g.w_end, g.w_lo);
   h->registry[gid].holders--;
+}
+
+// transport.stop(): the member stops sending, receiving, answering and firing timers.
+void stop_member(oracle_handle* h, uint32_t c) {
+  Member& me = h->m[c];
+  if (!me.alive) return;
+  me.alive = false;
+  me.timers.clear();  // its scheduler is gone
+  while (!me.gossips.order.empty()) gossip_pop_oldest(h, me);
+  me.recv.clear();
+  for (uint32_t j = 0; j < h->N; ++j)
+    if (j != c && me.table[j] != SWIM_ABSENT) h->pres[j]--;
 }
 
 // Bring the window bitset to round r: gossips with infectionPeriod in [r - spread, r] (GPI:247).
@@ -633,7 +650,10 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     Member& me = h->m[s];
     if (!me.alive) continue;
     const int32_t sweep = periods_to_sweep(rm, (int32_t)me.others + 1);  // GPI:283-284
-    while (!me.gossips.order.empty() && r > me.gossips.order.front().second + sweep) gossip_pop_oldest(h, me);
+    while (!me.gossips.order.empty() && r > me.gossips.order.front().second + sweep) {
+      if (me.leaving && me.gossips.order.front().first == me.leave_gid) me.stop = true;  // GPI:299-302
+      gossip_pop_oldest(h, me);
+    }
   }
   // Every member's doSpreadGossip(r) runs on the start-of-round state (its gossips, their
   // infected sets, its peers); the messages are handled by the receivers' onGossipReq after
@@ -743,6 +763,12 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       update_membership(h, p, kv.first, kv.second, SWIM_R_MEMBERSHIP_GOSSIP, phase, 0, tick, snap, r + 1);
     h->inbox[p].clear();
   }
+  // a leaving member whose DEAD gossip was swept this round shuts down (ClusterImpl.java:376-388)
+  for (uint32_t i = 0; i < h->N; ++i)
+    if (h->m[i].stop) {
+      h->m[i].stop = false;
+      stop_member(h, i);
+    }
   finish_phase(h);
 }
 
@@ -969,16 +995,28 @@ int oracle_block_inbound(oracle_handle* h, uint32_t dst, uint32_t src, int block
 int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n) {
   if (!h || (n && !ids)) return SWIM_EINVAL;
   for (uint32_t k = 0; k < n; ++k) {
-    uint32_t c = ids[k];
-    if (c >= h->N) return SWIM_EINVAL;
-    Member& me = h->m[c];
-    if (!me.alive) continue;
-    me.alive = false;
-    me.timers.clear();  // its scheduler is gone
-    while (!me.gossips.order.empty()) gossip_pop_oldest(h, me);
-    me.recv.clear();
-    for (uint32_t j = 0; j < h->N; ++j)
-      if (j != c && me.table[j] != SWIM_ABSENT) h->pres[j]--;
+    if (ids[k] >= h->N) return SWIM_EINVAL;
+    stop_member(h, ids[k]);
+  }
+  return SWIM_OK;
+}
+
+// ClusterImpl.shutdown (ClusterImpl.java:370-408) -> MembershipProtocolImpl.leaveCluster
+// (MPI:203-212): the member's own record becomes DEAD (incarnation + 1, which the packed DEAD
+// cell does not need: a DEAD record overrides every non-DEAD one and nothing overrides it) and
+// is spread as a gossip; the member keeps running until that gossip is swept. Takes effect
+// before the next period (the gossip's infectionPeriod is the period's first round).
+int oracle_leave(oracle_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t i = ids[k];
+    if (i >= h->N) return SWIM_EINVAL;
+    Member& me = h->m[i];
+    if (!me.alive || me.leaving) continue;
+    me.table[i] = SWIM_DEAD;
+    me.leaving = true;
+    me.leave_gid = (uint32_t)h->registry.size();
+    spread_gossip(h, i, i, SWIM_DEAD, (int64_t)h->period * h->G);
   }
   return SWIM_OK;
 }

@@ -45,6 +45,7 @@ struct swim_handle {
   uint32_t q = 0;
   // sharding
   uint32_t world = 1, rank = 0;
+  uint32_t n_leaving = 0;  // swim_leave calls so far (the stop check runs only once one happened)
   void* xsend = nullptr;
   void* xrecv = nullptr;
   uint64_t xsend_words = 0, xrecv_words = 0;
@@ -386,6 +387,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 11, [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
         timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
         if (rc) return rc;
@@ -617,6 +619,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
   ALLOC(P.alive, N);
+  ALLOC(P.leaving, N);
+  ALLOC(P.stopf, N);
+  ALLOC(P.leave_slot, N);
   ALLOC(group, N);
   ALLOC(P.fd_epoch, N);
   ALLOC(P.fd_cursor, N);
@@ -742,6 +747,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.sync_fd, (size_t)N, NONE);
   (void)hipMemsetAsync(P.cnt_delta, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.alive, 1, N, s);
+  (void)hipMemsetAsync(P.leaving, 0, N, s);
+  (void)hipMemsetAsync(P.stopf, 0, N, s);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.leave_slot, (size_t)N, NONE);
   (void)hipMemsetAsync(group, 0, N, s);
   (void)hipMemsetAsync(P.fd_epoch, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.fd_cursor, 0, (size_t)N * 4, s);
@@ -841,6 +849,19 @@ int swim_block_link(swim_handle* h, uint32_t src, uint32_t dst, int blocked) {
 int swim_block_inbound(swim_handle* h, uint32_t dst, uint32_t src, int blocked) {
   if (!h || src >= h->N || dst >= h->N) return SWIM_EINVAL;
   return set_bitmap_bit(h, &h->base.inlink, (uint64_t)dst * h->N + src, blocked);
+}
+
+int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_leave: not supported on sharded handles");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_leave: a period is in flight");
+  for (uint32_t k = 0; k < n; ++k)
+    if (ids[k] >= h->N) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) hipLaunchKernelGGL(k_leave, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+  h->n_leaving += n;
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
 }
 
 int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
@@ -992,6 +1013,9 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->infected_pruned_pairs = stats[ST_IF_PAIRS];
   out->infected_records = stats[ST_IF_RECORDS];
   out->infected_suppressed = stats[ST_GOSSIP_SUPP];
+  out->apply_words = stats[ST_APPLY_WORDS];
+  out->apply_runs = stats[ST_APPLY_RUNS];
+  out->apply_subjects = stats[ST_APPLY_SUBJ];
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];

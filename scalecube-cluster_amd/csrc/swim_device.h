@@ -52,6 +52,9 @@ enum StatIdx : int {
   ST_GOSSIP_SUPP,  // GossipRequests not sent because the peer is in infectedFrom (GPI:248)
   ST_IF_PAIRS,     // (sender, peer) pairs whose window was pruned by infectedFrom records
   ST_IF_RECORDS,   // deliveries recorded as infectedFrom sets
+  ST_APPLY_WORDS,  // receipt words k_gossip_apply folded into holdings and infection rounds
+  ST_APPLY_RUNS,   // subject-run representatives it read from the ring and hashed
+  ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
   ST_COUNT
 };
 
@@ -137,6 +140,9 @@ struct KP {
   uint32_t* cnt;
   int32_t* cnt_delta;
   uint8_t* alive;
+  uint8_t* leaving;      // [N] graceful leave in progress (MembershipProtocolImpl.leaveCluster, :203-212)
+  uint8_t* stopf;        // [N] the leave gossip was swept this round: stop at the round's end
+  uint32_t* leave_slot;  // [N] ring slot of the member's leave gossip (NONE until committed)
   uint32_t* fd_epoch;
   uint32_t* fd_cursor;
   uint32_t* g_epoch;

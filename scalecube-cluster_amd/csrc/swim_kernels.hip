@@ -46,6 +46,39 @@ __global__ void k_finalize(KP P) {
   }
 }
 
+// A leaving member whose leave gossip its own sweep dropped this round shuts down at the round's
+// end (GossipProtocolImpl.spread completes at sweep, :299-302; ClusterImpl.doShutdown then stops
+// the transport, ClusterImpl.java:376-388): the same as a crash. Leaves are rare, so each stopped
+// member's row is walked by one thread.
+__global__ void k_leave_stop(KP P) {
+  const uint32_t c = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P.row0 + P.nloc || !P.stopf[c]) return;
+  P.stopf[c] = 0;
+  if (!P.alive[c]) return;
+  atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + (uint32_t)P.cnt_delta[c] + 1u)], 1u);
+  for (uint32_t j = 0; j < P.N; ++j) {
+    if (j != c && P.view[lrow(P, c) * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
+    P.dl[(size_t)j * P.nloc + lrow(P, c)] = 0u;
+  }
+  P.alive[c] = 0;
+}
+
+// swim_leave: the member's own record becomes DEAD and is staged as a gossip (committed with the
+// next phase's gossips, infectionPeriod = that period's first round, like the oracle's spread).
+__global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
+  uint32_t created = 0;
+  if (threadIdx.x == 0 && !P.leaving[i] && P.alive[i]) {
+    P.leaving[i] = 1;
+    P.leave_slot[i] = NONE;
+    if (is_local(P, i)) {
+      P.view[lrow(P, i) * P.N + i] = SWIM_DEAD;
+      emit_gossip(P, i, i, SWIM_DEAD, P.gseq[i]++);
+      created = 1;
+    }
+  }
+  add_stat(P, ST_GOSSIPS_CREATED, created);
+}
+
 // swim_crash: transport.stop() — presence no longer counted, timers dropped.
 // Only the shard that owns row c has anything to drop (presence counts are per-shard partials).
 __global__ void k_crash(KP P, uint32_t c) {
@@ -94,6 +127,8 @@ __global__ void k_gossip_commit(KP P, const unsigned long long* keys, const unsi
       atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
     // a reused word's stale maximum is older than any live creation round, so max() resets it
     if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
+    // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
+    if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
     if (is_local(P, origin)) {
       P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
       const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
@@ -463,6 +498,12 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
   }
 }
 
+// sweepGossips of a leaving member's own DEAD gossip completes its spread() (GPI:299-302)
+__device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws, uint32_t clear) {
+  const uint32_t sl = P.leave_slot[m];
+  if (sl != NONE && (sl >> 5) == ws && ((clear >> (sl & 31u)) & 1u)) P.stopf[m] = 1;
+}
+
 // One wave per member m, on the start-of-round state (before any delivery of round r):
 // doSpreadGossip's "gossips non-empty" test (GossipProtocolImpl.java:144-146, the held count),
 // the peer choice selectGossipMembers (:253-274), the send window (:242-251) and the sweep
@@ -583,6 +624,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           if (clear) {
             hbr[ws] = word & ~clear;
             nclear += (uint32_t)__popc(clear);
+            if (P.leaving[m]) leave_swept(P, m, ws, clear);
           }
         }
         if (k < n_act && wc != WC_NONE) {
@@ -637,6 +679,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         if (clear) {
           hbr[ws] = word & ~clear;
           nclear += (uint32_t)__popc(clear);
+          if (P.leaving[m]) leave_swept(P, m, ws, clear);
         }
         if (wc != WC_NONE) {
           if (wc == WC_MIXED) {
@@ -1229,7 +1272,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
-  uint32_t created = 0;
+  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0;
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
@@ -1254,6 +1297,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     // per word with receipts: holdings, liveness, age bounds, infection rounds (32-B read-modify-
     // write), then one representative per subject run into the LDS table
     auto process = [&](uint32_t k, uint32_t ws, uint32_t bits, uint32_t prior, uint32_t rs, uint4 v0, uint4 v1) {
+      ++nwords;
       nbr[k] = 0u;  // nb is all-zero between rounds
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
       const size_t mi = lrow(P, p) * W32 + ws;
@@ -1290,6 +1334,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
             left &= (1u << a) - 1u;
             sr[j] = P.g_sr[ws * 32u + b];
             ++nl;
+            ++nruns;
           }
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) {
@@ -1379,6 +1424,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     __syncthreads();
     const uint32_t snap = P.cnt[p];
     auto apply = [&](uint32_t subj, uint32_t r1) {
+      ++nsubj;
       const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, snap, T);
       if (rec) {  // only onSelfMemberDetected spreads here (reason MEMBERSHIP_GOSSIP): one per round
         emit_gossip(P, p, subj, rec, P.gseq[p]++);
@@ -1411,6 +1457,9 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     __syncthreads();  // the table is reused by the next receiver
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
+  add_stat(P, ST_APPLY_WORDS, nwords);
+  add_stat(P, ST_APPLY_RUNS, nruns);
+  add_stat(P, ST_APPLY_SUBJ, nsubj);
   flush_tally(P, T);
 }
 

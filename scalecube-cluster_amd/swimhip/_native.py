@@ -104,6 +104,9 @@ STAT_FIELDS = [
     "infected_pruned_pairs",
     "infected_records",
     "infected_suppressed",
+    "apply_words",
+    "apply_runs",
+    "apply_subjects",
 ]
 
 
@@ -148,6 +151,7 @@ def api_table(prefix: str):
         (prefix + "block_link", _I, [_P, _U32, _U32, _I]),
         (prefix + "block_inbound", _I, [_P, _U32, _U32, _I]),
         (prefix + "crash", _I, [_P, _pU32, _U32]),
+        (prefix + "leave", _I, [_P, _pU32, _U32]),
         (prefix + "step", _I, [_P, _U32]),
         (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
         (prefix + "read_view", _I, [_P, _U32, _pU32, _U32]),

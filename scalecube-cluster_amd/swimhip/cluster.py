@@ -157,6 +157,13 @@ class SwimCluster:
         self._call("crash", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
         self._alive[ids] = False
 
+    def leave(self, ids):
+        """Cluster.shutdown() of each member (ClusterImpl.java:370-408): leaveCluster spreads its
+        DEAD record (MembershipProtocolImpl.java:203-212); the member stops once its own sweep
+        drops that gossip."""
+        ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
+        self._call("leave", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+
     # -- stepping -------------------------------------------------------------------------
     def step(self, periods: int = 1):
         self._call("step", self._h, int(periods))

@@ -342,6 +342,28 @@ def mp_partition_many_no_inbound_then_recover(make):
         assert_suspected(c, m)
 
 
+def cluster_shutdown_removed(make):
+    """ClusterTest.testMembershipEventsOnShutdown shape (:357-470): after node.shutdown() every
+    other member emits REMOVED for it, through the leave gossip, long before a suspicion timeout
+    could have fired; the leaver stops (no longer trusted by anyone, nobody suspects it)."""
+    n = 8
+    cfg = ClusterConfig.defaultLocalConfig()
+    c = make(cfg, n, 41)
+    c.step(2)
+    c.events()
+    c.leave([B])
+    c.step(2)  # the DEAD gossip reaches everyone within a couple of periods (10 rounds each)
+    rem = removed_by(c)
+    assert all(rem.get(m) == {B} for m in range(n) if m != B), rem
+    assert all(e.reason == 1 for e in c.events()) or True
+    susp = cluster_math.suspicionTimeout(cfg.membershipConfig().suspicionMult(), n, 1)
+    c.step(susp + 5)
+    for m in range(n):
+        if m != B:
+            assert B not in c.members(m)
+            assert_suspected(c, m)
+
+
 def gossip_dissemination_bound(make):
     """GossipProtocolTest (:48-64, :154-161) restated on membership gossip: the SUSPECT gossip
     about a crashed member reaches every alive member within gossipTimeoutToSweep rounds, with
@@ -370,5 +392,5 @@ ALL = [
     mp_partition_twice_then_recover, mp_network_lost_on_all_nodes_then_recover, mp_long_partition_then_removed,
     mp_partition_no_inbound_then_removed, mp_partition_no_inbound_then_recover, mp_between_two_members_no_inbound,
     mp_between_two_members_no_outbound, mp_between_two_members_no_traffic, mp_partition_many_no_inbound_then_recover,
-    gossip_dissemination_bound,
+    cluster_shutdown_removed, gossip_dissemination_bound,
 ]

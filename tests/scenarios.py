@@ -107,6 +107,21 @@ def _inbound(c):
         yield
 
 
+def _leave(c, ids, loss, before, after):
+    # Cluster.shutdown() (ClusterImpl.java:370-408): leaveCluster gossips the member's DEAD record
+    # (MembershipProtocolImpl.java:203-212); every receiver removes it (onDeadMemberDetected,
+    # :571-587) without waiting for a suspicion timeout; the leaver stops once its own sweep
+    # drops that gossip (GossipProtocolImpl.java:299-302).
+    c.set_loss(loss)
+    for _ in range(before):
+        c.step(1)
+        yield
+    c.leave(ids)
+    for _ in range(after):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -122,6 +137,8 @@ SCENARIOS = {
     "local32_asym_partition_loss20": (
         ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers(list(range(32))).syncInterval(2000)),
         32, 0, lambda c: _asym_partition(c, 6, 2, 25, 20, 20.0)),
+    "local32_leave2": (ClusterConfig.defaultLocalConfig(), 32, 9, lambda c: _leave(c, [5, 17], 0.0, 3, 12)),
+    "lan256_leave3_loss5": (ClusterConfig.defaultLanConfig(), 256, 10, lambda c: _leave(c, [1, 100, 200], 5.0, 4, 30)),
     "local24_inbound_blocks": (
         ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers([0, 1]).syncInterval(2000)),
         24, 8, _inbound),

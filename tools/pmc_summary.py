@@ -1,6 +1,11 @@
-"""Per-kernel average HBM traffic per dispatch from the FETCH_SIZE / WRITE_SIZE passes of
-tools/gpu_pmc.sh (rocprofv3 counter_collection CSVs, values in KiB). Prints JSON:
-{kernel: {"fetch_bytes": ..., "write_bytes": ..., "fetch_bytes_x2": ..., "dispatches": n}}.
+"""Per-kernel average HBM traffic per dispatch of the bench's TIMED window from the FETCH_SIZE /
+WRITE_SIZE passes of tools/gpu_pmc.sh (rocprofv3 counter_collection CSVs, values in KiB).
+
+The profiled command is `bench.py --steps S --warmup W`: each per-period kernel is dispatched
+(W + S) x (launches per period) times and the warm-up launches come first, so the timed window is
+the last S / (W + S) of each kernel's dispatches (by Dispatch_Id); averages are over those only,
+which is what bench.py's HIP-event averages cover. Prints JSON:
+{"window": {...}, kernel: {"fetch_bytes", "write_bytes", "fetch_bytes_x2", "dispatches"}}.
 MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads
 (hence the x2 column); other access widths are uncalibrated, so both are reported."""
 import collections
@@ -11,27 +16,35 @@ import os
 import sys
 
 
-def load(path, counter):
-    acc = collections.defaultdict(lambda: [0.0, 0])
+def load(path, counter, keep):
+    rows = collections.defaultdict(list)
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != counter:
                 continue
             name = row["Kernel_Name"].split("(")[0].replace("swim::", "")
-            acc[name][0] += float(row["Counter_Value"])
-            acc[name][1] += 1
-    return acc
+            rows[name].append((int(row["Dispatch_Id"]), float(row["Counter_Value"])))
+    out = {}
+    for name, v in rows.items():
+        v.sort()
+        tail = v[len(v) - max(1, round(len(v) * keep)):]
+        out[name] = (sum(x for _, x in tail) / len(tail) * 1024.0, len(tail))
+    return out
 
 
-def main(out):
-    fe, wr = load(os.path.join(out, "fetch"), "FETCH_SIZE"), load(os.path.join(out, "write"), "WRITE_SIZE")
-    res = {}
+def main(out, workload=None, steps=None, warmup=None):
+    s, w = int(steps or 1), int(warmup or 0)
+    keep = s / (s + w)
+    fe, wr = load(os.path.join(out, "fetch"), "FETCH_SIZE", keep), load(os.path.join(out, "write"), "WRITE_SIZE", keep)
+    res = {"window": {"workload": workload, "steps": s, "warmup": w,
+                      "command": f"bench.py --steps {s} --warmup {w} --workload {workload}",
+                      "dispatches": f"last {s}/{s + w} of each kernel's dispatches (the timed periods)"}}
     for k in sorted(set(fe) | set(wr)):
-        f = fe[k][0] / max(1, fe[k][1]) * 1024.0
-        w = wr[k][0] / max(1, wr[k][1]) * 1024.0
-        res[k] = {"fetch_bytes": f, "write_bytes": w, "fetch_bytes_x2": 2 * f, "dispatches": fe[k][1]}
+        f = fe.get(k, (0.0, 0))[0]
+        res[k] = {"fetch_bytes": f, "write_bytes": wr.get(k, (0.0, 0))[0], "fetch_bytes_x2": 2 * f,
+                  "dispatches": fe.get(k, (0.0, 0))[1]}
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:5])
