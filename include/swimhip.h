@@ -86,7 +86,7 @@ typedef struct swim_event {
  * ClusterConfig         (api/ClusterConfig.java:24-43)                                    */
 typedef struct swim_config {
   uint32_t n_members;   /* N simulated members (ids 0..N-1)                               */
-  uint32_t mode;        /* 0 = dense N x N views                                          */
+  uint32_t mode;        /* 0 = dense N x N views; 1 = N x K tracked-subject views (below)  */
   uint64_t seed;        /* Philox key                                                     */
   int32_t ping_interval_ms;
   int32_t ping_timeout_ms;
@@ -102,7 +102,10 @@ typedef struct swim_config {
   uint32_t gossip_capacity; /* live gossip slots (power of two; 0 = default)              */
   uint32_t event_capacity;  /* buffered MembershipEvents (0 = events not recorded)        */
   uint32_t sync_capacity;   /* SYNC requests per period (0 = default)                     */
-  uint32_t dirty_capacity;  /* gossip (observer, subject) inbox cells per round (0 = default) */
+  uint32_t tracked_subjects; /* mode 1: K subject columns. A subject gets a column the first time
+                               any observer's record of it leaves the converged baseline (ALIVE,
+                               incarnation 0); untracked subjects read as that baseline in every
+                               view. More than K such subjects -> SWIM_EOVERFLOW */
   uint32_t flags;           /* reserved, 0                                                */
   int32_t device;           /* HIP device ordinal the handle lives on                     */
   uint32_t shard_rank;      /* observer-row shard of this handle (0 .. shard_world-1)     */

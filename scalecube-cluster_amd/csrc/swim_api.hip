@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -149,17 +150,36 @@ void resolve_timing(swim_handle* h) {
 }
 
 // launch helper: optional per-launch HIP-event bracketing on the handle's stream
+// SWIMHIP_DEBUG_SYNC=1: synchronize after every timed launch and name the first kernel that
+// fails (a device fault otherwise surfaces at the next copy, far from its cause)
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = std::getenv("SWIMHIP_DEBUG_SYNC");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
 template <typename F>
-void timed(swim_handle* h, int cls, F&& launch) {
+void timed(swim_handle* h, int cls, const char* name, F&& launch) {
   if (!h->timing) {
     launch();
-    return;
+  } else {
+    hipEvent_t a = take_event(h), b = take_event(h);
+    (void)hipEventRecord(a, h->stream);
+    launch();
+    (void)hipEventRecord(b, h->stream);
+    h->pending.push_back({cls, a, b});
   }
-  hipEvent_t a = take_event(h), b = take_event(h);
-  (void)hipEventRecord(a, h->stream);
-  launch();
-  (void)hipEventRecord(b, h->stream);
-  h->pending.push_back({cls, a, b});
+  if (debug_sync()) {
+    const hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {  // stop at once: nothing more may run on a faulted device
+      std::fprintf(stderr, "swimhip debug: %s (period %llu, phase pc %d) failed: %s\n", name,
+                   (unsigned long long)h->period, h->pc, hipGetErrorString(e));
+      std::fflush(stderr);
+      std::_Exit(3);
+    }
+  }
 }
 
 uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)std::max<uint64_t>(1, (n + bs - 1) / bs); }
@@ -193,6 +213,12 @@ void set_phase(swim_handle* h, KP& P, uint32_t phase) {
   }
 }
 
+// N x K: allocate the requested columns (one thread per subject), then re-sort the column order
+void track_commit(swim_handle* h, const KP& P) {
+  hipLaunchKernelGGL(k_track_alloc, dim3(blocks_for(h->N, 256)), dim3(256), 0, h->stream, P);
+  hipLaunchKernelGGL(k_colorder, dim3(1), dim3(256), 0, h->stream, P);
+}
+
 int read_ctl(swim_handle* h, Ctl* c) {
   HIPC(h, hipMemcpyAsync(c, h->base.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -205,6 +231,8 @@ void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
   x->world = world;
 }
 
+int check_overflow(swim_handle* h);
+
 // Sort the n gossips staged in h->ck[0] / h->cv[0] by (subject, record) and commit them.
 int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
   hipStream_t s = h->stream;
@@ -213,7 +241,7 @@ int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
     const int end_bit = 32 + (int)bitlen(h->N);
     HIPC(h, hipcub::DeviceRadixSort::SortPairs(h->sort_tmp, tb, h->ck[0], h->ck[1], h->cv[0], h->cv[1], (int)n, 0,
                                                 end_bit, s));
-    timed(h, 7, [&] {
+    timed(h, 7, "k_gossip_commit", [&] {
       hipLaunchKernelGGL(k_gossip_commit, dim3(std::min<uint32_t>(blocks_for(n, 256), 2048)), dim3(256), 0, s, P,
                          h->ck[1], h->cv[1], n);
     });
@@ -226,11 +254,18 @@ int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
 // shard's stage first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
   hipStream_t s = h->stream;
-  uint32_t n = 0;
-  HIPC_RC(h, rc, hipMemcpyAsync(&n, &P.ctl->stg_count, 4, hipMemcpyDeviceToHost, s));
+  // {overflow, stg_count} in one copy: a single-GPU run stops at the first phase whose buffers
+  // overflowed (a wrapped gossip ring would otherwise feed the next phase's kernels)
+  static_assert(offsetof(Ctl, stg_count) == offsetof(Ctl, overflow) + 4, "Ctl layout");
+  uint32_t ovn[2] = {0u, 0u};
+  HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 8, hipMemcpyDeviceToHost, s));
   HIPC_RC(h, rc, hipStreamSynchronize(s));
-  n = std::min(n, P.stg_cap);  // beyond: OV_GOSSIP already raised
+  uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
   if (h->world == 1) {
+    if (ovn[0]) {
+      *rc = check_overflow(h);
+      return false;
+    }
     if (n) hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(n, 256)), dim3(256), 0, s, P.stg, n, 0u, h->ck[0], h->cv[0]);
     *rc = commit_sorted(h, P, n);
     return false;
@@ -278,7 +313,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
     switch (h->pc) {
       case PC_FD:  // phase 0: failure detector
         set_phase(h, P, 0);
-        timed(h, 0, [&] { hipLaunchKernelGGL(k_fd, dim3(gL), dim3(256), 0, s, P); });
+        if (P.nxk) {  // N x K: columns for the subjects this FD phase changes first
+          timed(h, 0, "k_fd_track", [&] { hipLaunchKernelGGL(k_fd_track, dim3(gL), dim3(256), 0, s, P); });
+          track_commit(h, P);
+        }
+        timed(h, 0, "k_fd", [&] { hipLaunchKernelGGL(k_fd, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_FD_C;
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
         if (rc) return rc;
@@ -297,10 +336,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.blx = h->d_blx;
           HIPC(h, hipMemsetAsync(P.ctl->xg_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         }
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
-        timed(h, 8, [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 10, [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
-        timed(h, 10, [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
+        timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
+        timed(h, 8, "k_gossip_select", [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
         if (W > 1) {  // (1) registrations with receivers on other shards
           Ctl c;
@@ -382,11 +421,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(h->n_in_pairs, 256)), dim3(256), 0, s, P,
                                h->n_in_pairs);
         }
-        timed(h, 9, [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 1, [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 11, [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
-        timed(h, 2, [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 1, "k_gossip_pull", [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 2, "k_gossip_apply", [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
+        timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
@@ -400,17 +439,17 @@ int period_resume(swim_handle* h, swim_xchg* x) {
       case PC_SUSP:  // phase G+1: suspicion timeouts
         set_phase(h, P, G + 1);
         memset_ctl_u32(h, offsetof(Ctl, due_count));
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_due, dim3(blocks_for(N, 256)), dim3(256), 0, s, P); });
-        timed(h, 3, [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 7, "k_due", [&] { hipLaunchKernelGGL(k_due, dim3(blocks_for(N, 256)), dim3(256), 0, s, P); });
+        timed(h, 3, "k_susp_sweep", [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         // phase G+2: SYNC requests
         set_phase(h, P, G + 2);
         memset_ctl_u32(h, offsetof(Ctl, stage_count));
         HIPC(h, hipMemsetAsync(P.ctl->xs_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
         (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
-        timed(h, 6, [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 7, "k_sync_select", [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 6, "k_sync_snapshot", [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_REQ;
         if (W > 1) {  // tables of requesters whose receiver lives on another shard
           Ctl c;
@@ -439,13 +478,13 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
           if (n_rec) hipLaunchKernelGGL(k_sync_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
-        timed(h, 7, [&] {
+        timed(h, 7, "k_scan", [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
+        timed(h, 7, "k_sync_scatter", [&] {
           hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * nloc, 256)), dim3(256), 0, s, P);
         });
         if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
-        timed(h, 4, [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
         if (W > 1) {  // SYNC_ACK tables back to the requesters' shards, in the order received
           uint64_t back[SWIM_MAX_WORLD];
@@ -466,8 +505,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 5, [&] { hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P); });
-        timed(h, 7, [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
+        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
         if (rc) return rc;
@@ -515,7 +554,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (!cfg || !out) return SWIM_EINVAL;
   *out = nullptr;
   const swim_config& c = *cfg;
-  if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode != 0 || c.ping_interval_ms <= 0 ||
+  if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode > 1 ||
+      (c.mode == 1 && (c.tracked_subjects < 1 || c.tracked_subjects > c.n_members || c.shard_world > 1)) ||
+      c.ping_interval_ms <= 0 ||
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
       c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
     return SWIM_EINVAL;
@@ -550,7 +591,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     const uint64_t bound = (uint64_t)N + (N + h->S - 1) / h->S;
-    const uint64_t fit = (uint64_t)(free_b * 0.30) / (8ull * N);
+    const uint64_t fit = (uint64_t)(free_b * 0.30) / (8ull * (c.mode == 1 ? c.tracked_subjects : N));
     h->scap = (uint32_t)std::max<uint64_t>(64, std::min(bound, fit));
   }
   h->ecap = c.event_capacity;
@@ -594,6 +635,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.rank = c.shard_rank;
   P.nloc = N / world;
   P.row0 = c.shard_rank * P.nloc;
+  P.nxk = c.mode == 1 ? 1u : 0u;
+  P.W = P.nxk ? c.tracked_subjects : N;  // cells per view row
   P.blx = nullptr;
   P.stg_cap = h->GC;
   P.loss_mode = 0;
@@ -601,7 +644,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.link = nullptr;
   P.inlink = nullptr;
 
-  const size_t NN = (size_t)P.nloc * N;  // this shard's rows
+  const size_t NN = (size_t)P.nloc * P.W;  // this shard's rows
   const size_t NL = P.nloc;
   int rc = SWIM_OK;
   uint8_t* group = nullptr;
@@ -615,7 +658,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.hd, NL * h->GC);
   ALLOC(P.mmin, NL * (h->GC / 32));
   ALLOC(P.mmax, NL * (h->GC / 32));
-  ALLOC(P.colmin, N);
+  ALLOC(P.colmin, P.W);
+  if (P.nxk) {
+    ALLOC(P.colmap, N);
+    ALLOC(P.colsubj, P.W);
+    ALLOC(P.colorder, P.W);
+    ALLOC(P.track_req, N);
+  }
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
   ALLOC(P.alive, N);
@@ -693,8 +742,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.req_to, 2ull * N);
   ALLOC(P.req_stage, 2ull * N);
   ALLOC(P.stage_req, h->scap);
-  ALLOC(P.stage_sync, (size_t)h->scap * N);
-  ALLOC(P.stage_ack, (size_t)h->scap * N);
+  ALLOC(P.stage_sync, (size_t)h->scap * P.W);
+  ALLOC(P.stage_ack, (size_t)h->scap * P.W);
   ALLOC(P.recv_count, N);
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
@@ -738,7 +787,11 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
   (void)hipMemsetAsync(P.hb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.wb, 0, NL * (h->GC / 32) * 4, s);
-  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmin, (size_t)N, NONE);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.W, 256)), dim3(256), 0, s, P.colmin, (size_t)P.W, NONE);
+  if (P.nxk) {
+    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmap, (size_t)N, NONE);
+    (void)hipMemsetAsync(P.track_req, 0, N, s);
+  }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, N - 1);
   // presence is per shard: observers of this shard holding the subject (all but the subject itself)
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, P.nloc);
@@ -767,9 +820,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
                      NONE);
-  {  // every member of this shard starts with others = N - 1
-    const uint32_t all = P.nloc;
+  {  // every member of this shard starts with others = N - 1; all N members alive
+    const uint32_t all = P.nloc, alive = N;
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(&P.ctl->alive_count, &alive, 4, hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
   }
   (void)hipMemsetAsync(P.stat_shards, 0, (size_t)STAT_SHARDS * STAT_STRIDE * 8, s);
@@ -857,7 +911,13 @@ int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n) {
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_leave: a period is in flight");
   for (uint32_t k = 0; k < n; ++k)
     if (ids[k] >= h->N) return SWIM_EINVAL;
-  for (uint32_t k = 0; k < n; ++k) hipLaunchKernelGGL(k_leave, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+  for (uint32_t k = 0; k < n; ++k) {
+    if (h->base.nxk) {  // the member's own record leaves the baseline: give it a column
+      hipLaunchKernelGGL(k_track_one, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+      track_commit(h, h->base);
+    }
+    hipLaunchKernelGGL(k_leave, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+  }
   h->n_leaving += n;
   HIPC(h, hipStreamSynchronize(h->stream));
   HIPC(h, hipGetLastError());
@@ -929,28 +989,67 @@ int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n
   return SWIM_OK;
 }
 
+namespace {
+// N x K: the allocated columns' subjects (host copy)
+int tracked_columns(swim_handle* h, std::vector<uint32_t>* subj) {
+  uint32_t nc = 0;
+  HIPC(h, hipMemcpyAsync(&nc, &h->base.ctl->ncols, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  nc = std::min(nc, h->base.W);
+  subj->resize(nc);
+  if (nc) HIPC(h, hipMemcpyAsync(subj->data(), h->base.colsubj, (size_t)nc * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+}  // namespace
+
 int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
   if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
   const size_t lr = observer - h->base.row0;
-  HIPC(h, hipMemcpyAsync(row, h->base.view + lr * h->N, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (!h->base.nxk) {
+    HIPC(h, hipMemcpyAsync(row, h->base.view + lr * h->N, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    return SWIM_OK;
+  }
+  std::vector<uint32_t> subj, cells;
+  int rc = tracked_columns(h, &subj);
+  if (rc) return rc;
+  cells.resize(subj.size());
+  if (!subj.empty())
+    HIPC(h, hipMemcpyAsync(cells.data(), h->base.view + lr * h->base.W, subj.size() * 4, hipMemcpyDeviceToHost,
+                           h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  std::fill(row, row + n, BASELINE);  // untracked subjects: the converged record
+  for (size_t c = 0; c < subj.size(); ++c) row[subj[c]] = cells[c];
   return SWIM_OK;
 }
 
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
   if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
-  // subject-major storage: strided 2D copy of one observer column
-  HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
-                           hipMemcpyDeviceToHost, h->stream));
+  // cell-major storage: strided 2D copy of one observer column
+  if (!h->base.nxk) {
+    HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
+                             hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    return SWIM_OK;
+  }
+  std::vector<uint32_t> subj, cells;
+  int rc = tracked_columns(h, &subj);
+  if (rc) return rc;
+  cells.resize(subj.size());
+  if (!subj.empty())
+    HIPC(h, hipMemcpy2DAsync(cells.data(), 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4,
+                             subj.size(), hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  std::fill(row, row + n, 0u);
+  for (size_t c = 0; c < subj.size(); ++c) row[subj[c]] = cells[c];
   return SWIM_OK;
 }
 
 int swim_digest(swim_handle* h, uint64_t* vd, uint64_t* dd) {
   if (!h) return SWIM_EINVAL;
   HIPC(h, hipMemsetAsync(h->d_digest, 0, 16, h->stream));
-  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base.view, h->base.dl, h->N, h->base.row0,
-                     h->base.nloc, h->d_digest);
+  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base, h->d_digest);
   unsigned long long out[2];
   HIPC(h, hipMemcpyAsync(out, h->d_digest, 16, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -959,9 +1058,38 @@ int swim_digest(swim_handle* h, uint64_t* vd, uint64_t* dd) {
   return SWIM_OK;
 }
 
+namespace {
+// presence per subject; N x K keeps it only for tracked subjects: an untracked one is held by
+// every alive observer but itself
+int presence_host(swim_handle* h, std::vector<uint32_t>* pres, std::vector<uint8_t>* alive) {
+  const uint32_t N = h->N;
+  pres->resize(N);
+  alive->resize(N);
+  HIPC(h, hipMemcpyAsync(pres->data(), h->base.pres, (size_t)N * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(alive->data(), h->base.alive, N, hipMemcpyDeviceToHost, h->stream));
+  if (h->base.nxk) {
+    std::vector<uint32_t> colmap(N);
+    uint32_t alive_count = 0;
+    HIPC(h, hipMemcpyAsync(colmap.data(), h->base.colmap, (size_t)N * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipMemcpyAsync(&alive_count, &h->base.ctl->alive_count, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    for (uint32_t j = 0; j < N; ++j)
+      if (colmap[j] == NONE) (*pres)[j] = alive_count - ((*alive)[j] ? 1u : 0u);
+  }
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+}  // namespace
+
 int swim_read_presence(swim_handle* h, uint32_t* present, uint32_t* last_removed, uint32_t n) {
   if (!h || n != h->N) return SWIM_EINVAL;
-  if (present) HIPC(h, hipMemcpyAsync(present, h->base.pres, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+  if (present) {
+    std::vector<uint32_t> pres;
+    std::vector<uint8_t> alive;
+    int rc = presence_host(h, &pres, &alive);
+    if (rc) return rc;
+    std::memcpy(present, pres.data(), (size_t)n * 4);
+  }
   if (last_removed)
     HIPC(h, hipMemcpyAsync(last_removed, h->base.last_removed, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -972,10 +1100,10 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   if (!h || !out) return SWIM_EINVAL;
   Ctl ctl;
   HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
-  std::vector<uint32_t> pres(h->N);
-  std::vector<uint8_t> alive(h->N);
-  HIPC(h, hipMemcpyAsync(pres.data(), h->base.pres, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
-  HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, h->N, hipMemcpyDeviceToHost, h->stream));
+  std::vector<uint32_t> pres;
+  std::vector<uint8_t> alive;
+  int prc = presence_host(h, &pres, &alive);
+  if (prc) return prc;
   std::vector<unsigned long long> shards((size_t)STAT_SHARDS * STAT_STRIDE);
   HIPC(h, hipMemcpyAsync(shards.data(), h->base.stat_shards, shards.size() * 8, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));

@@ -67,7 +67,10 @@ enum Overflow : uint32_t {
   OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
   OV_IFROM = 64u,  // infectedFrom bookkeeping out of capacity or a delivery predicted never to
                    // matter did: results would no longer be exact
+  OV_TRACK = 128u,  // N x K: more subjects left the baseline than there are columns
 };
+
+constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
 constexpr uint32_t STAT_STRIDE = 32;  // u64 per shard (256 B), >= ST_COUNT
@@ -94,7 +97,10 @@ struct Ctl {
   // infectedFrom bookkeeping: monotone counters of the record pools, and the
   // pools' fill at the start of each round (mod 256), so an allocation can check that it does
   // not overwrite a record still inside the horizon
-  uint32_t rec_cnt, body_cnt, sp_cnt, rp_cnt, pw_used, pad2[3];
+  uint32_t rec_cnt, body_cnt, sp_cnt, rp_cnt, pw_used;
+  uint32_t ncols;        // N x K: columns allocated
+  uint32_t alive_count;  // alive members (N x K: presence of untracked subjects)
+  uint32_t pad2;
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -112,6 +118,13 @@ struct KP {
   // observer-row shard of this handle: members [row0, row0 + nloc) live here;
   // view/inbox/hb/wb/nb/hd rows and dl columns are indexed by the local row m - row0
   uint32_t row0, nloc, rank, world;
+  // view geometry: a row holds W cells; dense W = N (cell = subject), N x K mode (nxk = 1) W = K
+  // (cell = the subject's column, colmap); an untracked subject reads as BASELINE everywhere
+  uint32_t W, nxk;
+  uint32_t* colmap;    // [N] subject -> column, NONE while untracked (N x K only)
+  uint32_t* colsubj;   // [K] column -> subject
+  uint32_t* colorder;  // [K] the allocated columns in subject order (SYNC merges walk it)
+  uint8_t* track_req;  // [N] subjects the coming FD phase changes first (k_fd_track)
   uint32_t sweepmax;  // max gossipPeriodsToSweep + 1: last round a holder may still count a gossip
   uint32_t ecap, scap;
   uint64_t seed;
@@ -215,8 +228,32 @@ struct KP {
   unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
 
+// Debug builds (-DSWIM_DEBUG_BOUNDS, tools/gpu_debug.sh): an index past its array prints the site
+// and is redirected to element 0 instead of faulting the device. Release builds: the index as is.
+#ifdef SWIM_DEBUG_BOUNDS
+#define DBG_IDX(idx, cap, site)                                                                              \
+  (((size_t)(idx) < (size_t)(cap))                                                                          \
+       ? (size_t)(idx)                                                                                      \
+       : (printf("swimhip bounds: %s idx %llu cap %llu block %u thread %u round %u\n", site,                \
+                 (unsigned long long)(idx), (unsigned long long)(cap), blockIdx.x, threadIdx.x, P.round),   \
+          (size_t)0))
+#else
+#define DBG_IDX(idx, cap, site) (idx)
+#endif
+
 __device__ __forceinline__ size_t lrow(const KP& P, uint32_t m) { return (size_t)(m - P.row0); }
 __device__ __forceinline__ bool is_local(const KP& P, uint32_t m) { return m - P.row0 < P.nloc; }
+
+// the cell of subject j in a row (dense: j itself; N x K: its column or NONE while untracked)
+__device__ __forceinline__ uint32_t col_of(const KP& P, uint32_t j) { return P.nxk ? P.colmap[j] : j; }
+__device__ __forceinline__ uint32_t subj_of(const KP& P, uint32_t c) { return P.nxk ? P.colsubj[c] : c; }
+// cells in use per row: dense N, N x K the columns allocated so far
+__device__ __forceinline__ uint32_t ncells(const KP& P);
+// observer obs's record of subject j (membershipTable.get, MembershipProtocolImpl.java:487)
+__device__ __forceinline__ uint32_t cell_get(const KP& P, uint32_t obs, uint32_t j) {
+  const uint32_t c = col_of(P, j);
+  return c == 0xFFFFFFFFu ? BASELINE : P.view[lrow(P, obs) * P.W + c];
+}
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t REMOTE = 0xFFFFFFFEu;   // req_stage of a request staged on another shard
@@ -227,6 +264,8 @@ constexpr uint32_t SPAIR = 0x40000000u;  // in_list entry: a pruned pair (window
 constexpr uint32_t IHCAP = 256;  // in-history entries per member (~f per round over the horizon)
 constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
 constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
+
+__device__ __forceinline__ uint32_t ncells(const KP& P) { return P.nxk ? P.ctl->ncols : P.N; }
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {
   return bm && (bm[bit >> 3] & (1u << (bit & 7)));
@@ -319,7 +358,12 @@ __device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t sub
 // number so that every origin's ids are canonical.
 __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint32_t subj, uint32_t r1,
                                                  uint32_t reason, uint32_t attempt, uint32_t others_snap, Tally& T) {
-  uint32_t* cellp = P.view + lrow(P, obs) * P.N + subj;
+  const uint32_t col = col_of(P, subj);
+  if (col == NONE) {  // N x K: k_fd_track gives every subject a column before its first change
+    atomicOr(&P.ctl->overflow, OV_TRACK);
+    return 0u;
+  }
+  uint32_t* cellp = P.view + lrow(P, obs) * P.W + col;
   const uint32_t r0 = *cellp;
   if (!is_overrides(r1, r0)) return 0u;
   const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;
@@ -332,7 +376,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.refut++;
     return r2;
   }
-  uint32_t* dlp = P.dl + (size_t)subj * P.nloc + lrow(P, obs);
+  uint32_t* dlp = P.dl + (size_t)col * P.nloc + lrow(P, obs);
   if (r1 == SWIM_DEAD) {
     *dlp = 0u;
     *cellp = SWIM_ABSENT;
@@ -350,7 +394,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     if (*dlp == 0u) {
       const uint32_t dl = P.period + susp_periods(P, others_snap);
       *dlp = dl + 1u;
-      atomicMin(&P.colmin[subj], dl);
+      atomicMin(&P.colmin[col], dl);
     }
     return spread ? r1 : 0u;
   }

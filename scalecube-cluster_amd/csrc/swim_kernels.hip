@@ -56,9 +56,12 @@ __global__ void k_leave_stop(KP P) {
   P.stopf[c] = 0;
   if (!P.alive[c]) return;
   atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + (uint32_t)P.cnt_delta[c] + 1u)], 1u);
-  for (uint32_t j = 0; j < P.N; ++j) {
-    if (j != c && P.view[lrow(P, c) * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[(size_t)j * P.nloc + lrow(P, c)] = 0u;
+  atomicSub(&P.ctl->alive_count, 1u);
+  const uint32_t nc = ncells(P);
+  for (uint32_t cc = 0; cc < nc; ++cc) {
+    const uint32_t j = subj_of(P, cc);
+    if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
+    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
   }
   P.alive[c] = 0;
 }
@@ -71,7 +74,7 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
     P.leaving[i] = 1;
     P.leave_slot[i] = NONE;
     if (is_local(P, i)) {
-      P.view[lrow(P, i) * P.N + i] = SWIM_DEAD;
+      P.view[lrow(P, i) * P.W + col_of(P, i)] = SWIM_DEAD;  // N x K: k_track_one gave i a column
       emit_gossip(P, i, i, SWIM_DEAD, P.gseq[i]++);
       created = 1;
     }
@@ -83,10 +86,15 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
 // Only the shard that owns row c has anything to drop (presence counts are per-shard partials).
 __global__ void k_crash(KP P, uint32_t c) {
   if (!is_local(P, c)) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < P.N; j += gridDim.x * blockDim.x) {
-    if (j != c && P.view[lrow(P, c) * P.N + j] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[(size_t)j * P.nloc + lrow(P, c)] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
+    atomicSub(&P.ctl->alive_count, 1u);  // N x K: every untracked subject loses this observer
+  }
+  const uint32_t nc = ncells(P);
+  for (uint32_t cc = blockIdx.x * blockDim.x + threadIdx.x; cc < nc; cc += gridDim.x * blockDim.x) {
+    const uint32_t j = subj_of(P, cc);
+    if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
+    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
   }
 }
 
@@ -147,6 +155,129 @@ __global__ void k_gossip_commit_fin(KP P, uint32_t n) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Phase 0: failure detector.
+// ---------------------------------------------------------------------------------------
+struct Probe {
+  uint32_t j, nA, nB, stB, preq, direct;  // outcome: nA SUSPECT events, then nB events of status stB
+};
+
+// doPing / doPingReq (FailureDetectorImpl.java:126-209) of alive observer i with others > 0:
+// selectPingMember advances i's cursor (written back only when `commit`), then the outcome of the
+// direct ping or the ping-req round.
+__device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) {
+  Probe pr = {NONE, 0u, 0u, SWIM_SUSPECT, 0u, 0u};
+  const uint32_t N = P.N;
+  const uint32_t half = perm_half_bits(N);
+  // selectPingMember (FailureDetectorImpl.java:340-349)
+  uint32_t ep = P.fd_epoch[i], cur = P.fd_cursor[i];
+  PermKey key = perm_key(P.seed, K_FD_PERM, i, ep);
+  uint32_t j = NONE;
+  for (uint32_t guard = 0; guard < 2u * N + 2u; ++guard) {
+    if (cur >= N) {
+      cur = 0;
+      ++ep;
+      key = perm_key(P.seed, K_FD_PERM, i, ep);
+    }
+    const uint32_t x = perm_apply(cur++, N, half, key);
+    if (x != i && cell_get(P, i, x) != 0u) {
+      j = x;
+      break;
+    }
+  }
+  if (commit) {
+    P.fd_epoch[i] = ep;
+    P.fd_cursor[i] = cur;
+  }
+  if (j == NONE) {  // member count says >0 but the row holds nobody: invariant broken
+    atomicOr(&P.ctl->overflow, OV_BUG);
+    j = (i + 1) % N;
+  }
+  pr.j = j;
+  if (delivered(P, K_PING, i, j, 0, P.tick) && delivered(P, K_ACK, j, i, 0, P.tick)) {
+    pr.direct = 1;
+    pr.nB = 1;
+    pr.stB = SWIM_ALIVE;
+    return pr;
+  }
+  // selectPingReqMembers (FailureDetectorImpl.java:351-363)
+  uint32_t proxies[MAXK];
+  uint32_t np = 0;
+  if (P.kreq > 0u) {
+    const PermKey pk = perm_key(P.seed, K_PROXY_PERM, i, P.period);
+    for (uint32_t pos = 0; pos < N && np < P.kreq; ++pos) {
+      const uint32_t x = perm_apply(pos, N, half, pk);
+      if (x != i && x != j && cell_get(P, i, x) != 0u) proxies[np++] = x;
+    }
+  }
+  if (!P.time_left_pos || np == 0) {
+    pr.nB = 1;  // FailureDetectorImpl.java:163-165
+    return pr;
+  }
+  pr.preq = 1;
+  uint32_t first = NONE;  // the proxy whose forwarded ack reaches i's transport first
+  for (uint32_t q = 0; q < np; ++q) {
+    const uint32_t p = proxies[q];
+    if (!out_ok(P, K_PING_REQ, i, p, j, P.tick)) {
+      ++pr.nA;  // NetworkEmulator send error -> immediate SUSPECT
+      continue;
+    }
+    ++pr.nB;
+    if (first == NONE && in_ok(P, p, i) && delivered(P, K_PROXY_PING, p, j, i, P.tick) &&
+        delivered(P, K_PROXY_ACK, j, p, i, P.tick) && out_ok(P, K_FWD_ACK, p, i, j, P.tick))
+      first = p;
+  }
+  // cid-only matching (TransportImpl.java:236-238): that ack completes every pending
+  // subscription, then i's inbound filter on its sender decides (NetworkEmulatorTransport.java:64-68)
+  pr.stB = (first != NONE && in_ok(P, i, first)) ? SWIM_ALIVE : SWIM_SUSPECT;
+  return pr;
+}
+
+// N x K mode, before the FD phase: an untracked target whose record this probe turns SUSPECT
+// (the only way a subject's record first leaves the baseline: every later change — gossip,
+// SYNC, timeout, refutation — concerns a subject some record already changed) needs a column.
+__global__ void __launch_bounds__(256) k_fd_track(KP P) {
+  const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
+    const Probe pr = fd_probe(P, i, false);
+    if (pr.nA + pr.nB > 0u && (pr.nA > 0u || pr.stB == SWIM_SUSPECT) && P.colmap[pr.j] == NONE)
+      P.track_req[pr.j] = 1;
+  }
+}
+
+// One thread per requested subject: the next free column (pre-filled with BASELINE cells), its
+// presence materialised (every alive observer but itself holds it), no deadline.
+__global__ void k_track_alloc(KP P) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P.N || !P.track_req[j]) return;
+  P.track_req[j] = 0;
+  if (P.colmap[j] != NONE) return;
+  const uint32_t c = atomicAdd(&P.ctl->ncols, 1u);
+  if (c >= P.W) {
+    atomicOr(&P.ctl->overflow, OV_TRACK);
+    return;
+  }
+  P.colsubj[c] = j;
+  P.pres[j] = P.ctl->alive_count - (P.alive[j] ? 1u : 0u);
+  P.colmap[j] = c;
+}
+
+// the allocated columns in subject order (SYNC merges assign gossip sequence numbers in it)
+__global__ void __launch_bounds__(256) k_colorder(KP P) {
+  const uint32_t n = P.ctl->ncols < P.W ? P.ctl->ncols : P.W;
+  for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
+    const uint32_t sj = P.colsubj[c];
+    uint32_t rank = 0;
+    for (uint32_t d = 0; d < n; ++d) rank += P.colsubj[d] < sj ? 1u : 0u;
+    P.colorder[rank] = c;
+  }
+}
+
+// N x K: give subject j a column now (swim_leave: the member's own record changes)
+__global__ void k_track_one(KP P, uint32_t j) {
+  if (threadIdx.x == 0) P.track_req[j] = P.colmap[j] == NONE ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // Phase 0: failure detector, one thread per observer.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_fd(KP P) {
@@ -154,79 +285,20 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
   uint32_t probes = 0, direct = 0, preq = 0, sev = 0, aev = 0, created = 0;
   Tally T;
   if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
-    const uint32_t N = P.N;
-    const uint32_t half = perm_half_bits(N);
-    const uint32_t* row = P.view + lrow(P, i) * N;
-    // selectPingMember (FailureDetectorImpl.java:340-349)
-    uint32_t ep = P.fd_epoch[i], cur = P.fd_cursor[i];
-    PermKey key = perm_key(P.seed, K_FD_PERM, i, ep);
-    uint32_t j = NONE;
-    for (uint32_t guard = 0; guard < 2u * N + 2u; ++guard) {
-      if (cur >= N) {
-        cur = 0;
-        ++ep;
-        key = perm_key(P.seed, K_FD_PERM, i, ep);
-      }
-      const uint32_t x = perm_apply(cur++, N, half, key);
-      if (x != i && row[x] != 0u) {
-        j = x;
-        break;
-      }
-    }
-    P.fd_epoch[i] = ep;
-    P.fd_cursor[i] = cur;
-    if (j == NONE) {  // member count says >0 but the row holds nobody: invariant broken
-      atomicOr(&P.ctl->overflow, OV_BUG);
-      j = (i + 1) % N;
-    }
+    const Probe pr = fd_probe(P, i, true);
+    const uint32_t j = pr.j;
     probes = 1;
-    // outcome as (nA SUSPECT events, then nB events of status stB) — DESIGN.md §3.3
-    uint32_t nA = 0, nB = 0, stB = SWIM_SUSPECT;
-    if (delivered(P, K_PING, i, j, 0, P.tick) && delivered(P, K_ACK, j, i, 0, P.tick)) {
-      direct = 1;
-      nB = 1;
-      stB = SWIM_ALIVE;
-    } else {
-      // selectPingReqMembers (FailureDetectorImpl.java:351-363)
-      uint32_t proxies[MAXK];
-      uint32_t np = 0;
-      if (P.kreq > 0u) {
-        const PermKey pk = perm_key(P.seed, K_PROXY_PERM, i, P.period);
-        for (uint32_t pos = 0; pos < N && np < P.kreq; ++pos) {
-          const uint32_t x = perm_apply(pos, N, half, pk);
-          if (x != i && x != j && row[x] != 0u) proxies[np++] = x;
-        }
-      }
-      if (!P.time_left_pos || np == 0) {
-        nB = 1;  // FailureDetectorImpl.java:163-165
-      } else {
-        preq = 1;
-        uint32_t first = NONE;  // the proxy whose forwarded ack reaches i's transport first
-        for (uint32_t q = 0; q < np; ++q) {
-          const uint32_t p = proxies[q];
-          if (!out_ok(P, K_PING_REQ, i, p, j, P.tick)) {
-            ++nA;  // NetworkEmulator send error -> immediate SUSPECT
-            continue;
-          }
-          ++nB;
-          if (first == NONE && in_ok(P, p, i) && delivered(P, K_PROXY_PING, p, j, i, P.tick) &&
-              delivered(P, K_PROXY_ACK, j, p, i, P.tick) && out_ok(P, K_FWD_ACK, p, i, j, P.tick))
-            first = p;
-        }
-        // cid-only matching (TransportImpl.java:236-238): that ack completes every pending
-        // subscription, then i's inbound filter on its sender decides (NetworkEmulatorTransport.java:64-68)
-        stB = (first != NONE && in_ok(P, i, first)) ? SWIM_ALIVE : SWIM_SUSPECT;
-      }
-    }
+    direct = pr.direct;
+    preq = pr.preq;
     // publishPingResult -> onFailureDetectorEvent, sequentially (MembershipProtocolImpl.java:376-404)
     const uint32_t snap = P.cnt[i];
-    for (uint32_t e = 0; e < nA + nB; ++e) {
-      const uint32_t st = e < nA ? (uint32_t)SWIM_SUSPECT : stB;
+    for (uint32_t e = 0; e < pr.nA + pr.nB; ++e) {
+      const uint32_t st = e < pr.nA ? (uint32_t)SWIM_SUSPECT : pr.stB;
       if (st == SWIM_ALIVE)
         ++aev;
       else
         ++sev;
-      const uint32_t r0 = row[j];
+      const uint32_t r0 = cell_get(P, i, j);
       if (r0 == 0u || rec_code(r0) == st) continue;
       if (st == SWIM_ALIVE) {
         P.sync_fd[i] = j;
@@ -348,17 +420,16 @@ __device__ __forceinline__ bool may_select(const KP& P, uint32_t p, uint32_t s) 
   // Exact refinement: selectGossipMembers takes the first f present members from the cursor each
   // round, so s comes up once the present members ahead of it are used up. Members removed in
   // the meantime only bring it closer: a quarter of margin (a misprediction raises OV_IFROM).
-  const uint32_t* row = P.view + lrow(P, p) * N;
   uint32_t ahead = 0;
   const uint32_t end0 = wrap ? N : pos;
   for (uint32_t x = cur; x < end0; ++x) {
     const uint32_t m = perm_apply(x, N, half, k0);
-    ahead += (m != p && row[m] != 0u) ? 1u : 0u;
+    ahead += (m != p && cell_get(P, p, m) != 0u) ? 1u : 0u;
   }
   if (wrap)
     for (uint32_t x = 0; x < pos; ++x) {
       const uint32_t m = perm_apply(x, N, half, k1);
-      ahead += (m != p && row[m] != 0u) ? 1u : 0u;
+      ahead += (m != p && cell_get(P, p, m) != 0u) ? 1u : 0u;
     }
   return ahead < (P.f * P.hzn * 5u) / 4u + 16u;
 }
@@ -407,6 +478,10 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     const uint32_t hi = c->gcount;
     uint32_t lo = c->glo;
     if (hi - lo > P.GC) lo = hi - P.GC;
+    // a full ring (k_gossip_commit has raised OV_GOSSIP): keep the listed words within one lap of
+    // the ring, so no list position reaches past a W32-word row of wb / nb
+    const uint32_t lo_w = (((hi + 31u) >> 5) - (P.GC >> 5)) << 5;
+    if (((hi + 31u) >> 5) - (lo >> 5) > (P.GC >> 5)) lo = lo_w;
     const uint32_t first = s_first == NONE ? hi : (s_first << 5);
     if (first > lo) lo = first < hi ? first : hi;
     c->glo = lo;
@@ -632,7 +707,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
           if (wc == WC_MIXED) {
             ++winw;
-            wbr[k] = win;
+            wbr[DBG_IDX(k, W32, "select wbr")] = win;
           }
           win_l |= win != 0u;
           winbits += (uint32_t)__popc(win);
@@ -684,7 +759,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         if (wc != WC_NONE) {
           if (wc == WC_MIXED) {
             ++winw;
-            wbr[k] = win;
+            wbr[DBG_IDX(k, W32, "select wbr")] = win;
           }
           win_l |= win != 0u;
           winbits += (uint32_t)__popc(win);
@@ -696,11 +771,10 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   if (any) {
     // selectGossipMembers, wave-cooperative: lanes test 64 consecutive positions of the
     // keyed shuffle, ballot, take the first members in position order.
-    const uint32_t* row = P.view + lrow(P, m) * N;
     if (others < P.f) {
       for (uint32_t base = 0; base < N; base += 64u) {
         const uint32_t x = base + lane;
-        const bool ok = x < N && x != m && row[x] != 0u;
+        const bool ok = x < N && x != m && cell_get(P, m, x) != 0u;
         const unsigned long long b = __ballot(ok);
         if (ok) {
           const uint32_t rank = np + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
@@ -722,7 +796,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           bool ok = false;
           if (p < N) {
             x = perm_apply(p, N, half, key);
-            ok = x != m && row[x] != 0u;
+            ok = x != m && cell_get(P, m, x) != 0u;
           }
           const unsigned long long b = __ballot(ok);
           const uint32_t need = P.f - np;
@@ -1068,11 +1142,11 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       uint32_t sreg = 0, cdeg = 0;
       if (done == 0) {
         cdeg = deg < INCAP ? deg : INCAP;
-        if (lane < cdeg) sreg = P.in_list[(size_t)p * INCAP + lane];
+        if (lane < cdeg) sreg = P.in_list[DBG_IDX((size_t)p * INCAP + lane, (size_t)P.N * INCAP, "pull in_list")];
       } else {
         while (cdeg == 0 && ov_pos < n_ov) {
           const uint32_t o = ov_pos + lane;
-          const bool mine = o < n_ov && P.in_ov[2 * o] == p;
+          const bool mine = o < n_ov && P.in_ov[DBG_IDX(2ull * o, 2ull * P.N * P.f, "pull in_ov")] == p;
           const unsigned long long b = __ballot(mine);
           const uint32_t rank = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
           const uint32_t snd = mine ? P.in_ov[2 * o + 1] : 0u;
@@ -1095,7 +1169,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
         if (sreg & XREC) {
           sid = P.rpairs[2 * (sreg & ~XREC)];
         } else if (sreg & SPAIR) {
-          const uint4 sp = P.sp_list[sreg & ~SPAIR];
+          const uint4 sp = P.sp_list[DBG_IDX(sreg & ~SPAIR, P.spcap, "pull sp_list")];
           sid = sp.x;
           pwo = sp.w;
         } else {
@@ -1143,7 +1217,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
         }
         if (!todo) continue;
         if (!first_chunk) {  // later chunks only add gossips earlier ones did not bring
-          const uint4 p4 = *reinterpret_cast<const uint4*>(nbr + kq);
+          const uint4 p4 = *reinterpret_cast<const uint4*>(nbr + DBG_IDX(kq, W32 - 3u, "pull nbr4"));
           prev[0] = p4.x;
           prev[1] = p4.y;
           prev[2] = p4.z;
@@ -1158,11 +1232,11 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
             mv[j] = has ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
             uint4 wa = make_uint4(0u, 0u, 0u, 0u), wm = make_uint4(0u, 0u, 0u, 0u);
             if (has && (en & SPAIR)) {  // pruned pair: its window was written to pw
-              const uint32_t* pwr = P.pw + s_pwo[threadIdx.x >> 6][q0 + j];
-              wm = *reinterpret_cast<const uint4*>(pwr + kq);  // act-indexed, padded to quads
+              wm = *reinterpret_cast<const uint4*>(
+                  P.pw + DBG_IDX((size_t)s_pwo[threadIdx.x >> 6][q0 + j] + kq, P.pwcap - 3u, "pull pw"));  // act-indexed, padded to quads
             } else if (has && !(en & XREC) && quad) {
-              if (anyall) wa = *reinterpret_cast<const uint4*>(P.hb + lrow(P, en) * W32 + ws0);
-              if (anymix) wm = *reinterpret_cast<const uint4*>(P.wb + lrow(P, en) * W32 + kq);
+              if (anyall) wa = *reinterpret_cast<const uint4*>(P.hb + DBG_IDX(lrow(P, en) * W32 + ws0, (size_t)P.nloc * W32 - 3u, "pull hb4"));
+              if (anymix) wm = *reinterpret_cast<const uint4*>(P.wb + DBG_IDX(lrow(P, en) * W32 + DBG_IDX(kq, W32 - 3u, "pull wb4 kq"), (size_t)P.nloc * W32 - 3u, "pull wb4"));
             }
             const uint32_t waa[4] = {wa.x, wa.y, wa.z, wa.w}, wma[4] = {wm.x, wm.y, wm.z, wm.w};
 #pragma unroll
@@ -1176,8 +1250,8 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
                 else if (quad)
                   v = wcv[i] == WC_ALL ? waa[i] & live[i] : wma[i];
                 else
-                  v = wcv[i] == WC_ALL ? P.hb[lrow(P, en) * W32 + wsv[i]] & live[i]
-                                       : P.wb[lrow(P, en) * W32 + kq + i];
+                  v = wcv[i] == WC_ALL ? P.hb[DBG_IDX(lrow(P, en) * W32 + wsv[i], (size_t)P.nloc * W32, "pull hb")] & live[i]
+                                       : P.wb[DBG_IDX(lrow(P, en) * W32 + DBG_IDX(kq + i, W32, "pull wb kq"), (size_t)P.nloc * W32, "pull wb")];
               }
               wv[j][i] = v;
             }
@@ -1208,7 +1282,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
 #pragma unroll
         for (uint32_t i = 0; i < 4u; ++i)
           if (u[i]) {  // holdings are updated by k_gossip_apply, after every receiver has pulled
-            nbr[kq + i] = prev[i] | u[i];
+            nbr[DBG_IDX(kq + i, W32, "pull nbr")] = prev[i] | u[i];
             receipts += (uint32_t)__popc(u[i]);
             sbits |= 1u << ((kq + i) & 31u);
           }
@@ -1219,7 +1293,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
     const uint32_t total = wave_sum(receipts);
     if (lane == 0 && total) {
       const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);
-      P.alist[2 * idx] = p;
+      P.alist[DBG_IDX(2ull * idx, 2ull * P.N, "pull alist")] = p;
       P.alist[2 * idx + 1] = total;
     }
     if (total && nsw <= NSUM) {
@@ -1352,7 +1426,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
             h = (h + 1u) & hm;
           }
           if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
-            if (atomicMax(&P.inbox[lrow(P, p) * P.N + sr[j].x], sr[j].y) == 0u) {
+            if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr[j].x)], sr[j].y) == 0u) {
               const uint32_t o = atomicAdd(&s_nspill, 1u);
               if (o < SPILL_CAP)
                 s_spl[o] = sr[j].x;
@@ -1451,7 +1525,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     if (nsp) __threadfence();
     for (uint32_t t = threadIdx.x; t < nsp; t += blockDim.x) {
       const uint32_t subj = s_spl[t];
-      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.N + subj], 0u));
+      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
     }
     if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
     __syncthreads();  // the table is reused by the next receiver
@@ -1699,9 +1773,9 @@ __global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
 // ---------------------------------------------------------------------------------------
 // Suspicion timeouts: stream due subject columns of the deadline matrix.
 // ---------------------------------------------------------------------------------------
-__global__ void k_due(KP P) {
+__global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < P.N && P.colmin[j] <= P.period) {
+  if (j < ncells(P) && P.colmin[j] <= P.period) {
     const uint32_t idx = atomicAdd(&P.ctl->due_count, 1u);
     P.due[idx] = j;
   }
@@ -1713,7 +1787,7 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   uint32_t fired = 0;
   const uint32_t n = P.ctl->due_count;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const uint32_t j = P.due[k];
+    const uint32_t j = P.due[k];  // the cell; its subject is subj_of(j)
     uint32_t* col = P.dl + (size_t)j * P.nloc;
     uint32_t mn = NONE;
     for (uint32_t li = threadIdx.x; li < P.nloc; li += blockDim.x) {
@@ -1727,9 +1801,9 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
       const uint32_t dl = v - 1u;
       if (dl <= P.period) {  // onSuspicionTimeout (MembershipProtocolImpl.java:637-647)
         col[li] = 0u;
-        if (P.view[(size_t)li * P.N + j] != 0u) {
+        if (P.view[(size_t)li * P.W + j] != 0u) {
           ++fired;
-          apply_record(P, i, j, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
+          apply_record(P, i, subj_of(P, j), SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
         }
       } else if (dl < mn) {
         mn = dl;
@@ -1760,19 +1834,18 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
 // selectSyncAddress (MembershipProtocolImpl.java:416-427): uniform over seeds U others.
 __device__ uint32_t select_sync_address(const KP& P, uint32_t i) {
   const uint32_t N = P.N;
-  const uint32_t* row = P.view + lrow(P, i) * N;
   uint32_t count = P.cnt[i];
   for (uint32_t s = 0; s < P.n_seeds && s < N; ++s)
-    if (s != i && row[s] == 0u) ++count;
+    if (s != i && cell_get(P, i, s) == 0u) ++count;
   if (count == 0u) return NONE;
   uint32_t x = 0;
   for (uint32_t a = 0; a < 64u; ++a) {
     x = (uint32_t)(((uint64_t)draw1(P.seed, K_SYNC_PICK, i, a, 0, P.tick) * N) >> 32);
-    if (x != i && (row[x] != 0u || x < P.n_seeds)) return x;
+    if (x != i && (cell_get(P, i, x) != 0u || x < P.n_seeds)) return x;
   }
   for (uint32_t d = 1; d <= N; ++d) {
     const uint32_t y = (uint32_t)(((uint64_t)x + d) % N);
-    if (y != i && (row[y] != 0u || y < P.n_seeds)) return y;
+    if (y != i && (cell_get(P, i, y) != 0u || y < P.n_seeds)) return y;
   }
   return NONE;
 }
@@ -1823,14 +1896,14 @@ __global__ void k_sync_select(KP P) {
 __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
   uint32_t n = P.ctl->stage_count;
   if (n > P.scap) n = P.scap;
-  const uint32_t nv = P.N / 4u;
+  const uint32_t W = ncells(P), nv = (P.W & 3u) ? 0u : W / 4u;  // a row = the first ncells cells
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t from = P.stage_req[k] >> 1;
-    const uint4* src = reinterpret_cast<const uint4*>(P.view + lrow(P, from) * P.N);
-    uint4* dst = reinterpret_cast<uint4*>(P.stage_sync + (size_t)k * P.N);
+    const uint4* src = reinterpret_cast<const uint4*>(P.view + lrow(P, from) * P.W);
+    uint4* dst = reinterpret_cast<uint4*>(P.stage_sync + (size_t)k * P.W);
     for (uint32_t c = threadIdx.x; c < nv; c += blockDim.x) dst[c] = src[c];
-    for (uint32_t c = nv * 4u + threadIdx.x; c < P.N; c += blockDim.x)
-      P.stage_sync[(size_t)k * P.N + c] = P.view[lrow(P, from) * P.N + c];
+    for (uint32_t c = nv * 4u + threadIdx.x; c < W; c += blockDim.x)
+      P.stage_sync[(size_t)k * P.W + c] = P.view[lrow(P, from) * P.W + c];
   }
 }
 
@@ -1897,32 +1970,38 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tot
 __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint32_t* src, uint32_t* ack_out,
                                           uint32_t attempt, uint32_t snap, uint32_t& seq, Tally& T, uint32_t& created,
                                           uint32_t* lds4) {
-  const uint32_t N = P.N;
-  uint32_t* row = P.view + lrow(P, obs) * N;
-  // 4 cells per thread (16-B loads) when rows are 16-B aligned, else 1; cells that the
-  // incoming record does not override (the common case) never enter updateMembership.
-  const uint32_t per = (N & 3u) == 0u ? 4u : 1u;
-  for (uint32_t c0 = 0; c0 < N; c0 += 256u * per) {
+  uint32_t* row = P.view + lrow(P, obs) * P.W;
+  // Dense rows: cell = subject, 4 cells per thread (16-B loads) when rows are 16-B aligned.
+  // N x K rows: one column per thread, walked in subject order (colorder) so gossip sequence
+  // numbers come out exactly as in the dense table; untracked subjects hold BASELINE on both
+  // sides, and equal records never override (MembershipProtocolImpl.java:489).
+  // Cells the incoming record does not override (the common case) never enter updateMembership.
+  const uint32_t nc = ncells(P);
+  const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
+  for (uint32_t c0 = 0; c0 < nc; c0 += 256u * per) {
     const uint32_t c = c0 + per * threadIdx.x;
     uint32_t recs[4], cells[4], nrec = 0;
-    if (c < N) {
-      uint32_t sv[4], vv[4];
+    if (c < nc) {
+      uint32_t sv[4], vv[4], cv[4];
       if (per == 4u) {
         const uint4 s4 = *reinterpret_cast<const uint4*>(src + c);
         const uint4 v4 = *reinterpret_cast<const uint4*>(row + c);
         sv[0] = s4.x, sv[1] = s4.y, sv[2] = s4.z, sv[3] = s4.w;
         vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+        cv[0] = c, cv[1] = c + 1u, cv[2] = c + 2u, cv[3] = c + 3u;
       } else {
-        sv[0] = src[c];
-        vv[0] = row[c];
+        cv[0] = P.nxk ? P.colorder[c] : c;
+        sv[0] = src[cv[0]];
+        vv[0] = row[cv[0]];
       }
       for (uint32_t k = 0; k < per; ++k) {
         if (sv[k] == 0u || !is_overrides(sv[k], vv[k])) continue;
-        const uint32_t rec = apply_record(P, obs, c + k, sv[k], SWIM_R_SYNC, attempt, snap, T);
-        vv[k] = row[c + k];
+        const uint32_t subj = subj_of(P, cv[k]);
+        const uint32_t rec = apply_record(P, obs, subj, sv[k], SWIM_R_SYNC, attempt, snap, T);
+        vv[k] = row[cv[k]];
         if (rec) {
           recs[nrec] = rec;
-          cells[nrec] = c + k;
+          cells[nrec] = subj;
           ++nrec;
         }
       }
@@ -1930,10 +2009,10 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
         if (per == 4u)
           *reinterpret_cast<uint4*>(ack_out + c) = make_uint4(vv[0], vv[1], vv[2], vv[3]);
         else
-          ack_out[c] = vv[0];
+          ack_out[cv[0]] = vv[0];
       }
     }
-    if (__syncthreads_or(nrec != 0u)) {  // gossip sequence numbers in cell order
+    if (__syncthreads_or(nrec != 0u)) {  // gossip sequence numbers in subject order
       uint32_t total;
       const uint32_t off = block_excl_scan256(nrec, &total, lds4);
       for (uint32_t k = 0; k < nrec; ++k) emit_gossip(P, obs, cells[k], recs[k], seq + off + k);
@@ -1981,8 +2060,8 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
     uint32_t* ack;
     if (is_local(P, q >> 1)) {
       const uint32_t slot = P.req_stage[q];
-      src = P.stage_sync + (size_t)slot * P.N;
-      ack = P.stage_ack + (size_t)slot * P.N;
+      src = P.stage_sync + (size_t)slot * P.W;
+      ack = P.stage_ack + (size_t)slot * P.W;
     } else {  // request from another shard: payload in the received record, ack into the same
       const size_t g = (size_t)P.rs_ref[q] * (P.N + 2u);  // position of the send buffer
       src = P.xrecv + g + 2;
@@ -1995,7 +2074,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
     merge_row(P, j, src, ack, q, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
-  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * P.N : 0u);
+  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * ncells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -2032,12 +2111,12 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
     const uint32_t slot = P.req_stage[q[k]];
     const uint32_t attempt = (to[k] << 1) | (q[k] & 1u);
     const uint32_t* src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[q[k]] * (P.N + 2u) + 2
-                                         : P.stage_ack + (size_t)slot * P.N;
+                                         : P.stage_ack + (size_t)slot * P.W;
     merge_row(P, i, src, nullptr, attempt, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
-  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * P.N : 0u);
+  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * ncells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -2045,17 +2124,23 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
 // ---------------------------------------------------------------------------------------
 // Observability.
 // ---------------------------------------------------------------------------------------
-__global__ void k_digest(const uint32_t* view, const uint32_t* dl, uint32_t N, uint32_t row0, uint32_t nloc,
-                         unsigned long long* out) {
+// Order-independent digests of every (observer, subject) record and deadline, the same sums
+// for dense and N x K tables (an untracked subject contributes BASELINE in every row).
+__global__ void k_digest(KP P, unsigned long long* out) {
   const uint64_t K = 0x9E3779B97F4A7C15ull;
+  const uint32_t N = P.N, nloc = P.nloc, row0 = P.row0, nc = ncells(P);
   unsigned long long a = 0, b = 0;
   const size_t total = (size_t)nloc * N;
   for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t v = view[x];  // x = local observer * N + subject
+    const uint32_t li = (uint32_t)(x / N), j = (uint32_t)(x % N);  // x = local observer * N + subject
+    const uint32_t v = cell_get(P, row0 + li, j);
     if (v) a += fmix64(((uint64_t)row0 * N + x) * K + v);
-    const uint32_t d = dl[x];  // x = subject * nloc + local observer
+  }
+  const size_t dtot = (size_t)nc * nloc;
+  for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < dtot; x += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t d = P.dl[x];  // x = cell * nloc + local observer
     if (d) {
-      const uint64_t subj = x / nloc, obs = row0 + x % nloc;
+      const uint64_t subj = subj_of(P, (uint32_t)(x / nloc)), obs = row0 + x % nloc;
       b += fmix64((obs * N + subj) * K + d);
     }
   }

@@ -51,7 +51,7 @@ class SwimConfig(ctypes.Structure):
         ("gossip_capacity", ctypes.c_uint32),
         ("event_capacity", ctypes.c_uint32),
         ("sync_capacity", ctypes.c_uint32),
-        ("dirty_capacity", ctypes.c_uint32),
+        ("tracked_subjects", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
         ("device", ctypes.c_int32),
         ("shard_rank", ctypes.c_uint32),

@@ -74,7 +74,7 @@ class MembershipRecord:
 
 class SwimCluster:
     def __init__(self, config: ClusterConfig, n_members: int, seed: int = 0, *, event_capacity: int = 0,
-                 gossip_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0,
+                 gossip_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
                  _lib=None, _prefix: str = "swim_", _shard=(0, 1)):
         self._lib = _lib if _lib is not None else nat.load_swimhip()
         self._p = _prefix
@@ -83,7 +83,7 @@ class SwimCluster:
         self.seed = int(seed)
         self._cfg = to_swim_config(config, self.n, seed, gossip_capacity=gossip_capacity,
                                    event_capacity=event_capacity, sync_capacity=sync_capacity,
-                                   dirty_capacity=dirty_capacity, device=device, shard_rank=_shard[0],
+                                   tracked_subjects=tracked_subjects, device=device, shard_rank=_shard[0],
                                    shard_world=_shard[1])
         h = ctypes.c_void_p()
         self._h = None

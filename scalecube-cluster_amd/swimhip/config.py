@@ -232,7 +232,7 @@ class ClusterConfig(_Cfg):
 
 
 def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_capacity: int = 0,
-                   event_capacity: int = 0, sync_capacity: int = 0, dirty_capacity: int = 0, device: int = 0,
+                   event_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
                    shard_rank: int = 0, shard_world: int = 1):
     """Marshal a ClusterConfig into the C struct of include/swimhip.h."""
     from ._native import SwimConfig
@@ -243,7 +243,7 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
         raise ValueError("simulated seedMembers must be the ids 0..k-1")
     c = SwimConfig()
     c.n_members = n_members
-    c.mode = 0
+    c.mode = 1 if tracked_subjects else 0  # N x K tracked-subject views
     c.seed = seed & 0xFFFFFFFFFFFFFFFF
     c.ping_interval_ms = fd.pingInterval()
     c.ping_timeout_ms = fd.pingTimeout()
@@ -259,7 +259,7 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
     c.gossip_capacity = gossip_capacity
     c.event_capacity = event_capacity
     c.sync_capacity = sync_capacity
-    c.dirty_capacity = dirty_capacity
+    c.tracked_subjects = tracked_subjects
     c.flags = 0
     c.device = device
     c.shard_rank = shard_rank

@@ -18,6 +18,64 @@ def test_scenario_parity(name):
     scenarios.run_pair(name, SwimCluster, OracleCluster)
 
 
+# N x K tracked-subject mode vs the dense oracle: K columns cover every subject whose record ever
+# leaves the converged baseline in the scenario (crashes, false suspicions under loss, leaves)
+NXK = {
+    "c1_local32_crash": 4,
+    "local32_leave2": 4,
+    "lan256_loss5_crash3": 256,
+    "local128_partition_heal": 128,
+    "local48_links": 48,
+    "local24_inbound_blocks": 24,
+}
+
+
+@pytest.mark.parametrize("name", sorted(NXK))
+def test_nxk_scenario_parity(name):
+    k = NXK[name]
+
+    def make_nxk(cfg, n, seed, **kw):
+        return SwimCluster(cfg, n, seed, tracked_subjects=k, **kw)
+
+    scenarios.run_pair(name, make_nxk, OracleCluster)
+
+
+def test_nxk_c2_shape_4096_parity():
+    """C2's shape (4,096, 5 % loss, 1 % crash) with 1,024 tracked columns for 12 periods."""
+    cfg = ClusterConfig.defaultLanConfig()
+    n = 4096
+    a = SwimCluster(cfg, n, seed=7, tracked_subjects=1024, event_capacity=1 << 22)
+    b = OracleCluster(cfg, n, seed=7, event_capacity=1 << 22)
+    crashed = scenarios.crash_ids(n, 41, 7)
+    for c in (a, b):
+        c.set_loss(5.0)
+        c.step(2)
+        c.crash(crashed)
+    for _ in range(3):
+        for c in (a, b):
+            c.step(4)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+        assert [e.key() for e in a.events()] == [e.key() for e in b.events()]
+    for i in range(0, n, 97):
+        assert np.array_equal(a.view(i), b.view(i)) and np.array_equal(a.deadlines(i), b.deadlines(i))
+    pa, pb = a.presence(), b.presence()
+    assert np.array_equal(pa[0], pb[0]) and np.array_equal(pa[1], pb[1])
+
+
+def test_nxk_column_overflow_is_loud():
+    """More subjects leaving the baseline than columns -> SWIM_EOVERFLOW, never a silent merge."""
+    from swimhip import SwimError
+
+    c = SwimCluster(ClusterConfig.defaultLocalConfig(), 64, seed=3, tracked_subjects=2)
+    c.step(2)
+    c.crash([1, 2, 3, 4, 5])
+    with pytest.raises(SwimError) as ei:
+        c.step(10)
+    assert ei.value.code == -75
+
+
 def test_philox_device_matches_oracle():
     from swimhip import native
 
