@@ -49,7 +49,13 @@ WORKLOADS = {
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
                     "crashes (concurrent churn), suspicion-timeout sweep",
-               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 16, tracked=256),
+               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 17, tracked=256),
+    # The SYNC re-spread storm of 256 simultaneous crashes at 2^20 members (~1.2e6 live gossips, each
+    # held by every member: DESIGN.md §6) exceeds any per-member holdings that fit one GPU, so the
+    # full-size N x K geometry is also measured with the churn it can hold exactly:
+    "c5g": dict(desc="C5 geometry at 1,048,576 members: N x K tracked-subject views (K = 256), LAN defaults, 8 "
+                     "simultaneous crashes, suspicion-timeout sweep",
+                n=1 << 20, preset="lan", loss=0.0, crash_n=8, part=0, gcap=1 << 17, tracked=256),
     "c5s": dict(desc="C5 geometry at 262,144 members: N x K tracked-subject views (K = 256), LAN defaults, 256 "
                      "simultaneous crashes",
                 n=1 << 18, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
@@ -310,24 +316,39 @@ def main():
     # the kernels are timed here too, for the suspicion sweep (no timeout fires in the timed region)
     periods_to_dead = None
     conv = None
+    sweep_rl = None
     if crashed and args.converge:
         sc0 = c.stats()
         c.kernel_timing(True)
         extra = 0
-        while extra < args.converge:
-            st = c.stats()
-            if st["not_converged"] == 0:
-                break
-            c.step(5)
-            extra += 5
-            log(f"converge: +{extra} periods, not_converged={st['not_converged']}")
+        # the suspicion sweep only has work in the periods whose deadlines fall due: its roofline is
+        # taken over those launches (one period at a time, kernel-time and sweep_cells deltas)
+        fire_ms, fire_n, fire_cells = 0.0, 0, 0
+        st = c.stats()
+        while extra < args.converge and st["not_converged"]:
+            k0 = c.kernel_times().get("k_susp_sweep", (0.0, 0))
+            c.step(1)
+            extra += 1
+            st1 = c.stats()
+            k1 = c.kernel_times().get("k_susp_sweep", (0.0, 0))
+            if st1["sweep_cells"] > st["sweep_cells"]:
+                fire_ms += k1[0] - k0[0]
+                fire_n += k1[1] - k0[1]
+                fire_cells += st1["sweep_cells"] - st["sweep_cells"]
+            st = st1
+            if extra % 5 == 0:
+                log(f"converge: +{extra} periods, not_converged={st['not_converged']}")
         pres, last = c.presence()
         if c.stats()["not_converged"] == 0:
             periods_to_dead = int(max(last[crashed])) - 1 - crash_period
         kt2 = c.kernel_times()
         dc = {k: v - sc0[k] for k, v in c.stats().items()}
-        conv = {k: round(v["frac"], 4) for k in ("k_susp_sweep", "k_sync_merge", "k_sync_ack")
+        conv = {k: round(v["frac"], 4) for k in ("k_sync_merge", "k_sync_ack")
                 for v in [roofline_of(k, kt2, dc, world)] if v}
+        if fire_n:
+            sweep_rl = roofline_of("k_susp_sweep", {"k_susp_sweep": (fire_ms, fire_n)},
+                                   {"sweep_cells": fire_cells}, world)
+            conv["k_susp_sweep"] = round(sweep_rl["frac"], 4)
         c.kernel_timing(False)
 
     value = n * args.steps / elapsed  # the one cluster's member-periods (all shards together)
@@ -356,6 +377,10 @@ def main():
         "kernels_ms": {k: round(v[0], 3) for k, v in ktimes.items()},
         "kernels_frac": fracs,
         "converge_kernels_frac": conv,
+        "sweep_roofline": None if sweep_rl is None else {
+            "achieved": sweep_rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sweep_rl["frac"],
+            "bytes_per_launch": sweep_rl["bytes_per_launch"], "avg_launch_ms": sweep_rl["avg_launch_ms"],
+            "launches": sweep_rl["launches"], "window": "the periods whose suspicion deadlines fell due"},
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",

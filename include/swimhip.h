@@ -197,10 +197,12 @@ int swim_sync(swim_handle* h);
  * cross-shard exchange and describes it in a swim_xchg; the host performs the collective
  * over its communicator (RCCL all-gather / all-to-all-v / all-reduce) on the two device
  * buffers it attached, fills recv_counts, and calls swim_shard_step again. The exchanges of
- * one period: gossip-id commits (all-gather of the gossips created in a phase), the
- * per-round gossip-liveness maximum (all-reduce MAX), the per-round sender windows bound for
- * receivers on other shards (all-to-all-v), and the SYNC / SYNC_ACK membership-table rows of
- * cross-shard pairs (all-to-all-v). Results are identical to the unsharded handle's. */
+ * one period: gossip-id commits (all-gather of the gossips created in a phase; each rank's block
+ * also carries its per-word gossip liveness and bit-length bounds, merged by element-wise max),
+ * the per-round sender windows bound for receivers on other shards (all-to-all-v), and the
+ * SYNC / SYNC_ACK membership-table rows of cross-shard pairs (all-to-all-v). Results are
+ * identical to the unsharded handle's. The library currently emits SWIM_X_ALLGATHER and
+ * SWIM_X_ALLTOALLV only; SWIM_X_ALLREDUCE_MAX stays reserved (an element-wise *unsigned* max). */
 #define SWIM_MAX_WORLD 64
 #define SWIM_X_DONE 0          /* the period is complete                                   */
 #define SWIM_X_ALLGATHER 1     /* every rank contributes send_words (host pads to the max)  */

@@ -254,18 +254,19 @@ int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
 // shard's stage first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
   hipStream_t s = h->stream;
-  // {overflow, stg_count} in one copy: a single-GPU run stops at the first phase whose buffers
-  // overflowed (a wrapped gossip ring would otherwise feed the next phase's kernels)
+  // {overflow, stg_count} in one copy: a run stops at the first phase whose buffers overflowed (a
+  // wrapped gossip ring would otherwise feed the next phase's kernels). Sharded hosts share the
+  // error with every rank before the next collective (swimhip/sharded.py, status all-gather).
   static_assert(offsetof(Ctl, stg_count) == offsetof(Ctl, overflow) + 4, "Ctl layout");
   uint32_t ovn[2] = {0u, 0u};
   HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 8, hipMemcpyDeviceToHost, s));
   HIPC_RC(h, rc, hipStreamSynchronize(s));
+  if (ovn[0]) {
+    *rc = check_overflow(h);
+    return false;
+  }
   uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
   if (h->world == 1) {
-    if (ovn[0]) {
-      *rc = check_overflow(h);
-      return false;
-    }
     if (n) hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(n, 256)), dim3(256), 0, s, P.stg, n, 0u, h->ck[0], h->cv[0]);
     *rc = commit_sorted(h, P, n);
     return false;
@@ -440,7 +441,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         set_phase(h, P, G + 1);
         memset_ctl_u32(h, offsetof(Ctl, due_count));
         timed(h, 7, "k_due", [&] { hipLaunchKernelGGL(k_due, dim3(blocks_for(N, 256)), dim3(256), 0, s, P); });
-        timed(h, 3, "k_susp_sweep", [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 3, "k_susp_sweep", [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(2048), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         // phase G+2: SYNC requests
         set_phase(h, P, G + 2);
@@ -532,15 +533,17 @@ int step_one(swim_handle* h) {
 }
 
 int check_overflow(swim_handle* h) {
-  uint32_t ov = 0;
+  uint32_t ov = 0, why = 0;
   HIPC(h, hipMemcpyAsync(&ov, &h->base.ctl->overflow, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(&why, &h->base.ctl->ov_detail, 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   if (ov) {
-    char buf[160];
+    char buf[320];
     std::snprintf(buf, sizeof buf,
                   "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 apply spill list, "
-                  "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping)",
-                  ov);
+                  "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping, 128 N x K columns); infectedFrom "
+                  "detail 0x%x (1 misprediction, 2 records per pair, 4 pruned pairs, 8 delivery records, 16 in-history)",
+                  ov, why);
     return fail(h, SWIM_EOVERFLOW, buf);
   }
   return SWIM_OK;
@@ -561,7 +564,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
       c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
     return SWIM_EINVAL;
   const uint32_t world = c.shard_world ? c.shard_world : 1u;
-  if (world >= SWIM_MAX_WORLD || c.shard_rank >= world || c.n_members % world) return SWIM_EINVAL;
+  if (world > SWIM_MAX_WORLD || c.shard_rank >= world || c.n_members % world) return SWIM_EINVAL;
   // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
   if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
     return SWIM_EINVAL;

@@ -70,6 +70,15 @@ enum Overflow : uint32_t {
   OV_TRACK = 128u,  // N x K: more subjects left the baseline than there are columns
 };
 
+// OV_IFROM causes (Ctl::ov_detail), named in the error message
+enum IfromOverflow : uint32_t {
+  IF_MISPREDICT = 1u,  // a selected peer delivered within the horizon without a record (may_select)
+  IF_MAXREC = 2u,      // one pair needs more than MAXREC records
+  IF_PAIRS = 4u,       // pruned pairs of a round over spcap / pwcap
+  IF_RECORDS = 8u,     // delivery records or their bodies over rcap / bcap within the horizon
+  IF_INHIST = 16u,     // a member's in-history ring (IHCAP) wrapped inside the horizon
+};
+
 constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
@@ -100,7 +109,7 @@ struct Ctl {
   uint32_t rec_cnt, body_cnt, sp_cnt, rp_cnt, pw_used;
   uint32_t ncols;        // N x K: columns allocated
   uint32_t alive_count;  // alive members (N x K: presence of untracked subjects)
-  uint32_t pad2;
+  uint32_t ov_detail;    // which infectedFrom bound OV_IFROM hit (IfromOverflow bits)
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -261,9 +270,15 @@ constexpr uint32_t XREC = 0x80000000u;     // in_list entry: a received window r
 constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
 constexpr uint32_t NSUM = 1024;  // receipt-summary words per receiver: active lists up to 32,768 words
 constexpr uint32_t SPAIR = 0x40000000u;  // in_list entry: a pruned pair (window in pw), not a member id
-constexpr uint32_t IHCAP = 256;  // in-history entries per member (~f per round over the horizon)
+constexpr uint32_t IHCAP = 512;  // in-history entries per member (~f per round over the horizon: ~2 f hzn,
+                                 // with the in-degree tail of 10^6 members)
 constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
 constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
+
+__device__ __forceinline__ void ifrom_overflow(const KP& P, uint32_t why) {
+  atomicOr(&P.ctl->overflow, OV_IFROM);
+  atomicOr(&P.ctl->ov_detail, why);
+}
 
 __device__ __forceinline__ uint32_t ncells(const KP& P) { return P.nxk ? P.ctl->ncols : P.N; }
 

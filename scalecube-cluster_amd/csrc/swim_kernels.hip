@@ -856,13 +856,13 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           for (uint32_t q = 0; q < np; ++q)
             if (s_peers[w][q] == e.x) {
               if (e.z == NONE) {  // a delivery predicted never to be sent back: cannot stay exact
-                atomicOr(&P.ctl->overflow, OV_IFROM);
+                ifrom_overflow(P, IF_MISPREDICT);
               } else {
                 const uint32_t c = atomicAdd(&s_nrec[w][q], 1u);
                 if (c < MAXREC)
                   s_rec[w][q][c] = e.z;
                 else
-                  atomicOr(&P.ctl->overflow, OV_IFROM);
+                  ifrom_overflow(P, IF_MAXREC);
               }
             }
       }
@@ -880,7 +880,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         for (uint32_t c = 0; c < nr; ++c) P.sp_recs[(size_t)sp * MAXREC + c] = s_rec[w][lane][c];
         entry = SPAIR | sp;
       } else {
-        atomicOr(&P.ctl->overflow, OV_IFROM);
+        ifrom_overflow(P, IF_PAIRS);
       }
     }
   }
@@ -1083,7 +1083,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
       // the records still inside the horizon start at rs_rec / rs_body of round r - hzn
       if (rec + 1u - P.ctl->rs_rec[(r - P.hzn) & 255u] > P.rcap ||
           body + n_act - P.ctl->rs_body[(r - P.hzn) & 255u] > P.bcap || o >= P.spcap) {
-        atomicOr(&P.ctl->overflow, OV_IFROM);
+        ifrom_overflow(P, IF_RECORDS);
       } else {
         P.rec_hdr[rec & (P.rcap - 1u)] = make_uint4(sid, p, r, body);
         P.rec_len[rec & (P.rcap - 1u)] = n_act;
@@ -1094,7 +1094,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
     if (ok_l) {
       const uint32_t pos = ihh + (uint32_t)__popcll(reach & ((1ull << lane) - 1ull));
       uint4* slot = ring + (pos & (IHCAP - 1u));
-      if (pos >= IHCAP && (*slot).y + P.hzn >= r) atomicOr(&P.ctl->overflow, OV_IFROM);
+      if (pos >= IHCAP && (*slot).y + P.hzn >= r) ifrom_overflow(P, IF_INHIST);
       *slot = make_uint4(sid, r, rec, 0u);
     }
     ihh += (uint32_t)__popcll(reach);
@@ -1324,6 +1324,11 @@ constexpr uint32_t SPILL_CAP = 1024;       // spilled subjects per receiver and 
 constexpr uint32_t PRES_WORDS = 2048;     // subject-presence bitmap for N <= 65,536
 constexpr uint32_t APPLY_THREADS = SWIM_APPLY_THREADS;
 constexpr uint32_t APPLY_BLOCKS = SWIM_APPLY_BLOCKS;  // persistent: one 16-wave workgroup per CU (LDS-bound)
+// build-time tunables (-DSWIM_APPLY_HLOG / _THREADS): the table init starts at 64 slots, the
+// block scan keeps one partial per wave (16 at most), and the kernel's LDS must fit gfx950's 160 KiB
+static_assert(HCAP_LOG >= 6 && HCAP_LOG <= 14, "SWIM_APPLY_HLOG out of range");
+static_assert(APPLY_THREADS % 64 == 0 && APPLY_THREADS <= 1024, "SWIM_APPLY_THREADS must be a multiple of 64, <= 1024");
+static_assert(4 * (2 * HCAP + SPILL_CAP + PRES_WORDS + 17) <= 160 * 1024, "k_gossip_apply LDS over 160 KiB");
 
 // Membership apply of a round's first receipts: onGossipReq's new-gossip branch
 // (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
@@ -1778,37 +1783,61 @@ __global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
   if (j < ncells(P) && P.colmin[j] <= P.period) {
     const uint32_t idx = atomicAdd(&P.ctl->due_count, 1u);
     P.due[idx] = j;
+    P.colmin[j] = NONE;  // rebuilt by the sweep from the deadlines it leaves standing
   }
 }
 
+// onSuspicionTimeout (MembershipProtocolImpl.java:637-647) for one deadline cell of column j
+__device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t li, uint32_t v, uint32_t* mn,
+                                               uint32_t* fired, Tally& T) {
+  if (v == 0u) return 0u;
+  const uint32_t i = P.row0 + li;
+  if (!P.alive[i]) return 0u;  // a stopped member's timers never fire: dropped
+  const uint32_t dl = v - 1u;
+  if (dl > P.period) {
+    *mn = dl < *mn ? dl : *mn;
+    return v;
+  }
+  if (P.view[(size_t)li * P.W + j] != 0u) {
+    ++*fired;
+    apply_record(P, i, subj_of(P, j), SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
+  }
+  return 0u;
+}
+
+// Due deadline columns, streamed in SWEEP_CHUNK-cell pieces (a few due columns still fill the
+// chip), 16 B per thread; each piece folds the deadlines it leaves standing into colmin.
+constexpr uint32_t SWEEP_CHUNK = 4096;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   __shared__ uint32_t s_min[4];
   Tally T;
-  uint32_t fired = 0;
+  uint32_t fired = 0, cells = 0;
   const uint32_t n = P.ctl->due_count;
-  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const uint32_t j = P.due[k];  // the cell; its subject is subj_of(j)
+  const uint32_t nch = (P.nloc + SWEEP_CHUNK - 1u) / SWEEP_CHUNK;
+  const bool vec = (P.nloc & 3u) == 0u;  // columns 16-B aligned
+  for (uint32_t u = blockIdx.x; u < n * nch; u += gridDim.x) {
+    const uint32_t j = P.due[u / nch];  // the cell; its subject is subj_of(j)
+    const uint32_t c0 = (u % nch) * SWEEP_CHUNK, c1 = min(P.nloc, c0 + SWEEP_CHUNK);
     uint32_t* col = P.dl + (size_t)j * P.nloc;
     uint32_t mn = NONE;
-    for (uint32_t li = threadIdx.x; li < P.nloc; li += blockDim.x) {
-      const uint32_t i = P.row0 + li;
-      const uint32_t v = col[li];
-      if (v == 0u) continue;
-      if (!P.alive[i]) {
-        col[li] = 0u;
-        continue;
+    if (vec) {
+      for (uint32_t li = c0 + 4u * threadIdx.x; li < c1; li += 4u * blockDim.x) {
+        uint4 v = *reinterpret_cast<const uint4*>(col + li);
+        if ((v.x | v.y | v.z | v.w) == 0u) continue;
+        const uint4 w = make_uint4(sweep_cell(P, j, li, v.x, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 1u, v.y, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 2u, v.z, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 3u, v.w, &mn, &fired, T));
+        if (w.x != v.x || w.y != v.y || w.z != v.z || w.w != v.w) *reinterpret_cast<uint4*>(col + li) = w;
       }
-      const uint32_t dl = v - 1u;
-      if (dl <= P.period) {  // onSuspicionTimeout (MembershipProtocolImpl.java:637-647)
-        col[li] = 0u;
-        if (P.view[(size_t)li * P.W + j] != 0u) {
-          ++fired;
-          apply_record(P, i, subj_of(P, j), SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
-        }
-      } else if (dl < mn) {
-        mn = dl;
+    } else {
+      for (uint32_t li = c0 + threadIdx.x; li < c1; li += blockDim.x) {
+        const uint32_t v = col[li];
+        const uint32_t w = sweep_cell(P, j, li, v, &mn, &fired, T);
+        if (w != v) col[li] = w;
       }
     }
+    cells += c1 - c0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const uint32_t y = __shfl_xor(mn, o, 64);
@@ -1819,12 +1848,12 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     if (threadIdx.x == 0) {
       uint32_t b = s_min[0];
       for (uint32_t q = 1; q < blockDim.x / 64u; ++q) b = s_min[q] < b ? s_min[q] : b;
-      P.colmin[j] = b;
+      if (b != NONE) atomicMin(&P.colmin[j], b);
     }
     __syncthreads();
   }
   add_stat(P, ST_SUSP_TIMEOUTS, fired);
-  add_stat(P, ST_SWEEP_CELLS, threadIdx.x == 0 ? ((n + gridDim.x - 1u - blockIdx.x) / gridDim.x) * P.nloc : 0u);
+  add_stat(P, ST_SWEEP_CELLS, threadIdx.x == 0 ? cells : 0u);
   flush_tally(P, T);
 }
 

@@ -3,9 +3,10 @@
 Rank r of a torch.distributed group owns observers [r*N/W, (r+1)*N/W): their membership tables,
 suspicion deadlines, gossip holdings and protocol cursors. Each rank drives its
 libswimhip.so handle with swim_shard_step and performs the exchanges the library describes on
-the group: all-gather of each phase's new gossips (ids stay identical on every shard), all-reduce
-MAX of per-word gossip liveness, all-to-all-v of sender windows bound for remote receivers and
-of SYNC / SYNC_ACK tables of cross-shard pairs. On ROCm the "nccl" backend is RCCL over xGMI and
+the group: all-gather of each phase's new gossips (ids stay identical on every shard; each block
+also carries the rank's per-word gossip liveness), all-to-all-v of sender windows bound for remote
+receivers and of SYNC / SYNC_ACK tables of cross-shard pairs. Every collective, and every period
+end, is preceded by a small status all-gather, so an error on one rank is raised on all. On ROCm the "nccl" backend is RCCL over xGMI and
 the buffers stay in HBM; with "gloo" (tests on one GPU, or CPU rehearsal of the protocol) they are
 staged through host memory. Results equal the unsharded SwimCluster's bit for bit.
 
@@ -19,7 +20,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .cluster import MembershipEvent, SwimCluster
+from .cluster import MembershipEvent, SwimCluster, SwimError
 
 
 class ShardedSwimCluster(SwimCluster):
@@ -54,19 +55,12 @@ class ShardedSwimCluster(SwimCluster):
         self._dist.all_gather(out, t, group=self._group)
         return [o.cpu().tolist() for o in out]
 
-    def _exchange(self):
+    def _exchange(self, status):
+        """The collective the library described; `status` = every rank's [code, op, counts...]
+        (one row per rank, from the status all-gather that precedes it)."""
         torch, dist, x, W = self._torch, self._dist, self._x, self.world
-        if x.op == nat.X_ALLREDUCE_MAX:
-            n = int(x.send_words)
-            buf = self._send[:n]
-            if self._gloo:
-                h = buf.cpu()
-                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self._group)
-                buf.copy_(h)
-            else:
-                dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=self._group)
-        elif x.op == nat.X_ALLGATHER:
-            counts = [c[0] for c in self._all_gather_ints([int(x.send_words)])]
+        if x.op == nat.X_ALLGATHER:
+            counts = [row[2] for row in status]
             m = max(counts)
             if m:
                 src = self._send[:m]
@@ -81,8 +75,8 @@ class ShardedSwimCluster(SwimCluster):
                 x.recv_counts[q] = counts[q]
             x.recv_stride = m
         elif x.op == nat.X_ALLTOALLV:
-            sc = [int(x.send_counts[q]) for q in range(W)]
-            allc = self._all_gather_ints(sc)  # allc[q][r] = words rank q sends to rank r
+            allc = [row[2:] for row in status]  # allc[q][r] = words rank q sends to rank r
+            sc = allc[self.rank]
             rc = [allc[q][self.rank] for q in range(W)]
             si, ri = sum(sc), sum(rc)
             if max(max(row) for row in allc):
@@ -101,13 +95,42 @@ class ShardedSwimCluster(SwimCluster):
         if self._send.is_cuda:  # the library resumes on its own stream
             torch.cuda.synchronize(self._send.device)
 
+    def _status(self, err):
+        """Status all-gather before every collective and at the end of every period: a failure on
+        one rank (an overflow only it detected, a bad size) becomes the same SwimError on every
+        rank instead of leaving the others blocked in the next collective."""
+        x, W = self._x, self.world
+        if err is not None:
+            row = [int(err.code), -1] + [0] * W
+        elif x.op == nat.X_ALLGATHER:
+            row = [0, int(x.op), int(x.send_words)] + [0] * (W - 1)
+        elif x.op == nat.X_ALLTOALLV:
+            row = [0, int(x.op)] + [int(x.send_counts[q]) for q in range(W)]
+        else:
+            row = [0, int(x.op)] + [0] * W
+        status = self._all_gather_ints(row)
+        bad = [(q, r[0]) for q, r in enumerate(status) if r[0]]
+        if err is not None:
+            raise err
+        if bad:
+            q, code = bad[0]
+            raise SwimError(code, f"shard_step failed on rank {q} (status {code})")
+        if len({r[1] for r in status}) != 1:
+            raise SwimError(-22, f"shards out of step: exchange ops {[r[1] for r in status]}")
+        return status
+
     def step(self, periods: int = 1):
         for _ in range(int(periods)):
             while True:
-                self._call("shard_step", self._h, ctypes.byref(self._x))
+                err = None
+                try:
+                    self._call("shard_step", self._h, ctypes.byref(self._x))
+                except SwimError as e:
+                    err = e
+                status = self._status(err)
                 if self._x.op == nat.X_DONE:
                     break
-                self._exchange()
+                self._exchange(status)
 
     def step_async(self, periods: int = 1):
         self.step(periods)

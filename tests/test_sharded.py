@@ -10,6 +10,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from swimhip import _native as nat
+from swimhip.cluster import SwimError
 from swimhip.sharded import ShardedSwimCluster
 
 
@@ -39,7 +40,7 @@ def _exchange_worker(rank, world, port):
         n = 2 + 3 * rank
         c._send[:n] = torch.arange(n, dtype=torch.int32) + 100 * rank
         x.op, x.send_words = nat.X_ALLGATHER, n
-        c._exchange()
+        c._exchange(c._status(None))
         m = int(x.recv_stride)
         assert m == 2 + 3 * (world - 1)
         for q in range(world):
@@ -53,7 +54,7 @@ def _exchange_worker(rank, world, port):
             x.send_counts[q] = q + 1
             c._send[off:off + q + 1] = 10 * rank + q
             off += q + 1
-        c._exchange()
+        c._exchange(c._status(None))
         got, off = [], 0
         for q in range(world):
             cnt = int(x.recv_counts[q])
@@ -61,11 +62,17 @@ def _exchange_worker(rank, world, port):
             got.append(c._recv[off:off + cnt].tolist())
             off += cnt
         assert got == [[10 * q + rank] * (rank + 1) for q in range(world)]
-        # element-wise max
-        c._send[:4] = torch.tensor([rank, 5 - rank, 7, rank * 3], dtype=torch.int32)
-        x.op, x.send_words = nat.X_ALLREDUCE_MAX, 4
-        c._exchange()
-        assert c._send[:4].tolist() == [world - 1, 5, 7, 3 * (world - 1)]
+        # a failure on one rank is raised on every rank at the next status all-gather
+        x.op = nat.X_DONE
+        err = SwimError(-75, "shard_step: simulator buffer overflow") if rank == world - 1 else None
+        with pytest.raises(SwimError) as ei:
+            c._status(err)
+        assert ei.value.code == -75
+        # ranks out of step (different exchange ops) are an error too, never a mismatched collective
+        x.op = nat.X_ALLGATHER if rank == 0 else nat.X_DONE
+        x.send_words = 0
+        with pytest.raises(SwimError):
+            c._status(None)
     finally:
         dist.destroy_process_group()
 
@@ -96,3 +103,25 @@ def test_shards_match_unsharded(world, names):
     """`world` ranks sharing cuda:0, gloo exchanges: views, deadlines, events, counters, digests
     and presence equal the unsharded handle's after every period."""
     mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
+
+
+def _overflow_worker(rank, world, port):
+    from swimhip import ClusterConfig
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        # rank 0 alone gets a 1-row SYNC staging area: only it detects the overflow
+        c = ShardedSwimCluster(ClusterConfig.defaultLanConfig(), 256, seed=5, sync_capacity=1 if rank == 0 else 0)
+        with pytest.raises(SwimError) as ei:
+            c.step(40)
+        assert ei.value.code == -75
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_overflow_on_one_rank_fails_every_rank():
+    """An overflow only one shard detects raises SWIM_EOVERFLOW on both ranks (no hang)."""
+    mp.spawn(_overflow_worker, args=(2, _free_port()), nprocs=2, join=True)
