@@ -106,7 +106,9 @@ typedef struct swim_config {
                                any observer's record of it leaves the converged baseline (ALIVE,
                                incarnation 0); untracked subjects read as that baseline in every
                                view. More than K such subjects -> SWIM_EOVERFLOW */
-  uint32_t flags;           /* reserved, 0                                                */
+  uint32_t n_initial;       /* members started (converged) at create: ids [0, n_initial); 0 = all
+                               N. Ids [n_initial, N) are spare slots, absent from every view, for
+                               swim_join / swim_restart (dense, unsharded handles only)          */
   int32_t device;           /* HIP device ordinal the handle lives on                     */
   uint32_t shard_rank;      /* observer-row shard of this handle (0 .. shard_world-1)     */
   uint32_t shard_world;     /* shards of the cluster (0 or 1 = unsharded); see swim_shard_step */
@@ -151,6 +153,7 @@ typedef struct swim_stats {
   uint64_t apply_words;       /* receipt words folded into holdings / infection rounds        */
   uint64_t apply_runs;        /* subject-run representatives read from the ring               */
   uint64_t apply_subjects;    /* updateMembership calls (one per subject per receiver)        */
+  uint64_t fd_dead_events;    /* FailureDetectorEvent(DEAD): an ACK with DEST_GONE (FDI:231-235,383) */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -181,6 +184,22 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
  * keeps running until its own sweep drops that gossip (spread() completes at sweep,
  * GossipProtocolImpl.java:299-302), then stops at the end of that gossip round. Unsharded handles. */
 int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n);
+
+/* Join = a new member's ClusterImpl.start() (ClusterImpl.java:170-227): spare slot `ids[k]` (never
+ * started) starts before the next period at an address of its own with a table holding only itself
+ * (MembershipProtocolImpl.java:130-139), and in that period's SYNC phase makes the initial SYNC to
+ * every seed address (start0, :222-257); the first SYNC_ACK that comes back (lowest seed address
+ * whose round trip is delivered) is merged with reason INITIAL_SYNC (not re-spread, :649-656).
+ * Periodic doSync follows the usual stagger from the next period on. Dense, unsharded handles. */
+int swim_join(swim_handle* h, const uint32_t* ids, uint32_t n);
+/* Restart on the same address (MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses,
+ * :453-520): stopped member old_ids[k]'s address is taken by spare slot new_ids[k], a NEW member id
+ * joining as in swim_join. Messages sent to the old id reach the new member: a PING answers
+ * DEST_GONE, so the prober's FD emits DEAD for the old id (FailureDetectorImpl.java:231-235,383);
+ * a metadata request for the old id fails (MetadataStoreImpl.java:216-223); gossip and SYNC are
+ * handled by the new member, which ignores records of other ids at its own address
+ * (MembershipProtocolImpl.java:499-505). Dense, unsharded handles. */
+int swim_restart(swim_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n);
 
 /* Advance `periods` protocol periods (FD, G gossip rounds, suspicion
  * timeouts, SYNC/SYNC_ACK). Asynchronous to the host only inside the call. */

@@ -219,8 +219,14 @@ struct Member {
 };
 
 struct SyncReq {
-  uint32_t from, to, kind;  // kind 0 = periodic doSync (MPI:304-320), 1 = FD-triggered (MPI:389-397)
+  // kind 0 = periodic doSync (MPI:304-320), 1 = FD-triggered (MPI:389-397), 2 = a joining member's
+  // initial SYNC to a seed (start0, MPI:222-257). `to` = the member addressed (for a seed: the member
+  // id that owns the seed address), the process at its address receives it.
+  uint32_t from, to, kind;
 };
+
+// the metadata-fetch attempt id of a SYNC / SYNC_ACK merge (distinct per request)
+inline uint32_t sync_attempt(uint32_t peer, uint32_t kind) { return kind == 2 ? 0x80000000u | peer : (peer << 1) | kind; }
 
 }  // namespace
 
@@ -237,6 +243,12 @@ struct oracle_handle {
   std::vector<uint8_t> link;    // outbound block src->dst (send error), lazily allocated
   std::vector<uint8_t> inlink;  // inbound block at dst of messages from src (silent drop)
   std::vector<Member> m;
+  // Addresses: member id x is reached at address addr[x]; occ[a] is the running
+  // member at address a (NONE when its transport is stopped). A restart on the same address gives
+  // the address to a new member id, so messages sent to the old id reach the new member.
+  std::vector<uint32_t> addr, occ;
+  std::vector<std::vector<uint32_t>> movers;  // per address: the members restarted on it
+  std::vector<uint8_t> started, joining;
   std::vector<Gossip> registry;  // by gid
   uint32_t gbase = 0;            // every gid below is held by nobody
   uint32_t rc = 256;             // slots of each member's GossipMap (power of two)
@@ -258,32 +270,44 @@ inline bool bit_set(const std::vector<uint8_t>& bm, uint64_t bit) {
   return !bm.empty() && (bm[bit >> 3] & (1u << (bit & 7)));
 }
 
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// The member whose transport receives what is sent to member x (TransportImpl sends to
+// member.address(), NET:44-70): the running member at x's address, or NONE.
+inline uint32_t route(const oracle_handle* h, uint32_t x) { return h->occ[h->addr[x]]; }
+
 // The sender side of NetworkEmulatorTransport.send/requestResponse (NET:44-70): tryFailOutbound
 // (NE:166-180) fails the send immediately — a NETWORK_BREAK error the sender sees — on a
 // loss draw (NE:348-351, nextInt(100) < lossPercent) or a blocked destination (loss 100 %,
 // NE:105-119; the partition cut is a blockOutbound on both sides). A stopped transport
 // (crash) neither sends nor accepts connections, which the sender also sees as an error.
+// src and dst are the member ids the message is addressed from / to; the processes at their
+// addresses send and receive it (route), partition groups and blocks are per address, and the loss
+// draw is keyed by the two processes.
 bool out_ok(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
-  if (!h->m[src].alive || !h->m[dst].alive) return false;
-  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[src] != h->group[dst]) return false;
-  if (bit_set(h->link, (uint64_t)src * h->N + dst)) return false;
+  const uint32_t rs = route(h, src), rd = route(h, dst);
+  if (rs == NONE || rd == NONE) return false;
+  const uint32_t as = h->addr[src], ad = h->addr[dst];
+  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[as] != h->group[ad]) return false;
+  if (bit_set(h->link, (uint64_t)as * h->N + ad)) return false;
   if (h->loss_bp == 0) return true;      // NE:349 lossPercent > 0
   if (h->loss_bp >= 10000) return false; // NE:350 lossPercent >= 100
   uint32_t thr = (uint32_t)(((uint64_t)h->loss_bp << 32) / 10000u);
-  return draw(h->seed, kind, src, dst, c, tick) >= thr;  // NE:350 nextInt(100) < loss => lost
+  return draw(h->seed, kind, rs, rd, c, tick) >= thr;  // NE:350 nextInt(100) < loss => lost
 }
 
 // The receiver side: NET:73-77 (listen) and NET:64-68 (responses) drop a message whose sender
 // the receiver blocks inbound (NE:255-269), silently — the sender saw a successful send.
 bool in_ok(const oracle_handle* h, uint32_t dst, uint32_t src) {
-  return !bit_set(h->inlink, (uint64_t)dst * h->N + src);
+  return !bit_set(h->inlink, (uint64_t)h->addr[dst] * h->N + h->addr[src]);
 }
 
 // Everything of delivered() but the loss draw: both transports up, no partition cut, no block.
 bool link_ok(const oracle_handle* h, uint32_t src, uint32_t dst) {
-  if (!h->m[src].alive || !h->m[dst].alive) return false;
-  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[src] != h->group[dst]) return false;
-  return !bit_set(h->link, (uint64_t)src * h->N + dst) && in_ok(h, dst, src);
+  if (route(h, src) == NONE || route(h, dst) == NONE) return false;
+  const uint32_t as = h->addr[src], ad = h->addr[dst];
+  if (h->period >= h->part_t0 && h->period < h->part_t1 && h->group[as] != h->group[ad]) return false;
+  return !bit_set(h->link, (uint64_t)as * h->N + ad) && in_ok(h, dst, src);
 }
 
 // Is message src->dst delivered to dst's protocol handlers?
@@ -383,6 +407,7 @@ void stop_member(oracle_handle* h, uint32_t c) {
   Member& me = h->m[c];
   if (!me.alive) return;
   me.alive = false;
+  if (h->occ[h->addr[c]] == c) h->occ[h->addr[c]] = NONE;
   me.timers.clear();  // its scheduler is gone
   while (!me.gossips.order.empty()) gossip_pop_oldest(h, me);
   me.recv.clear();
@@ -420,9 +445,11 @@ void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t
 
 // MetadataStoreImpl.fetchMetadata (core/metadata/MetadataStoreImpl.java:151-193) as a
 // liveness round trip: GET_METADATA_REQ obs->subj and GET_METADATA_RESP subj->obs delivered
-// and the subject serving (onMetadataRequest :209-249).
+// and the subject serving: the process at its address must be the subject itself (onMetadataRequest
+// answers only requests for its own id, :216-223; otherwise the fetch times out).
 bool fetch_ok(const oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t attempt, uint32_t tick) {
-  return delivered(h, K_MREQ, obs, subj, attempt, tick) && delivered(h, K_MRESP, subj, obs, attempt, tick);
+  return route(h, subj) == subj && delivered(h, K_MREQ, obs, subj, attempt, tick) &&
+         delivered(h, K_MRESP, subj, obs, attempt, tick);
 }
 
 // MembershipProtocolImpl.updateMembership (MPI:481-547) with its callees onSelfMemberDetected
@@ -436,6 +463,7 @@ void update_membership(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t r
   uint32_t& cell = me.table[subj];
   const uint32_t r0 = cell;
   if (!is_overrides(r1, r0)) return;  // MPI:489-496 (equal records never override)
+  if (subj != obs && h->addr[subj] == h->addr[obs]) return;  // MPI:499-505: another id at my address
   const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;  // MPI:652-653
   if (subj == obs) {  // MPI:499-501 -> onSelfMemberDetected MPI:549-569
     uint32_t inc1 = (r1 == SWIM_DEAD) ? inc_of(r0) : inc_of(r1);
@@ -530,8 +558,9 @@ void on_fd_event(oracle_handle* h, uint32_t i, uint32_t j, uint32_t status, uint
     me.sync_fd = j;
     return;
   }
-  update_membership(h, i, j, SWIM_PACK(inc_of(r0), status), SWIM_R_FAILURE_DETECTOR_EVENT, 0, 0, tick, me.others,
-                    (int64_t)h->period * h->G);  // MPI:399-402
+  // MPI:399-402 (status SUSPECT, or DEAD from a DEST_GONE ack: the packed DEAD cell)
+  update_membership(h, i, j, status == SWIM_DEAD ? SWIM_DEAD : SWIM_PACK(inc_of(r0), status),
+                    SWIM_R_FAILURE_DETECTOR_EVENT, 0, 0, tick, me.others, (int64_t)h->period * h->G);
 }
 
 // doPing (FDI:126-170) + doPingReq (FDI:172-209) + responder handlers onPing (FDI:226-252),
@@ -545,9 +574,12 @@ void do_ping(oracle_handle* h, uint32_t i) {
   const uint32_t j = select_ping_member(h, i);
   h->st.fd_probes++;
   std::vector<uint32_t> evs;
+  // onPing (FDI:226-252) at the process on j's address answers DEST_GONE unless it is j itself;
+  // computeMemberStatus (FDI:370-391) turns that ack into DEAD
+  const uint32_t acked = route(h, j) == j ? SWIM_ALIVE : SWIM_DEAD;
   if (delivered(h, K_PING, i, j, 0, tick) && delivered(h, K_ACK, j, i, 0, tick)) {  // FDI:143-150
     h->st.fd_direct_ok++;
-    evs.push_back(SWIM_ALIVE);
+    evs.push_back(acked);
   } else {
     const int32_t time_left = h->cfg.ping_interval_ms - h->cfg.ping_timeout_ms;  // FDI:160
     std::vector<uint32_t> proxies = select_ping_req_members(h, i, j);           // FDI:161
@@ -577,12 +609,14 @@ void do_ping(oracle_handle* h, uint32_t i) {
       // ack's sender (the proxy): blocked -> Mono.never() -> every subscription times out.
       const bool ok = first != 0xFFFFFFFFu && in_ok(h, i, first);
       for (uint32_t u = 0; u < unsent; ++u) evs.push_back(SWIM_SUSPECT);
-      for (uint32_t s = 0; s < sent; ++s) evs.push_back(ok ? SWIM_ALIVE : SWIM_SUSPECT);  // FDI:190-207
+      for (uint32_t s = 0; s < sent; ++s) evs.push_back(ok ? acked : SWIM_SUSPECT);  // FDI:190-207
     }
   }
   for (uint32_t ev : evs) {  // publishPingResult (FDI:365-368) -> MPI:376
     if (ev == SWIM_ALIVE)
       h->st.fd_alive_events++;
+    else if (ev == SWIM_DEAD)
+      h->st.fd_dead_events++;
     else
       h->st.fd_suspect_events++;
     on_fd_event(h, i, j, ev, tick);
@@ -679,7 +713,8 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     std::vector<uint32_t> peers = select_gossip_members(h, s);  // GPI:150
     if (me.gossips.w_lo == me.gossips.w_end) continue;
     for (uint32_t p : peers) {
-      Member& pm = h->m[p];
+      const uint32_t rp = route(h, p);  // the process that receives what s sends to p
+      Member& pm = h->m[rp == NONE ? p : rp];
       // !isInfected(member.id()) (GPI:248): the window gossips p delivered to s during their
       // current state
       std::fill(S.begin(), S.end(), 0ull);
@@ -707,7 +742,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       }
       // the link part of delivered(): both alive, no partition cut, no outbound / inbound block
       if (!nsend || !pm.alive || h->loss_bp >= 10000 || !link_ok(h, s, p)) continue;
-      Sent st{p, s, Batch{r, tick, 0, {}}};
+      Sent st{rp, s, Batch{r, tick, 0, {}}};
       uint32_t k0 = 0, k1 = nw;
       while (k0 < k1 && !(W[k0] & ~S[k0])) ++k0;
       while (k1 > k0 && !(W[k1 - 1] & ~S[k1 - 1])) --k1;
@@ -718,7 +753,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
         // first receipts: messages p lacks the gossip of, each with its own loss draw
         for (uint64_t cand = eff & ~held_word(h, pm, wlo + k); cand; cand &= cand - 1) {
           const uint32_t g = ((wlo + k) << 6) + (uint32_t)__builtin_ctzll(cand);
-          if (not_lost(s, p, g, tick)) deliveries.push_back({p, g});
+          if (not_lost(s, rp, g, tick)) deliveries.push_back({rp, g});
         }
       }
       sent.push_back(std::move(st));
@@ -801,14 +836,23 @@ void suspicion_phase(oracle_handle* h) {
 // SYNC anti-entropy: doSync (MPI:304-320), selectSyncAddress (MPI:416-427), onSync
 // (MPI:352-373), onSyncAck (MPI:343-349), syncMembership (MPI:463-473).
 // ---------------------------------------------------------------------------------------
-// selectSyncAddress: uniform over seeds U otherMembers (MPI:417-425), by rejection sampling.
+// selectSyncAddress: uniform over the set of addresses seeds U otherMembers' addresses (MPI:417-425),
+// by rejection sampling over address ids (address x = the one of member x; seed addresses are those
+// of members [0, n_seeds); the own address is never a seed, MPI:166-172).
 bool select_sync_address(oracle_handle* h, uint32_t i, uint32_t tick, uint32_t* out) {
   const Member& me = h->m[i];
-  uint64_t count = me.others;
-  for (uint32_t s = 0; s < h->cfg.n_seeds && s < h->N; ++s)
-    if (s != i && me.table[s] == SWIM_ABSENT) ++count;
-  if (count == 0) return false;  // MPI:421-422
-  auto valid = [&](uint32_t x) { return x != i && (me.table[x] != SWIM_ABSENT || x < h->cfg.n_seeds); };
+  const uint32_t own = h->addr[i];
+  const uint32_t nseeds = std::min<uint32_t>(h->cfg.n_seeds, h->N);
+  // MPI:421-422: nothing to pick when no other member is known and no seed address is not our own
+  if (me.others == 0 && (nseeds == 0 || (nseeds == 1 && own == 0))) return false;
+  auto valid = [&](uint32_t x) {
+    if (x == own || h->addr[x] != x) return false;  // own address / an id that moved to another address
+    if (x < nseeds) return true;
+    if (me.table[x] != SWIM_ABSENT) return true;
+    for (uint32_t y : h->movers[x])  // members restarted on address x
+      if (y != i && me.table[y] != SWIM_ABSENT) return true;
+    return false;
+  };
   uint32_t x = 0;
   for (uint32_t a = 0; a < 64; ++a) {
     x = (uint32_t)(((uint64_t)draw(h->seed, K_SYNC_PICK, i, a, 0, tick) * h->N) >> 32);
@@ -839,8 +883,12 @@ void sync_phase(oracle_handle* h) {
       continue;
     }
     uint32_t peer;
-    if ((uint32_t)(h->period % h->S) == i % h->S && select_sync_address(h, i, tick_s, &peer))
+    if (h->joining[i]) {  // start0 (MPI:222-257): SYNC to every seed address; no periodic doSync yet
+      for (uint32_t s = 0; s < h->cfg.n_seeds && s < h->N; ++s)
+        if (s != h->addr[i]) reqs.push_back({i, s, 2});
+    } else if ((uint32_t)(h->period % h->S) == i % h->S && select_sync_address(h, i, tick_s, &peer)) {
       reqs.push_back({i, peer, 0});
+    }
     if (me.sync_fd != 0xFFFFFFFFu) reqs.push_back({i, me.sync_fd, 1});
     me.sync_fd = 0xFFFFFFFFu;
   }
@@ -852,13 +900,16 @@ void sync_phase(oracle_handle* h) {
   // onSync at each receiver, requests in (receiver, sender, kind) order.
   std::vector<size_t> order(reqs.size());
   for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  // receivers: the processes at the addressed members' addresses
+  std::vector<uint32_t> recv(reqs.size());
+  for (size_t k = 0; k < reqs.size(); ++k) recv[k] = route(h, reqs[k].to);
   std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-    if (reqs[a].to != reqs[b].to) return reqs[a].to < reqs[b].to;
+    if (recv[a] != recv[b]) return recv[a] < recv[b];
     if (reqs[a].from != reqs[b].from) return reqs[a].from < reqs[b].from;
     return reqs[a].kind < reqs[b].kind;
   });
   struct Ack {
-    uint32_t responder, to, kind;
+    uint32_t responder, to, kind, seed;
     std::vector<uint32_t> table;
   };
   std::vector<Ack> acks;
@@ -866,17 +917,26 @@ void sync_phase(oracle_handle* h) {
     const SyncReq& rq = reqs[oi];
     if (!delivered(h, K_SYNC, rq.from, rq.to, rq.kind, tick_s)) continue;
     h->st.syncs_delivered++;
-    Member& me = h->m[rq.to];
+    const uint32_t rcv = recv[oi];
+    Member& me = h->m[rcv];
     const uint32_t others_snap = me.others;  // phase-start count (delta deferred)
     const std::vector<uint32_t>& data = snap[rq.from];
-    const uint32_t attempt = (rq.from << 1) | rq.kind;
+    const uint32_t attempt = sync_attempt(rq.from, rq.kind);
     for (uint32_t c = 0; c < h->N; ++c)  // syncMembership (MPI:468-471), reason SYNC
       if (data[c] != SWIM_ABSENT)
-        update_membership(h, rq.to, c, data[c], SWIM_R_SYNC, ph_sync, attempt, tick_s, others_snap, create_round);
-    // MPI:357-371: reply SYNC_ACK with the table after the merge
-    if (delivered(h, K_SYNC_ACK, rq.to, rq.from, rq.kind, tick_a)) acks.push_back({rq.to, rq.from, rq.kind, me.table});
+        update_membership(h, rcv, c, data[c], SWIM_R_SYNC, ph_sync, attempt, tick_s, others_snap, create_round);
+    // MPI:357-371: reply SYNC_ACK with the table after the merge (to the sender's address)
+    if (delivered(h, K_SYNC_ACK, rcv, rq.from, rq.kind, tick_a)) acks.push_back({rcv, rq.from, rq.kind, rq.to, me.table});
   }
   finish_phase(h);
+  // start0 takes the first initial SyncAck only (take(1), MPI:244-247): canonically the lowest seed
+  // address whose round trip was delivered; the others are dropped unprocessed (MPI:330-333)
+  std::vector<uint32_t> first_seed(h->N, NONE);
+  for (auto& ak : acks)
+    if (ak.kind == 2) first_seed[ak.to] = std::min(first_seed[ak.to], ak.seed);
+  acks.erase(std::remove_if(acks.begin(), acks.end(),
+                            [&](const Ack& a) { return a.kind == 2 && a.seed != first_seed[a.to]; }),
+             acks.end());
   // onSyncAck at each requester (MPI:343-349), acks in (requester, responder, kind) order.
   std::sort(acks.begin(), acks.end(), [](const Ack& a, const Ack& b) {
     if (a.to != b.to) return a.to < b.to;
@@ -886,12 +946,14 @@ void sync_phase(oracle_handle* h) {
   for (auto& ak : acks) {
     h->st.sync_acks_delivered++;
     Member& me = h->m[ak.to];
-    const uint32_t attempt = (ak.responder << 1) | ak.kind;
+    const uint32_t attempt = sync_attempt(ak.responder, ak.kind);
+    const uint32_t reason = ak.kind == 2 ? SWIM_R_INITIAL_SYNC : SWIM_R_SYNC;  // MPI:463-473 (onStart)
     const uint32_t others_snap = me.others;
     for (uint32_t c = 0; c < h->N; ++c)
       if (ak.table[c] != SWIM_ABSENT)
-        update_membership(h, ak.to, c, ak.table[c], SWIM_R_SYNC, ph_ack, attempt, tick_a, others_snap, create_round);
+        update_membership(h, ak.to, c, ak.table[c], reason, ph_ack, attempt, tick_a, others_snap, create_round);
   }
+  for (uint32_t i = 0; i < h->N; ++i) h->joining[i] = 0;
   finish_phase(h);
 }
 
@@ -931,18 +993,35 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
   h->seed = cfg->seed;
   h->group.assign(h->N, 0);
   std::memset(&h->st, 0, sizeof h->st);
+  const uint32_t n0 = cfg->n_initial ? cfg->n_initial : cfg->n_members;
+  if (n0 > h->N || n0 < 1) {
+    delete h;
+    return SWIM_EINVAL;
+  }
   try {
     h->m.resize(h->N);
     for (uint32_t i = 0; i < h->N; ++i) {
-      h->m[i].table.assign(h->N, SWIM_PACK(0, SWIM_ALIVE));  // converged start, all ALIVE inc 0
-      h->m[i].others = h->N - 1;
+      // converged start: members [0, n0) hold each other ALIVE inc 0; spare slots are in no table
+      h->m[i].table.assign(h->N, SWIM_ABSENT);
+      std::fill(h->m[i].table.begin(), h->m[i].table.begin() + n0, SWIM_PACK(0, SWIM_ALIVE));
+      h->m[i].others = n0 - 1;
+      h->m[i].alive = i < n0;
       h->m[i].gossips.held.assign(h->rc / 64, 0);
       h->m[i].gossips.win.assign(h->rc / 64, 0);
       h->m[i].gossips.inf.assign(h->rc, 0);
     }
     h->inbox.resize(h->N);
-    h->pres.assign(h->N, h->N - 1);
+    h->pres.assign(h->N, 0);
+    std::fill(h->pres.begin(), h->pres.begin() + n0, n0 - 1);
     h->last_removed.assign(h->N, 0);
+    h->addr.resize(h->N);
+    h->occ.assign(h->N, NONE);
+    for (uint32_t i = 0; i < h->N; ++i) h->addr[i] = i;
+    for (uint32_t i = 0; i < n0; ++i) h->occ[i] = i;
+    h->movers.resize(h->N);
+    h->started.assign(h->N, 0);
+    std::fill(h->started.begin(), h->started.begin() + n0, 1);
+    h->joining.assign(h->N, 0);
   } catch (...) {
     delete h;
     return SWIM_ENOMEM;
@@ -1017,6 +1096,49 @@ int oracle_leave(oracle_handle* h, const uint32_t* ids, uint32_t n) {
     me.leaving = true;
     me.leave_gid = (uint32_t)h->registry.size();
     spread_gossip(h, i, i, SWIM_DEAD, (int64_t)h->period * h->G);
+  }
+  return SWIM_OK;
+}
+
+// A new member starts in spare slot x at address a (ClusterImpl.start, ClusterImpl.java:170-227):
+// its table holds only itself ALIVE inc 0 (MPI:138-142), every protocol cursor starts afresh, and
+// this period's SYNC phase makes its initial SYNC to the seeds (MPI:222-257).
+void start_member(oracle_handle* h, uint32_t x, uint32_t a) {
+  Member& me = h->m[x];
+  std::fill(me.table.begin(), me.table.end(), SWIM_ABSENT);
+  me.table[x] = SWIM_PACK(0, SWIM_ALIVE);
+  me.others = 0;
+  me.delta = 0;
+  me.timers.clear();
+  me.alive = true;
+  h->started[x] = 1;
+  h->joining[x] = 1;
+  h->addr[x] = a;
+  h->occ[a] = x;
+}
+
+int oracle_join(oracle_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k)
+    if (ids[k] >= h->N || h->started[ids[k]] || h->occ[ids[k]] != NONE) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) start_member(h, ids[k], ids[k]);
+  return SWIM_OK;
+}
+
+int oracle_restart(oracle_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n) {
+  if (!h || (n && (!old_ids || !new_ids))) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t o = old_ids[k], x = new_ids[k];
+    if (o >= h->N || x >= h->N || !h->started[o] || h->m[o].alive || h->started[x] ||
+        h->occ[h->addr[o]] != NONE)
+      return SWIM_EINVAL;
+    for (uint32_t q = 0; q < k; ++q)
+      if (new_ids[q] == x || h->addr[old_ids[q]] == h->addr[o]) return SWIM_EINVAL;
+  }
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t a = h->addr[old_ids[k]];
+    h->movers[a].push_back(new_ids[k]);
+    start_member(h, new_ids[k], a);
   }
   return SWIM_OK;
 }

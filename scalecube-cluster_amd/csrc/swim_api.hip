@@ -47,6 +47,8 @@ struct swim_handle {
   // sharding
   uint32_t world = 1, rank = 0;
   uint32_t n_leaving = 0;  // swim_leave calls so far (the stop check runs only once one happened)
+  uint32_t n0 = 0;          // members started at create (swim_config.n_initial)
+  std::vector<uint8_t> started;  // ids ever started (spare slots: until swim_join / swim_restart)
   void* xsend = nullptr;
   void* xrecv = nullptr;
   uint64_t xsend_words = 0, xrecv_words = 0;
@@ -450,6 +452,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
         (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
         timed(h, 7, "k_sync_select", [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
+        if (P.njoin) hipLaunchKernelGGL(k_join_select, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
         timed(h, 6, "k_sync_snapshot", [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_REQ;
         if (W > 1) {  // tables of requesters whose receiver lives on another shard
@@ -484,6 +487,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * nloc, 256)), dim3(256), 0, s, P);
         });
         if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+        if (P.njoin) hipLaunchKernelGGL(k_join_scatter, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
         timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
@@ -516,6 +520,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (W > 1 && (rc = commit_end(h, P, x))) return rc;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
+        if (h->base.njoin) {  // the joins of this period are complete
+          HIPC(h, hipMemsetAsync(h->base.joining, 0, N, s));
+          h->base.njoin = 0;
+        }
         h->period++;
         h->pc = PC_FD;
         xchg_clear(x, SWIM_X_DONE, W);
@@ -557,7 +565,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (!cfg || !out) return SWIM_EINVAL;
   *out = nullptr;
   const swim_config& c = *cfg;
-  if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode > 1 ||
+  if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode > 1 || c.n_initial > c.n_members ||
+      (c.n_initial && c.n_initial < c.n_members && (c.mode != 0 || c.shard_world > 1)) ||
       (c.mode == 1 && (c.tracked_subjects < 1 || c.tracked_subjects > c.n_members || c.shard_world > 1)) ||
       c.ping_interval_ms <= 0 ||
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
@@ -598,6 +607,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     h->scap = (uint32_t)std::max<uint64_t>(64, std::min(bound, fit));
   }
   h->ecap = c.event_capacity;
+  h->n0 = c.n_initial ? c.n_initial : N;
+  h->started.assign(N, 0);
+  std::fill(h->started.begin(), h->started.begin() + h->n0, 1);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return SWIM_EHIP;
@@ -646,6 +658,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.loss_thr = 0;
   P.link = nullptr;
   P.inlink = nullptr;
+  P.rerouted = 0;
+  P.njoin = 0;
 
   const size_t NN = (size_t)P.nloc * P.W;  // this shard's rows
   const size_t NL = P.nloc;
@@ -674,6 +688,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.leaving, N);
   ALLOC(P.stopf, N);
   ALLOC(P.leave_slot, N);
+  ALLOC(P.addr, N);
+  ALLOC(P.occ, N);
+  ALLOC(P.mv_head, N);
+  ALLOC(P.mv_next, N);
+  ALLOC(P.joining, N);
+  ALLOC(P.jslot, N);
+  ALLOC(P.jwin, N);
   ALLOC(group, N);
   ALLOC(P.fd_epoch, N);
   ALLOC(P.fd_cursor, N);
@@ -784,8 +805,18 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   }
   hipStream_t s = h->stream;
   const uint32_t fill_blocks = 4096;
-  // converged start: every view holds every member ALIVE incarnation 0 (MPI:139 + initial SYNC)
-  hipLaunchKernelGGL(k_fill_u32, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, SWIM_PACK(0, SWIM_ALIVE));
+  // converged start: every view holds every member ALIVE incarnation 0 (MPI:139 + initial SYNC);
+  // spare slots (ids >= n_initial) are in no view
+  const uint32_t n0 = h->n0;
+  if (n0 == N)
+    hipLaunchKernelGGL(k_fill_u32, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, SWIM_PACK(0, SWIM_ALIVE));
+  else
+    hipLaunchKernelGGL(k_init_rows, dim3(fill_blocks), dim3(256), 0, s, P.view, NN, P.W, n0);
+  hipLaunchKernelGGL(k_iota_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.addr, N, N);
+  hipLaunchKernelGGL(k_iota_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.occ, N, n0);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.mv_head, (size_t)N, NONE);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.mv_next, (size_t)N, NONE);
+  (void)hipMemsetAsync(P.joining, 0, N, s);
   (void)hipMemsetAsync(P.dl, 0, NN * 4, s);
   (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
   (void)hipMemsetAsync(P.hb, 0, NL * (h->GC / 32) * 4, s);
@@ -795,14 +826,20 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmap, (size_t)N, NONE);
     (void)hipMemsetAsync(P.track_req, 0, N, s);
   }
-  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, N - 1);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, n0 - 1);
   // presence is per shard: observers of this shard holding the subject (all but the subject itself)
-  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, P.nloc);
-  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P.pres + P.row0, (size_t)P.nloc,
-                     P.nloc - 1);
+  if (n0 == N) {
+    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, P.nloc);
+    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P.pres + P.row0, (size_t)P.nloc,
+                       P.nloc - 1);
+  } else {  // unsharded
+    (void)hipMemsetAsync(P.pres, 0, (size_t)N * 4, s);
+    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(n0, 256)), dim3(256), 0, s, P.pres, (size_t)n0, n0 - 1);
+  }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.sync_fd, (size_t)N, NONE);
   (void)hipMemsetAsync(P.cnt_delta, 0, (size_t)N * 4, s);
-  (void)hipMemsetAsync(P.alive, 1, N, s);
+  (void)hipMemsetAsync(P.alive, 1, n0, s);
+  if (n0 < N) (void)hipMemsetAsync(P.alive + n0, 0, N - n0, s);
   (void)hipMemsetAsync(P.leaving, 0, N, s);
   (void)hipMemsetAsync(P.stopf, 0, N, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.leave_slot, (size_t)N, NONE);
@@ -823,9 +860,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
                      NONE);
-  {  // every member of this shard starts with others = N - 1; all N members alive
-    const uint32_t all = P.nloc, alive = N;
-    (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(N)], &all, 4, hipMemcpyHostToDevice, s);
+  {  // every started member of this shard starts with others = n0 - 1; n0 members alive
+    const uint32_t all = n0 == N ? P.nloc : n0, alive = n0;
+    (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(n0)], &all, 4, hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(&P.ctl->alive_count, &alive, 4, hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
   }
@@ -927,6 +964,70 @@ int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n) {
   return SWIM_OK;
 }
 
+namespace {
+// a spare slot x starts at address a (ClusterImpl.start): table = itself ALIVE inc 0, fresh cursors,
+// initial SYNC to the seeds in this period's SYNC phase (k_join_select)
+int start_member(swim_handle* h, uint32_t x, uint32_t a) {
+  hipLaunchKernelGGL(k_join_one, dim3(1), dim3(256), 0, h->stream, h->base, x, a);
+  h->started[x] = 1;
+  h->base.njoin++;
+  return SWIM_OK;
+}
+
+int join_checks(swim_handle* h, uint32_t n) {
+  if (h->world > 1 || h->base.nxk) return fail(h, SWIM_EINVAL, "join / restart: dense, unsharded handles only");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "join / restart: a period is in flight");
+  const uint64_t seeds = std::min<uint64_t>(h->cfg.n_seeds, h->N);
+  if ((uint64_t)(h->base.njoin + n) * std::max<uint64_t>(1, seeds) > h->scap)
+    return fail(h, SWIM_EINVAL, "join / restart: too many initial SYNCs in one period for sync_capacity");
+  return SWIM_OK;
+}
+}  // namespace
+
+int swim_join(swim_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  int rc = join_checks(h, n);
+  if (rc) return rc;
+  std::vector<uint32_t> occ(h->N);
+  HIPC(h, hipMemcpyAsync(occ.data(), h->base.occ, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  for (uint32_t k = 0; k < n; ++k) {
+    if (ids[k] >= h->N || h->started[ids[k]] || occ[ids[k]] != NONE)
+      return fail(h, SWIM_EINVAL, "swim_join: not a free spare slot");
+    for (uint32_t q = 0; q < k; ++q)
+      if (ids[q] == ids[k]) return fail(h, SWIM_EINVAL, "swim_join: duplicate id");
+  }
+  for (uint32_t k = 0; k < n; ++k) start_member(h, ids[k], ids[k]);
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
+int swim_restart(swim_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n) {
+  if (!h || (n && (!old_ids || !new_ids))) return SWIM_EINVAL;
+  int rc = join_checks(h, n);
+  if (rc) return rc;
+  const uint32_t N = h->N;
+  std::vector<uint32_t> occ(N), addr(N);
+  std::vector<uint8_t> alive(N);
+  HIPC(h, hipMemcpyAsync(occ.data(), h->base.occ, (size_t)N * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(addr.data(), h->base.addr, (size_t)N * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, N, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t o = old_ids[k], x = new_ids[k];
+    if (o >= N || x >= N || !h->started[o] || alive[o] || h->started[x] || occ[addr[o]] != NONE)
+      return fail(h, SWIM_EINVAL, "swim_restart: old id must be stopped with its address free, new id a spare slot");
+    for (uint32_t q = 0; q < k; ++q)
+      if (new_ids[q] == x || addr[old_ids[q]] == addr[o]) return fail(h, SWIM_EINVAL, "swim_restart: duplicate");
+  }
+  h->base.rerouted = 1;
+  for (uint32_t k = 0; k < n; ++k) start_member(h, new_ids[k], addr[old_ids[k]]);
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
 int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
   if (!h || (n && !ids)) return SWIM_EINVAL;
   std::vector<uint8_t> alive(h->N);
@@ -938,6 +1039,7 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
     if (!alive[c]) continue;
     alive[c] = 0;
     hipLaunchKernelGGL(k_crash, dim3(blocks_for(h->N, 256)), dim3(256), 0, h->stream, h->base, c);
+    hipLaunchKernelGGL(k_stop_addr, dim3(1), dim3(64), 0, h->stream, h->base, c);
   }
   HIPC(h, hipMemcpyAsync(h->base.alive, alive.data(), h->N, hipMemcpyHostToDevice, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -1147,6 +1249,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->apply_words = stats[ST_APPLY_WORDS];
   out->apply_runs = stats[ST_APPLY_RUNS];
   out->apply_subjects = stats[ST_APPLY_SUBJ];
+  out->fd_dead_events = stats[ST_FD_DEAD_EV];
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];
@@ -1306,3 +1409,4 @@ int swim_kernel_time_reset(swim_handle* h, int enable) {
 }
 
 }  // extern "C"
+

@@ -55,6 +55,7 @@ enum StatIdx : int {
   ST_APPLY_WORDS,  // receipt words k_gossip_apply folded into holdings and infection rounds
   ST_APPLY_RUNS,   // subject-run representatives it read from the ring and hashed
   ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
+  ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
   ST_COUNT
 };
 
@@ -146,6 +147,19 @@ struct KP {
   const uint8_t* group;
   const uint8_t* link;    // outbound block bitmap [src][dst] (send error) or nullptr
   const uint8_t* inlink;  // inbound block bitmap [dst][src] (silent drop at dst) or nullptr
+  // addresses. Until the first swim_restart (rerouted == 0) member x lives at
+  // address x and is reached iff alive; afterwards a message to x reaches occ[addr[x]], the running
+  // member at x's address, and partition groups / blocks apply per address
+  uint32_t rerouted;
+  uint32_t* addr;     // [N] member -> address
+  uint32_t* occ;      // [N] address -> running member or NONE (kept current in every mode)
+  uint32_t* mv_head;  // [N] address -> the last member restarted on it, or NONE
+  uint32_t* mv_next;  // [N] member -> the member restarted on the same address before it, or NONE
+  // joins (swim_join / swim_restart) of the current period: initial SYNC to the seeds
+  uint32_t njoin;     // members joining this period (0: none, the join kernels are not launched)
+  uint8_t* joining;   // [N]
+  uint32_t* jslot;    // [N] a joiner's SYNC staging slot (its table, one payload for every seed)
+  uint32_t* jwin;     // [N] the seed member whose SYNC_ACK the joiner merges (first round trip), or NONE
   // state
   uint32_t* view;
   uint32_t* dl;
@@ -265,6 +279,13 @@ __device__ __forceinline__ uint32_t cell_get(const KP& P, uint32_t obs, uint32_t
 }
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// the member whose transport receives a message sent to member x (TransportImpl sends to
+// member.address()): x itself while alive, or after a restart on x's address the new member
+__device__ __forceinline__ uint32_t route(const KP& P, uint32_t x) {
+  return P.rerouted ? P.occ[P.addr[x]] : (P.alive[x] ? x : NONE);
+}
+__device__ __forceinline__ uint32_t addr_of(const KP& P, uint32_t x) { return P.rerouted ? P.addr[x] : x; }
 constexpr uint32_t REMOTE = 0xFFFFFFFEu;   // req_stage of a request staged on another shard
 constexpr uint32_t XREC = 0x80000000u;     // in_list entry: a received window record, not a local row
 constexpr uint32_t INCAP = 16;  // in_list slots per receiver per round (random peers: in-degree ~ f)
@@ -291,6 +312,8 @@ __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {
 // send; an inbound block at dst (blockInbound, :255-269) drops it silently
 // (NetworkEmulatorTransport.java:73-77). For one-way messages both just lose the message.
 __device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t dst) {
+  src = addr_of(P, src);
+  dst = addr_of(P, dst);
   if (P.part_active && P.group[src] != P.group[dst]) return false;
   if (bit_at(P.link, (uint64_t)src * P.N + dst)) return false;
   return !bit_at(P.inlink, (uint64_t)dst * P.N + src);
@@ -298,19 +321,30 @@ __device__ __forceinline__ bool link_open(const KP& P, uint32_t src, uint32_t ds
 
 // Sender side (tryFailOutbound, NetworkEmulator.java:166-180): false = the send fails at once
 // (loss draw, blocked destination / partition cut, stopped transport on either end).
+// src / dst are the member ids the message is addressed from / to; the loss draw is keyed by the
+// two processes that send and receive it (route).
 __device__ __forceinline__ bool out_ok(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
                                        uint32_t tick) {
-  if (!P.alive[src] || !P.alive[dst]) return false;
+  uint32_t rs = src, rd = dst;
+  if (P.rerouted) {
+    rs = route(P, src);
+    rd = route(P, dst);
+    if (rs == NONE || rd == NONE) return false;
+    src = P.addr[src];
+    dst = P.addr[dst];
+  } else if (!P.alive[src] || !P.alive[dst]) {
+    return false;
+  }
   if (P.part_active && P.group[src] != P.group[dst]) return false;
   if (bit_at(P.link, (uint64_t)src * P.N + dst)) return false;
   if (P.loss_mode == 0) return true;
   if (P.loss_mode == 2) return false;
-  return draw1(P.seed, kind, src, dst, c, tick) >= P.loss_thr;
+  return draw1(P.seed, kind, rs, rd, c, tick) >= P.loss_thr;
 }
 
 // Receiver side: dst's inbound filter on the message's sender (NetworkEmulatorTransport.java:64-68,73-77).
 __device__ __forceinline__ bool in_ok(const KP& P, uint32_t dst, uint32_t src) {
-  return !bit_at(P.inlink, (uint64_t)dst * P.N + src);
+  return !bit_at(P.inlink, (uint64_t)addr_of(P, dst) * P.N + addr_of(P, src));
 }
 
 __device__ __forceinline__ bool delivered(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
@@ -361,8 +395,10 @@ __device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32
   P.stg[idx] = make_uint4(origin, subject, record, gossip_hash(origin, seq));
 }
 
-// MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip.
+// MetadataStoreImpl.fetchMetadata (MetadataStoreImpl.java:151-193) as a liveness round trip; the
+// process at the subject's address answers only requests for its own id (:216-223).
 __device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t subj, uint32_t attempt) {
+  if (P.rerouted && route(P, subj) != subj) return false;
   return delivered(P, K_MREQ, obs, subj, attempt, P.tick) && delivered(P, K_MRESP, subj, obs, attempt, P.tick);
 }
 
@@ -381,6 +417,8 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
   uint32_t* cellp = P.view + lrow(P, obs) * P.W + col;
   const uint32_t r0 = *cellp;
   if (!is_overrides(r1, r0)) return 0u;
+  // a record of another member id at the observer's own address is ignored (MPI:499-505)
+  if (P.rerouted && subj != obs && P.addr[subj] == P.addr[obs]) return 0u;
   const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;
   if (subj == obs) {
     const uint32_t inc1 = (r1 == SWIM_DEAD) ? rec_inc(r0) : rec_inc(r1);

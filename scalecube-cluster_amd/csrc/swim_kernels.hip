@@ -64,6 +64,7 @@ __global__ void k_leave_stop(KP P) {
     P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
   }
   P.alive[c] = 0;
+  if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
 }
 
 // swim_leave: the member's own record becomes DEAD and is staged as a gossip (committed with the
@@ -80,6 +81,52 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
     }
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
+}
+
+// converged start with spare slots: cell (row, col) = BASELINE for col < n0, absent otherwise
+__global__ void k_init_rows(uint32_t* view, size_t n, uint32_t W, uint32_t n0) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    view[i] = (uint32_t)(i % W) < n0 ? BASELINE : SWIM_ABSENT;
+}
+
+// p[i] = i for i < n_id, NONE for the rest
+__global__ void k_iota_u32(uint32_t* p, uint32_t n, uint32_t n_id) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i < n_id ? i : NONE;
+}
+
+// a stopped member's address goes quiet (unless a restarted member already holds it)
+__global__ void k_stop_addr(KP P, uint32_t c) {
+  if (threadIdx.x == 0 && P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
+}
+
+// swim_join / swim_restart: spare slot x starts at address a (ClusterImpl.start, ClusterImpl.java:
+// 170-227) with a table holding only itself ALIVE inc 0 (MembershipProtocolImpl.java:138-142) and
+// fresh protocol state; a restart on another member's address links x into that address's movers.
+__global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
+  for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
+    P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
+    P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
+  }
+  if (threadIdx.x == 0) {
+    P.cnt[x] = 0u;
+    P.cnt_delta[x] = 0;
+    P.fd_epoch[x] = P.fd_cursor[x] = P.g_epoch[x] = P.g_cursor[x] = 0u;
+    P.gseq[x] = 0u;
+    P.sync_fd[x] = NONE;
+    P.held[x] = 0u;
+    P.ih_head[x] = 0u;
+    P.alive[x] = 1;
+    P.joining[x] = 1;
+    if (a != x) {
+      P.mv_next[x] = P.mv_head[a];
+      P.mv_head[a] = x;
+    }
+    P.addr[x] = a;
+    P.occ[a] = x;
+    atomicAdd(&P.ctl->bl_hist[bitlen(1u)], 1u);
+    atomicAdd(&P.ctl->alive_count, 1u);
+  }
 }
 
 // swim_crash: transport.stop() — presence no longer counted, timers dropped.
@@ -193,10 +240,13 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
     j = (i + 1) % N;
   }
   pr.j = j;
+  // onPing at the process on j's address answers DEST_GONE unless it is j itself (FDI:226-252),
+  // which computeMemberStatus turns into DEAD (FDI:370-391)
+  const uint32_t acked = (P.rerouted && route(P, j) != j) ? SWIM_DEAD : SWIM_ALIVE;
   if (delivered(P, K_PING, i, j, 0, P.tick) && delivered(P, K_ACK, j, i, 0, P.tick)) {
     pr.direct = 1;
     pr.nB = 1;
-    pr.stB = SWIM_ALIVE;
+    pr.stB = acked;
     return pr;
   }
   // selectPingReqMembers (FailureDetectorImpl.java:351-363)
@@ -228,7 +278,7 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
   }
   // cid-only matching (TransportImpl.java:236-238): that ack completes every pending
   // subscription, then i's inbound filter on its sender decides (NetworkEmulatorTransport.java:64-68)
-  pr.stB = (first != NONE && in_ok(P, i, first)) ? SWIM_ALIVE : SWIM_SUSPECT;
+  pr.stB = (first != NONE && in_ok(P, i, first)) ? acked : SWIM_SUSPECT;
   return pr;
 }
 
@@ -282,7 +332,7 @@ __global__ void k_track_one(KP P, uint32_t j) {
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_fd(KP P) {
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t probes = 0, direct = 0, preq = 0, sev = 0, aev = 0, created = 0;
+  uint32_t probes = 0, direct = 0, preq = 0, sev = 0, aev = 0, dev = 0, created = 0;
   Tally T;
   if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
     const Probe pr = fd_probe(P, i, true);
@@ -296,6 +346,8 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
       const uint32_t st = e < pr.nA ? (uint32_t)SWIM_SUSPECT : pr.stB;
       if (st == SWIM_ALIVE)
         ++aev;
+      else if (st == SWIM_DEAD)
+        ++dev;
       else
         ++sev;
       const uint32_t r0 = cell_get(P, i, j);
@@ -304,8 +356,9 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
         P.sync_fd[i] = j;
         continue;
       }
-      const uint32_t rec = apply_record(P, i, j, SWIM_PACK(rec_inc(r0), SWIM_SUSPECT), SWIM_R_FAILURE_DETECTOR_EVENT, 0u,
-                                        snap, T);
+      // SUSPECT with the record's incarnation, or DEAD (a DEST_GONE ack: never spread, MPI:571-587)
+      const uint32_t rec = apply_record(P, i, j, st == SWIM_DEAD ? SWIM_DEAD : SWIM_PACK(rec_inc(r0), SWIM_SUSPECT),
+                                        SWIM_R_FAILURE_DETECTOR_EVENT, 0u, snap, T);
       if (rec) {
         emit_gossip(P, i, j, rec, P.gseq[i]++);
         ++created;
@@ -317,6 +370,7 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
   add_stat(P, ST_FD_PING_REQ, preq);
   add_stat(P, ST_FD_SUSPECT_EV, sev);
   add_stat(P, ST_FD_ALIVE_EV, aev);
+  add_stat(P, ST_FD_DEAD_EV, dev);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -834,7 +888,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   const bool reg = __any(win_l) && np > 0u;
   // GossipRequest messages: every window gossip to every alive peer (GPI:225-239), counted here
   // because receivers that already hold a whole word never look at the senders' windows
-  const uint32_t alive_peers = (uint32_t)__popcll(__ballot(reg && lane < np && P.alive[s_peers[w][lane]]));
+  const uint32_t alive_peers = (uint32_t)__popcll(__ballot(reg && lane < np && route(P, s_peers[w][lane]) != NONE));
   winbits = wave_sum(winbits);
   uint32_t entry = m;  // what peer `lane` registers: m, or a pruned pair
   if (reg) {
@@ -885,7 +939,8 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     }
   }
   if (reg && lane < np) {
-    const uint32_t p = s_peers[w][lane];
+    uint32_t p = s_peers[w][lane];
+    if (P.rerouted && route(P, p) != NONE) p = route(P, p);  // the process at p's address receives it
     if (is_local(P, p)) {
       register_sender(P, p, entry);
     } else {  // the window travels to p's shard (k_gossip_pack / k_gossip_unpack)
@@ -969,7 +1024,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t);
       if (supp) removed += (uint32_t)__popc(atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
-    if (P.alive[sp.y]) removed_alive += removed;  // the send counter covers alive peers only
+    if (route(P, sp.y) != NONE) removed_alive += removed;  // the send counter covers alive peers only
   }
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
   add_stat(P, ST_IF_PAIRS, (blockIdx.x == 0 && threadIdx.x == 0) ? n : 0u);
@@ -1730,7 +1785,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
     const uint32_t to = rec[1];
-    P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = rec[0];
+    P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = 4u * (rec[0] >> 1) + (rec[0] & 1u);
   }
 }
 
@@ -1860,21 +1915,31 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
 // ---------------------------------------------------------------------------------------
 // SYNC / SYNC_ACK.
 // ---------------------------------------------------------------------------------------
-// selectSyncAddress (MembershipProtocolImpl.java:416-427): uniform over seeds U others.
+// selectSyncAddress (MembershipProtocolImpl.java:416-427): uniform over the set of addresses
+// seeds U otherMembers' addresses, by rejection sampling over address ids (address x = member x's;
+// seed addresses are members [0, n_seeds)'s; the own address is never a seed, MPI:166-172).
+__device__ __forceinline__ bool sync_addr_valid(const KP& P, uint32_t i, uint32_t own, uint32_t x) {
+  if (!P.rerouted) return x != i && (cell_get(P, i, x) != 0u || x < P.n_seeds);
+  if (x == own || P.addr[x] != x) return false;  // own address / an id that moved to another address
+  if (x < P.n_seeds || cell_get(P, i, x) != 0u) return true;
+  for (uint32_t y = P.mv_head[x]; y != NONE; y = P.mv_next[y])  // members restarted on address x
+    if (y != i && cell_get(P, i, y) != 0u) return true;
+  return false;
+}
+
 __device__ uint32_t select_sync_address(const KP& P, uint32_t i) {
   const uint32_t N = P.N;
-  uint32_t count = P.cnt[i];
-  for (uint32_t s = 0; s < P.n_seeds && s < N; ++s)
-    if (s != i && cell_get(P, i, s) == 0u) ++count;
-  if (count == 0u) return NONE;
+  const uint32_t own = addr_of(P, i), nseeds = P.n_seeds < N ? P.n_seeds : N;
+  // MPI:421-422: nothing to pick when no other member is known and no seed address is not our own
+  if (P.cnt[i] == 0u && (nseeds == 0u || (nseeds == 1u && own == 0u))) return NONE;
   uint32_t x = 0;
   for (uint32_t a = 0; a < 64u; ++a) {
     x = (uint32_t)(((uint64_t)draw1(P.seed, K_SYNC_PICK, i, a, 0, P.tick) * N) >> 32);
-    if (x != i && (cell_get(P, i, x) != 0u || x < P.n_seeds)) return x;
+    if (sync_addr_valid(P, i, own, x)) return x;
   }
   for (uint32_t d = 1; d <= N; ++d) {
     const uint32_t y = (uint32_t)(((uint64_t)x + d) % N);
-    if (y != i && (cell_get(P, i, y) != 0u || y < P.n_seeds)) return y;
+    if (sync_addr_valid(P, i, own, y)) return y;
   }
   return NONE;
 }
@@ -1891,7 +1956,9 @@ __global__ void k_sync_select(KP P) {
     P.sync_fd[i] = NONE;
     if (P.alive[i]) {
       uint32_t to[2];
-      to[0] = (P.period % P.S == i % P.S) ? select_sync_address(P, i) : NONE;  // doSync (:304-320)
+      // doSync (:304-320); a member joining this period makes its initial SYNCs instead (k_join_select)
+      const bool joins = P.njoin && P.joining[i];
+      to[0] = (!joins && P.period % P.S == i % P.S) ? select_sync_address(P, i) : NONE;
       to[1] = fdt;                                                              // MPI:389-397
       for (uint32_t k = 0; k < 2; ++k) {
         if (to[k] == NONE) continue;
@@ -1899,6 +1966,8 @@ __global__ void k_sync_select(KP P) {
         P.req_to[2 * i + k] = to[k];
         if (!delivered(P, K_SYNC, i, to[k], k, P.tick)) continue;
         ++dlv;
+        if (P.rerouted) to[k] = route(P, to[k]);  // the process at the address receives it
+        P.req_to[2 * i + k] = to[k];
         if (!is_local(P, to[k])) {  // the table travels to the receiver's shard (k_sync_pack)
           const uint32_t dst = to[k] / P.nloc;
           const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
@@ -1919,6 +1988,55 @@ __global__ void k_sync_select(KP P) {
   }
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
+}
+
+// start0 (MembershipProtocolImpl.java:222-257) of the members joining this period: one SYNC to every
+// seed address but the own one, all carrying the joiner's table (one staging slot); the joiner will
+// merge only the first SYNC_ACK to come back (take(1), :244-247), canonically the lowest seed address
+// whose round trip is delivered (jwin). Thread per member; launched only when some member joins.
+__global__ void k_join_select(KP P) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t sent = 0, dlv = 0;
+  if (i < P.N && P.joining[i] && P.alive[i]) {
+    P.jwin[i] = NONE;
+    P.jslot[i] = NONE;
+    const uint32_t nseeds = P.n_seeds < P.N ? P.n_seeds : P.N, own = addr_of(P, i);
+    uint32_t slot = NONE;
+    for (uint32_t s = 0; s < nseeds; ++s) {
+      if (s == own) continue;
+      ++sent;
+      if (!delivered(P, K_SYNC, i, s, 2u, P.tick)) continue;
+      ++dlv;
+      if (slot == NONE) {
+        slot = atomicAdd(&P.ctl->stage_count, 1u);
+        if (slot >= P.scap) {
+          atomicOr(&P.ctl->overflow, OV_SYNC);
+          break;
+        }
+        P.stage_req[slot] = 2 * i;
+        P.jslot[i] = slot;
+      }
+      const uint32_t rcv = route(P, s);
+      atomicAdd(&P.recv_count[rcv], 1u);
+      if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
+    }
+  }
+  add_stat(P, ST_SYNCS_SENT, sent);
+  add_stat(P, ST_SYNCS_DELIVERED, dlv);
+}
+
+// bucket entries are 4 * sender + kind (kind 2 = initial SYNC), so a receiver's requests sort in
+// (sender, kind) order
+__global__ void k_join_scatter(KP P) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P.N && P.joining[i] && P.alive[i] && P.jslot[i] != NONE && P.jslot[i] < P.scap) {
+    const uint32_t nseeds = P.n_seeds < P.N ? P.n_seeds : P.N, own = addr_of(P, i);
+    for (uint32_t s = 0; s < nseeds; ++s) {
+      if (s == own || !delivered(P, K_SYNC, i, s, 2u, P.tick)) continue;
+      const uint32_t rcv = route(P, s);
+      P.bucket[P.recv_off[rcv] + atomicAdd(&P.recv_fill[rcv], 1u)] = 4u * i + 2u;
+    }
+  }
 }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:457-461): payload = sender's table at phase start.
@@ -1967,7 +2085,7 @@ __global__ void k_sync_scatter(KP P) {
   if (q < 2u * (P.row0 + P.nloc) && P.req_stage[q] != NONE && P.req_stage[q] != REMOTE) {
     const uint32_t to = P.req_to[q];
     const uint32_t pos = P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u);
-    P.bucket[pos] = q;
+    P.bucket[pos] = 4u * (q >> 1) + (q & 1u);
   }
 }
 
@@ -1997,8 +2115,8 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tot
 // cells in parallel, gossip sequence numbers assigned in cell order by a block scan.
 // `ack_out` (may be null) receives the row after the merge (onSync's SYNC_ACK payload).
 __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint32_t* src, uint32_t* ack_out,
-                                          uint32_t attempt, uint32_t snap, uint32_t& seq, Tally& T, uint32_t& created,
-                                          uint32_t* lds4) {
+                                          uint32_t attempt, uint32_t reason, uint32_t snap, uint32_t& seq, Tally& T,
+                                          uint32_t& created, uint32_t* lds4) {
   uint32_t* row = P.view + lrow(P, obs) * P.W;
   // Dense rows: cell = subject, 4 cells per thread (16-B loads) when rows are 16-B aligned.
   // N x K rows: one column per thread, walked in subject order (colorder) so gossip sequence
@@ -2026,7 +2144,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
       for (uint32_t k = 0; k < per; ++k) {
         if (sv[k] == 0u || !is_overrides(sv[k], vv[k])) continue;
         const uint32_t subj = subj_of(P, cv[k]);
-        const uint32_t rec = apply_record(P, obs, subj, sv[k], SWIM_R_SYNC, attempt, snap, T);
+        const uint32_t rec = apply_record(P, obs, subj, sv[k], reason, attempt, snap, T);
         vv[k] = row[cv[k]];
         if (rec) {
           recs[nrec] = rec;
@@ -2067,7 +2185,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   const uint32_t off = P.recv_off[j];
   for (uint32_t k = threadIdx.x; k < cntj; k += blockDim.x) s_list[k] = P.bucket[off + k];
   __syncthreads();
-  if (threadIdx.x == 0) {  // insertion sort: request index q = 2*sender + kind
+  if (threadIdx.x == 0) {  // insertion sort: bucket entry 4 * sender + kind
     for (uint32_t a = 1; a < cntj; ++a) {
       const uint32_t v = s_list[a];
       uint32_t b = a;
@@ -2084,10 +2202,18 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   uint32_t seq = P.gseq[j];
   const uint32_t snap = P.cnt[j];
   for (uint32_t k = 0; k < cntj; ++k) {
-    const uint32_t q = s_list[k];
+    const uint32_t b = s_list[k], from = b >> 2, kind = b & 3u;
+    const uint32_t q = 2u * from + (kind & 1u);  // request index of a periodic / FD-triggered SYNC
     const uint32_t* src;
     uint32_t* ack;
-    if (is_local(P, q >> 1)) {
+    if (kind == 2u) {  // a joiner's initial SYNC; only the seed it will take the SYNC_ACK of keeps one
+      const uint32_t slot = P.jslot[from];
+      src = P.stage_sync + (size_t)slot * P.W;
+      ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
+      merge_row(P, j, src, ack, 0x80000000u | from, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
+      continue;
+    }
+    if (is_local(P, from)) {
       const uint32_t slot = P.req_stage[q];
       src = P.stage_sync + (size_t)slot * P.W;
       ack = P.stage_ack + (size_t)slot * P.W;
@@ -2100,7 +2226,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
         P.xsend[g + 1] = j;
       }
     }
-    merge_row(P, j, src, ack, q, snap, seq, T, created, s_lds4);
+    merge_row(P, j, src, ack, q, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
   add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * ncells(P) : 0u);
@@ -2113,35 +2239,48 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   __shared__ uint32_t s_lds4[4];
   const uint32_t i = P.row0 + blockIdx.x;
   if (i >= P.row0 + P.nloc) return;
-  uint32_t q[2], to[2], n = 0;
+  uint32_t kd[3], to[3], n = 0;  // kind 0 / 1: request 2i + kind; kind 2: the initial SYNC's first ack
   for (uint32_t k = 0; k < 2; ++k) {
     const uint32_t qq = 2 * i + k;
     if (P.req_stage[qq] == NONE) continue;
     const uint32_t t = P.req_to[qq];
     if (!delivered(P, K_SYNC_ACK, t, i, k, P.tick)) continue;
-    q[n] = qq;
+    kd[n] = k;
     to[n] = t;
     ++n;
   }
-  if (n == 0) return;
-  if (n == 2 && to[1] < to[0]) {  // (responder, kind) order
-    uint32_t a = q[0];
-    q[0] = q[1];
-    q[1] = a;
-    a = to[0];
-    to[0] = to[1];
-    to[1] = a;
+  if (P.njoin && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap) {  // checked in k_join_select
+    kd[n] = 2u;
+    to[n] = P.jwin[i];
+    ++n;
   }
+  if (n == 0) return;
+  for (uint32_t a = 1; a < n; ++a)  // (responder, kind) order
+    for (uint32_t b = a; b > 0 && (to[b] < to[b - 1] || (to[b] == to[b - 1] && kd[b] < kd[b - 1])); --b) {
+      uint32_t x = kd[b];
+      kd[b] = kd[b - 1];
+      kd[b - 1] = x;
+      x = to[b];
+      to[b] = to[b - 1];
+      to[b - 1] = x;
+    }
   Tally T;
   uint32_t created = 0;
   uint32_t seq = P.gseq[i];
   const uint32_t snap = P.cnt[i];
   for (uint32_t k = 0; k < n; ++k) {
-    const uint32_t slot = P.req_stage[q[k]];
-    const uint32_t attempt = (to[k] << 1) | (q[k] & 1u);
-    const uint32_t* src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[q[k]] * (P.N + 2u) + 2
-                                         : P.stage_ack + (size_t)slot * P.W;
-    merge_row(P, i, src, nullptr, attempt, snap, seq, T, created, s_lds4);
+    const uint32_t* src;
+    uint32_t attempt, reason = SWIM_R_SYNC;
+    if (kd[k] == 2u) {  // syncMembership(onStart = true): reason INITIAL_SYNC (MPI:463-473)
+      src = P.stage_ack + (size_t)P.jslot[i] * P.W;
+      attempt = 0x80000000u | to[k];
+      reason = SWIM_R_INITIAL_SYNC;
+    } else {
+      const uint32_t qq = 2 * i + kd[k], slot = P.req_stage[qq];
+      attempt = (to[k] << 1) | kd[k];
+      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.N + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
+    }
+    merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);

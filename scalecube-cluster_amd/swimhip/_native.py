@@ -52,7 +52,7 @@ class SwimConfig(ctypes.Structure):
         ("event_capacity", ctypes.c_uint32),
         ("sync_capacity", ctypes.c_uint32),
         ("tracked_subjects", ctypes.c_uint32),
-        ("flags", ctypes.c_uint32),
+        ("n_initial", ctypes.c_uint32),
         ("device", ctypes.c_int32),
         ("shard_rank", ctypes.c_uint32),
         ("shard_world", ctypes.c_uint32),
@@ -107,6 +107,7 @@ STAT_FIELDS = [
     "apply_words",
     "apply_runs",
     "apply_subjects",
+    "fd_dead_events",
 ]
 
 
@@ -152,6 +153,8 @@ def api_table(prefix: str):
         (prefix + "block_inbound", _I, [_P, _U32, _U32, _I]),
         (prefix + "crash", _I, [_P, _pU32, _U32]),
         (prefix + "leave", _I, [_P, _pU32, _U32]),
+        (prefix + "join", _I, [_P, _pU32, _U32]),
+        (prefix + "restart", _I, [_P, _pU32, _pU32, _U32]),
         (prefix + "step", _I, [_P, _U32]),
         (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
         (prefix + "read_view", _I, [_P, _U32, _pU32, _U32]),

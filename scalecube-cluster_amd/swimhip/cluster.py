@@ -75,7 +75,7 @@ class MembershipRecord:
 class SwimCluster:
     def __init__(self, config: ClusterConfig, n_members: int, seed: int = 0, *, event_capacity: int = 0,
                  gossip_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
-                 _lib=None, _prefix: str = "swim_", _shard=(0, 1)):
+                 n_initial: int = 0, _lib=None, _prefix: str = "swim_", _shard=(0, 1)):
         self._lib = _lib if _lib is not None else nat.load_swimhip()
         self._p = _prefix
         self.config = config
@@ -84,12 +84,12 @@ class SwimCluster:
         self._cfg = to_swim_config(config, self.n, seed, gossip_capacity=gossip_capacity,
                                    event_capacity=event_capacity, sync_capacity=sync_capacity,
                                    tracked_subjects=tracked_subjects, device=device, shard_rank=_shard[0],
-                                   shard_world=_shard[1])
+                                   shard_world=_shard[1], n_initial=n_initial)
         h = ctypes.c_void_p()
         self._h = None
         self._call("create", ctypes.byref(self._cfg), ctypes.byref(h))
         self._h = h
-        self._alive = np.ones(self.n, dtype=bool)
+        self._alive = np.arange(self.n) < (n_initial or self.n)
 
     # -- plumbing -------------------------------------------------------------------------
     def _fn(self, name):
@@ -163,6 +163,23 @@ class SwimCluster:
         drops that gossip."""
         ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
         self._call("leave", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+
+    def join(self, ids):
+        """ClusterImpl.start() of new members in spare slots (ids >= n_initial), each at an address
+        of its own: initial SYNC to the seeds (MembershipProtocolImpl.start0, :222-257)."""
+        ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
+        self._call("join", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+        self._alive[ids] = True
+
+    def restart(self, old_ids, new_ids):
+        """Restart stopped members on their addresses as new member ids (spare slots new_ids):
+        MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses (:453-520)."""
+        o = np.ascontiguousarray(np.asarray(list(old_ids), dtype=np.uint32))
+        w = np.ascontiguousarray(np.asarray(list(new_ids), dtype=np.uint32))
+        assert len(o) == len(w)
+        P = ctypes.POINTER(ctypes.c_uint32)
+        self._call("restart", self._h, o.ctypes.data_as(P), w.ctypes.data_as(P), len(o))
+        self._alive[w] = True
 
     # -- stepping -------------------------------------------------------------------------
     def step(self, periods: int = 1):

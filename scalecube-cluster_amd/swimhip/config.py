@@ -233,8 +233,9 @@ class ClusterConfig(_Cfg):
 
 def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_capacity: int = 0,
                    event_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
-                   shard_rank: int = 0, shard_world: int = 1):
-    """Marshal a ClusterConfig into the C struct of include/swimhip.h."""
+                   shard_rank: int = 0, shard_world: int = 1, n_initial: int = 0):
+    """Marshal a ClusterConfig into the C struct of include/swimhip.h. n_initial < n_members leaves
+    ids [n_initial, n_members) as spare slots for joins and restarts."""
     from ._native import SwimConfig
 
     fd, g, m = cfg.failureDetectorConfig(), cfg.gossipConfig(), cfg.membershipConfig()
@@ -260,7 +261,7 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
     c.event_capacity = event_capacity
     c.sync_capacity = sync_capacity
     c.tracked_subjects = tracked_subjects
-    c.flags = 0
+    c.n_initial = n_initial
     c.device = device
     c.shard_rank = shard_rank
     c.shard_world = shard_world

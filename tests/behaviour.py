@@ -386,11 +386,67 @@ def gossip_dissemination_bound(make):
         assert all(c.view(o)[n - 1] == 0 for o in range(n - 1)), (n, loss)
 
 
+def mp_restart_stopped_members(make):
+    """testRestartStoppedMembers (:374-451): c and d stop; a and b suspect, then remove them; new
+    members start on new addresses (spare ids 4 and 5) with the four old addresses as seeds and
+    join through the initial SYNC: everyone trusts everyone, nobody is suspected."""
+    c = make(membership_test_config(4), 6, 51, n_initial=4)
+    c.step(seconds(1))
+    for m in (A, B, C, D):
+        assert_trusted(c, m, *[x for x in (A, B, C, D) if x != m])
+    c.events()
+    c.crash([C, D])
+    c.step(seconds(1))
+    for m, o in ((A, B), (B, A)):
+        assert_trusted(c, m, o)
+        assert_suspected(c, m, C, D)
+    c.step(await_suspicion(4))
+    rem = removed_by(c)
+    for m, o in ((A, B), (B, A)):
+        assert_trusted(c, m, o)
+        assert_suspected(c, m)
+        assert rem.get(m) == {C, D}, rem
+    c2, d2 = 4, 5
+    c.join([c2, d2])
+    c.step(seconds(2))
+    for m in (A, B, c2, d2):
+        assert_trusted(c, m, *[x for x in (A, B, c2, d2) if x != m])
+        assert_suspected(c, m)
+
+
+def mp_restart_on_same_addresses(make):
+    """testRestartStoppedMembersOnSameAddresses (:453-520): c and d stop and are suspected; new
+    members (new ids 4 and 5) start on c's and d's addresses. A ping to the old ids now reaches the
+    new members, which answer DEST_GONE (FailureDetectorImpl.java:231-235): a and b remove the old
+    ids without waiting for the suspicion timeout, and everyone trusts the new ones."""
+    c = make(membership_test_config(4), 6, 52, n_initial=4)
+    c.step(seconds(1))
+    for m in (A, B, C, D):
+        assert_trusted(c, m, *[x for x in (A, B, C, D) if x != m])
+    c.events()
+    c.crash([C, D])
+    c.step(seconds(1))
+    for m, o in ((A, B), (B, A)):
+        assert_trusted(c, m, o)
+        assert_suspected(c, m, C, D)
+    c2, d2 = 4, 5
+    c.restart([C, D], [c2, d2])
+    c.step(seconds(2))
+    assert seconds(3) < await_suspicion(4)  # the removals below cannot be suspicion timeouts
+    rem = removed_by(c)
+    for m in (A, B, c2, d2):
+        assert_trusted(c, m, *[x for x in (A, B, c2, d2) if x != m])
+        assert_suspected(c, m)
+    for m in (A, B):
+        assert rem.get(m) == {C, D}, rem
+    assert c.stats()["fd_dead_events"] > 0
+
+
 ALL = [
     fd_trusted, fd_suspected, fd_trusted_despite_bad_network,
     mp_initial_phase_ok, mp_partition_no_outbound_then_recover, mp_member_lost_network_then_recover,
     mp_partition_twice_then_recover, mp_network_lost_on_all_nodes_then_recover, mp_long_partition_then_removed,
     mp_partition_no_inbound_then_removed, mp_partition_no_inbound_then_recover, mp_between_two_members_no_inbound,
     mp_between_two_members_no_outbound, mp_between_two_members_no_traffic, mp_partition_many_no_inbound_then_recover,
-    cluster_shutdown_removed, gossip_dissemination_bound,
+    cluster_shutdown_removed, gossip_dissemination_bound, mp_restart_stopped_members, mp_restart_on_same_addresses,
 ]

@@ -25,8 +25,8 @@ OUT = os.path.join(HERE, "oracle_scenarios.json")
 
 
 def trace(name):
-    cfg, n, seed, script = scenarios.SCENARIOS[name]
-    c = OracleCluster(cfg, n, seed, event_capacity=1 << 20)
+    cfg, n, seed, script, kw = scenarios.scenario(name)
+    c = OracleCluster(cfg, n, seed, event_capacity=1 << 20, **kw)
     steps = []
     ev_hash = hashlib.sha256()
     for _ in script(c):

@@ -14,7 +14,7 @@ PARITY_KEYS = [
     "period", "fd_probes", "fd_direct_ok", "fd_ping_req", "fd_suspect_events", "fd_alive_events",
     "gossips_created", "gossip_first_receipts", "gossip_sends", "syncs_sent", "syncs_delivered",
     "sync_acks_delivered", "records_accepted", "events_added", "events_removed", "suspicion_timeouts",
-    "refutations", "not_converged", "infected_suppressed",
+    "refutations", "not_converged", "infected_suppressed", "fd_dead_events",
 ]
 
 
@@ -122,6 +122,27 @@ def _leave(c, ids, loss, before, after):
         yield
 
 
+def _churn(c, crash, restart_new, join_new, loss, before=3, mid=4, after=25):
+    # Restarts and joins (MembershipProtocolTest.testRestartStoppedMembers / ...OnSameAddresses,
+    # :374-520, scaled up): members crash; some restart on their old addresses as new member ids
+    # (spare slots), whose replies to pings of the old ids are DEST_GONE (FailureDetectorImpl.java:
+    # 231-235); fresh members join on new addresses through the initial SYNC to the seeds
+    # (MembershipProtocolImpl.start0, :222-257).
+    c.set_loss(loss)
+    for _ in range(before):
+        c.step(1)
+        yield
+    c.crash(crash)
+    for _ in range(mid):
+        c.step(1)
+        yield
+    c.restart(crash[:len(restart_new)], restart_new)
+    c.join(join_new)
+    for _ in range(after):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -142,14 +163,28 @@ SCENARIOS = {
     "local24_inbound_blocks": (
         ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers([0, 1]).syncInterval(2000)),
         24, 8, _inbound),
+    # (config, n, seed, script, create kwargs): n_initial < n leaves spare slots for joins/restarts
+    "local40_restart_join": (
+        ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers([0, 1, 2]).syncInterval(3000)),
+        40, 11, lambda c: _churn(c, [3, 7, 20], [32, 33], [34, 35], 0.0), {"n_initial": 32}),
+    "lan288_restart_join_loss5": (
+        ClusterConfig.defaultLanConfig().membership(lambda o: o.seedMembers([0, 1, 2, 3])),
+        288, 12, lambda c: _churn(c, [5, 40, 41, 100, 200, 255], [256, 257, 258, 259], [260, 261, 262], 5.0),
+        {"n_initial": 256}),
 }
+
+
+def scenario(name):
+    """(config, n, seed, script, create kwargs) of scenario `name`."""
+    cfg, n, seed, script, *kw = SCENARIOS[name]
+    return cfg, n, seed, script, (kw[0] if kw else {})
 
 
 def run_pair(name, make_a, make_b, compare_every=1, full_tables=True, event_capacity=1 << 20):
     """Drive two implementations through scenario `name`, asserting equality as it goes."""
-    cfg, n, seed, script = SCENARIOS[name]
-    a = make_a(cfg, n, seed, event_capacity=event_capacity)
-    b = make_b(cfg, n, seed, event_capacity=event_capacity)
+    cfg, n, seed, script, kw = scenario(name)
+    a = make_a(cfg, n, seed, event_capacity=event_capacity, **kw)
+    b = make_b(cfg, n, seed, event_capacity=event_capacity, **kw)
     ga, gb = script(a), script(b)
     step = 0
     for _ in ga:

@@ -6,14 +6,14 @@ import behaviour
 from oracle_py import OracleCluster
 
 
-def _oracle(cfg, n, seed):
-    return OracleCluster(cfg, n, seed, event_capacity=1 << 16)
+def _oracle(cfg, n, seed, **kw):
+    return OracleCluster(cfg, n, seed, event_capacity=1 << 16, **kw)
 
 
-def _gpu(cfg, n, seed):
+def _gpu(cfg, n, seed, **kw):
     from swimhip import SwimCluster
 
-    return SwimCluster(cfg, n, seed, event_capacity=1 << 16)
+    return SwimCluster(cfg, n, seed, event_capacity=1 << 16, **kw)
 
 
 @pytest.mark.parametrize("case", behaviour.ALL, ids=[f.__name__ for f in behaviour.ALL])

@@ -10,9 +10,9 @@ from oracle_py import OracleCluster  # noqa: E402
 from swimhip import SwimCluster  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "local48_links"
-cfg, n, seed, script = scenarios.SCENARIOS[name]
-a = SwimCluster(cfg, n, seed, event_capacity=1 << 20)
-b = OracleCluster(cfg, n, seed, event_capacity=1 << 20)
+cfg, n, seed, script, kw = scenarios.scenario(name)
+a = SwimCluster(cfg, n, seed, event_capacity=1 << 20, **kw)
+b = OracleCluster(cfg, n, seed, event_capacity=1 << 20, **kw)
 ga, gb = script(a), script(b)
 step = 0
 for _ in ga:

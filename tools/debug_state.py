@@ -12,9 +12,9 @@ from oracle_py import OracleCluster  # noqa: E402
 from swimhip import SwimCluster  # noqa: E402
 
 name = sys.argv[1]
-cfg, n, seed, script = scenarios.SCENARIOS[name]
-a = SwimCluster(cfg, n, seed, event_capacity=1 << 20)
-b = OracleCluster(cfg, n, seed, event_capacity=1 << 20)
+cfg, n, seed, script, kw = scenarios.scenario(name)
+a = SwimCluster(cfg, n, seed, event_capacity=1 << 20, **kw)
+b = OracleCluster(cfg, n, seed, event_capacity=1 << 20, **kw)
 ga, gb = script(a), script(b)
 step = 0
 for _ in ga:
