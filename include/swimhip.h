@@ -154,6 +154,7 @@ typedef struct swim_stats {
   uint64_t apply_runs;        /* subject-run representatives read from the ring               */
   uint64_t apply_subjects;    /* updateMembership calls (one per subject per receiver)        */
   uint64_t fd_dead_events;    /* FailureDetectorEvent(DEAD): an ACK with DEST_GONE (FDI:231-235,383) */
+  uint64_t apply_spills;      /* subjects k_gossip_apply merged through the global inbox (LDS hash full); 0 in the oracle */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;

@@ -1250,6 +1250,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->apply_runs = stats[ST_APPLY_RUNS];
   out->apply_subjects = stats[ST_APPLY_SUBJ];
   out->fd_dead_events = stats[ST_FD_DEAD_EV];
+  out->apply_spills = stats[ST_APPLY_SPILL];
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];

@@ -56,6 +56,7 @@ enum StatIdx : int {
   ST_APPLY_RUNS,   // subject-run representatives it read from the ring and hashed
   ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
   ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
+  ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
   ST_COUNT
 };
 

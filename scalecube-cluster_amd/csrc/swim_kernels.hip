@@ -1406,7 +1406,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
-  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0;
+  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0;
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
@@ -1588,12 +1588,14 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
     }
     if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
+    nspills += threadIdx.x == 0 ? nsp : 0u;
     __syncthreads();  // the table is reused by the next receiver
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   add_stat(P, ST_APPLY_WORDS, nwords);
   add_stat(P, ST_APPLY_RUNS, nruns);
   add_stat(P, ST_APPLY_SUBJ, nsubj);
+  add_stat(P, ST_APPLY_SPILL, nspills);
   flush_tally(P, T);
 }
 

@@ -108,6 +108,7 @@ STAT_FIELDS = [
     "apply_runs",
     "apply_subjects",
     "fd_dead_events",
+    "apply_spills",
 ]
 
 

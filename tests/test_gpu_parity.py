@@ -150,3 +150,54 @@ def test_c3_schedule_small_parity():
         sa, sb = a.stats(), b.stats()
         assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
     assert a.stats()["gossips_created"] > 10 * n  # the storm really happened
+
+
+_SPILL_SCRIPT = """
+import sys
+sys.path[:0] = {paths!r}
+import scenarios
+from oracle_py import OracleCluster
+from swimhip import SwimCluster
+a, b = scenarios.run_pair("lan288_restart_join_loss5", SwimCluster, OracleCluster)
+spills = a.stats()["apply_spills"]
+import bench
+from swimhip import ClusterConfig
+n = 1024
+x = SwimCluster(bench.preset_config("lan"), n, seed=1, gossip_capacity=1 << 17)
+y = OracleCluster(bench.preset_config("lan"), n, seed=1)
+for c in (x, y):
+    c.step(3)
+    bench.inject_faults(c, "c3", 3, 1, n=n)
+for _ in range(6):
+    for c in (x, y):
+        c.step(5)
+    assert x.digest() == y.digest()
+    sx, sy = x.stats(), y.stats()
+    assert {{k: sx[k] for k in scenarios.PARITY_KEYS}} == {{k: sy[k] for k in scenarios.PARITY_KEYS}}
+spills += x.stats()["apply_spills"]
+print("SPILLS", spills)
+"""
+
+
+def test_apply_spill_path_parity():
+    """k_gossip_apply's overflow paths (a subject that finds no LDS hash slot within HPROBE probes
+    goes through the global inbox and the LDS spill list; the summary walk without compaction when
+    the table is at its cap) only run in storm rounds of the full C3 bench with the product's
+    16,384-slot hash. A variant built with a 64-slot hash (__graft_entry__.build, -DSWIM_APPLY_HLOG=6)
+    takes them in almost every round: it must still match the oracle bit for bit, and the spill
+    counter proves the path ran."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "variants", "libswimhip_hlog6.so")
+    assert os.path.exists(lib), "variant not built: run __graft_entry__.build()"
+    paths = [here, repo, os.path.join(repo, "oracle"), os.path.join(repo, "scalecube-cluster_amd")]
+    env = dict(os.environ, SWIMHIP_LIB=lib)
+    out = subprocess.run([sys.executable, "-c", _SPILL_SCRIPT.format(paths=paths)], env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    spills = int(out.stdout.split("SPILLS")[-1])
+    assert spills > 0, "the spill path never ran"
