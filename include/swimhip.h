@@ -274,6 +274,10 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
  * gossip cursor, gossip counter, member count (others). */
 int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n);
 
+/* Debug: per sender, cumulative GossipRequests to alive peers before infectedFrom suppression
+ * (out2n[2i]) and the ones suppressed (out2n[2i+1]); gossip_sends = sum(before) - sum(suppressed). */
+int swim_debug_sends(swim_handle* h, uint64_t* out2n, uint32_t n);
+
 /* Kernel timing for the bench: the last step's per-kernel-class device time (ms, HIP events
  * on the handle's stream). idx: 0 fd, 1 gossip_pull, 2 gossip_apply, 3 suspicion, 4 sync_merge,
  * 5 sync_ack, 6 sync_snapshot, 7 bookkeeping, 8 gossip_select, 9 gossip_inhist, 10 gossip_pairwin

@@ -38,6 +38,8 @@ def load_oracle():
         lib.oracle_debug_holdings.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P, P, ctypes.c_uint32, P]
         lib.oracle_debug_member_state.restype = ctypes.c_int
         lib.oracle_debug_member_state.argtypes = [ctypes.c_void_p, P, ctypes.c_uint32]
+        lib.oracle_debug_sends.restype = ctypes.c_int
+        lib.oracle_debug_sends.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
         lib.oracle_is_overrides.restype = ctypes.c_int
         lib.oracle_is_overrides.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         lib.oracle_philox.restype = ctypes.c_uint32

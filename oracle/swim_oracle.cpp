@@ -21,6 +21,8 @@
 #include "swim_oracle.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -256,6 +258,8 @@ struct oracle_handle {
   std::vector<swim_event> events;
   swim_stats st;
   std::vector<uint32_t> pres, last_removed;
+  std::vector<uint64_t> dbg_send;  // debug: per sender, GossipRequests to alive peers before / by infectedFrom
+  uint32_t dbg_watch = 0xFFFFFFFFu;
   // pending gossip-delivered records per receiver: subject -> lattice max
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> inbox;
 };
@@ -739,6 +743,11 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       if (pm.alive) {
         h->st.gossip_sends += nsend;
         h->st.infected_suppressed += nsupp;
+        h->dbg_send[2 * s] += nsend + nsupp;
+        h->dbg_send[2 * s + 1] += nsupp;
+        if (s == h->dbg_watch)
+          std::fprintf(stderr, "oracle watch r=%lld peer=%u rp=%d send=%llu supp=%llu\n", (long long)r, p, (int)rp,
+                       (unsigned long long)nsend, (unsigned long long)nsupp);
       }
       // the link part of delivered(): both alive, no partition cut, no outbound / inbound block
       if (!nsend || !pm.alive || h->loss_bp >= 10000 || !link_ok(h, s, p)) continue;
@@ -1014,6 +1023,8 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
     h->pres.assign(h->N, 0);
     std::fill(h->pres.begin(), h->pres.begin() + n0, n0 - 1);
     h->last_removed.assign(h->N, 0);
+    h->dbg_send.assign(2ull * h->N, 0);
+    if (const char* w = std::getenv("SWIMHIP_DEBUG_WATCH")) h->dbg_watch = (uint32_t)std::strtoul(w, nullptr, 10);
     h->addr.resize(h->N);
     h->occ.assign(h->N, NONE);
     for (uint32_t i = 0; i < h->N; ++i) h->addr[i] = i;
@@ -1226,6 +1237,12 @@ int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash,
     ++n;
   }
   *n_out = n;
+  return SWIM_OK;
+}
+
+int oracle_debug_sends(oracle_handle* h, uint64_t* out2n, uint32_t n) {
+  if (!h || !out2n || n != h->N) return SWIM_EINVAL;
+  std::copy(h->dbg_send.begin(), h->dbg_send.end(), out2n);
   return SWIM_OK;
 }
 

@@ -49,6 +49,7 @@ int oracle_debug_holdings(oracle_handle* h, uint32_t member, uint32_t* out_hash,
                           uint32_t* n_out);
 
 int oracle_debug_member_state(oracle_handle* h, uint32_t* out6n, uint32_t n);
+int oracle_debug_sends(oracle_handle* h, uint64_t* out2n, uint32_t n);
 
 /* Pure helpers (known-answer tests). */
 int oracle_is_overrides(uint32_t r1, uint32_t r0);

@@ -14,9 +14,6 @@
 #include <string>
 #include <vector>
 
-#include <hipcub/device/device_radix_sort.hpp>
-#include <hipcub/device/device_scan.hpp>
-
 #include "swim_kernels.hip"
 
 using namespace swim;
@@ -54,16 +51,14 @@ struct swim_handle {
   uint64_t xsend_words = 0, xrecv_words = 0;
   uint32_t* d_xcounts = nullptr;
   uint32_t* d_blx = nullptr;
-  // gossip commits: sort keys/values (in, out) and radix-sort scratch
+  // gossip commits: sort keys/values (ping-pong) and the radix sort's counters (k_commit, k_rs_*)
+  uint32_t *cs_ghist = nullptr, *cs_ctr = nullptr, *cs_stat = nullptr;
+  uint32_t cs_maxt = 1;
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
-  void* sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
   uint32_t n_out_pairs = 0, n_in_pairs = 0, nneed = 0;
   uint32_t out_pairs[SWIM_MAX_WORLD] = {0};
-  void* scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
   unsigned long long* d_digest = nullptr;
   std::vector<void*> allocs;
   std::string err;
@@ -235,30 +230,45 @@ void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
 
 int check_overflow(swim_handle* h);
 
-// Sort the n gossips staged in h->ck[0] / h->cv[0] by (subject, record) and commit them.
-int commit_sorted(swim_handle* h, const KP& P, uint32_t n) {
+// Order the phase's gossips by (subject, record) and commit them: one k_commit launch. stg != nullptr: the local stage, counted on the device (no host round trip); otherwise
+// the n gathered gossips already in h->ck[0] / h->cv[0].
+int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n) {
   hipStream_t s = h->stream;
-  if (n) {
-    size_t tb = h->sort_tmp_bytes;
-    const int end_bit = 32 + (int)bitlen(h->N);
-    HIPC(h, hipcub::DeviceRadixSort::SortPairs(h->sort_tmp, tb, h->ck[0], h->ck[1], h->cv[0], h->cv[1], (int)n, 0,
-                                                end_bit, s));
-    timed(h, 7, "k_gossip_commit", [&] {
-      hipLaunchKernelGGL(k_gossip_commit, dim3(std::min<uint32_t>(blocks_for(n, 256), 2048)), dim3(256), 0, s, P,
-                         h->ck[1], h->cv[1], n);
-    });
-  }
-  hipLaunchKernelGGL(k_gossip_commit_fin, dim3(1), dim3(1), 0, s, P, n);
+  CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u};
+  C.npass = (32u + bitlen(h->N - 1u) + 7u) / 8u;  // key = subject << 32 | record
+  // the sharded batch size is known here: launch the radix kernels only when they have work
+  const bool big = stg != nullptr || n > CS_SMALL;
+  const uint32_t tiles = stg ? h->cs_maxt : std::max<uint32_t>(1, (n + CS_TILE - 1) / CS_TILE);
+  timed(h, 7, "k_commit", [&] {
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
+    if (big) {
+      hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C);
+      for (uint32_t p = 0; p < C.npass; ++p) {
+        const bool even = (p & 1u) == 0u;
+        hipLaunchKernelGGL(k_rs_pass, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C, p, even ? C.k0 : C.k1,
+                           even ? C.v0 : C.v1, even ? C.k1 : C.k0, even ? C.v1 : C.v0);
+      }
+      const bool in0 = (C.npass & 1u) == 0u;
+      hipLaunchKernelGGL(k_rs_commit, dim3(1024), dim3(256), 0, s, P, stg, n, in0 ? C.k0 : C.k1, in0 ? C.v0 : C.v1);
+      hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n);
+    }
+  });
   return SWIM_OK;
 }
 
-// Commit the phase's staged gossips. Unsharded: in place. Sharded: the host all-gathers every
-// shard's stage first (returns true: exchange pending); all shards then sort the same batch.
+// Commit the phase's staged gossips. Unsharded: in place, sized on the device (overflow is
+// reported at the next swim_sync; k_gossip_prep lists nothing once it is set, so a run never
+// feeds a wrapped ring to the gossip kernels). Sharded: the host all-gathers every shard's stage
+// first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
   hipStream_t s = h->stream;
-  // {overflow, stg_count} in one copy: a run stops at the first phase whose buffers overflowed (a
-  // wrapped gossip ring would otherwise feed the next phase's kernels). Sharded hosts share the
-  // error with every rank before the next collective (swimhip/sharded.py, status all-gather).
+  if (h->world == 1) {
+    *rc = commit_sorted(h, P, P.stg, 0u);
+    return false;
+  }
+  // {overflow, stg_count} in one copy: a sharded run stops at the first phase whose buffers
+  // overflowed; the hosts share the error with every rank before the next collective
+  // (swimhip/sharded.py, status all-gather).
   static_assert(offsetof(Ctl, stg_count) == offsetof(Ctl, overflow) + 4, "Ctl layout");
   uint32_t ovn[2] = {0u, 0u};
   HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 8, hipMemcpyDeviceToHost, s));
@@ -267,13 +277,9 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
     *rc = check_overflow(h);
     return false;
   }
-  uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
-  if (h->world == 1) {
-    if (n) hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(n, 256)), dim3(256), 0, s, P.stg, n, 0u, h->ck[0], h->cv[0]);
-    *rc = commit_sorted(h, P, n);
-    return false;
-  }
+  const uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
   if (n) (void)hipMemcpyAsync(h->xsend, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
+  HIPC_RC(h, rc, hipMemsetAsync(&P.ctl->stg_count, 0, 4, s));
   KP Q = P;
   Q.xsend = reinterpret_cast<uint32_t*>(h->xsend);
   hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, 4u * n);
@@ -301,7 +307,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   KP Q = P;
   Q.xrecv = xr;
   hipLaunchKernelGGL(k_round_max_merge, dim3(64), dim3(256), 0, s, Q, h->d_xcounts, h->d_blx);
-  return commit_sorted(h, P, total);
+  return commit_sorted(h, P, nullptr, total);
 }
 
 // Runs the current period from h->pc. Returns SWIM_OK with x->op = SWIM_X_DONE at the end of
@@ -321,6 +327,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           track_commit(h, P);
         }
         timed(h, 0, "k_fd", [&] { hipLaunchKernelGGL(k_fd, dim3(gL), dim3(256), 0, s, P); });
+        // a DEST_GONE ack (restarted address) removes the probed member in this phase: its count
+        // change is visible from the first gossip round on, as at the end of every other phase
+        timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_FD_C;
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
         if (rc) return rc;
@@ -381,8 +390,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
         if (n_in) {
           hipLaunchKernelGGL(k_gossip_need, dim3(std::min<uint32_t>(n_in, 8192)), dim3(256), 0, s, P, n_in, h->nneed);
-          size_t tb = h->scan_tmp_bytes;
-          HIPC(h, hipcub::DeviceScan::ExclusiveSum(h->scan_tmp, tb, P.rtot, P.roff, (int)n_in, s));
+          hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(CS_THREADS), 0, s, P.rtot, P.roff, n_in);
         }
         xchg_clear(x, SWIM_X_ALLTOALLV, W);
         for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
@@ -398,8 +406,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         xchg_clear(x, SWIM_X_ALLTOALLV, W);
         if (n_out) {
           hipLaunchKernelGGL(k_gossip_wcount, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, P, n_out, h->nneed);
-          size_t tb = h->scan_tmp_bytes;
-          HIPC(h, hipcub::DeviceScan::ExclusiveSum(h->scan_tmp, tb, P.wcnt, P.woff, (int)n_out + 1, s));
+          hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(CS_THREADS), 0, s, P.wcnt, P.woff, n_out + 1);
           std::vector<uint32_t> woff(n_out + 1);
           HIPC(h, hipMemcpyAsync(woff.data(), P.woff, 4ull * (n_out + 1), hipMemcpyDeviceToHost, s));
           HIPC(h, hipStreamSynchronize(s));
@@ -725,29 +732,16 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.roff, pin);
     ALLOC(P.wcnt, pout + 1);
     ALLOC(P.woff, pout + 1);
-    if (rc == SWIM_OK) {
-      size_t tb = 0;
-      (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, P.rtot, P.roff, (int)std::max(pin, pout + 1), h->stream);
-      h->scan_tmp_bytes = tb;
-      char* tmp = nullptr;
-      rc = dalloc(h, &tmp, tb);
-      h->scan_tmp = tmp;
-      if (rc == SWIM_OK) (void)hipMemsetAsync(P.wcnt, 0, (pout + 1) * 4, h->stream);
-    }
+    if (rc == SWIM_OK) (void)hipMemsetAsync(P.wcnt, 0, (pout + 1) * 4, h->stream);
   }
   for (int k = 0; k < 2; ++k) {
     ALLOC(h->ck[k], (size_t)P.stg_cap * world);
     ALLOC(h->cv[k], (size_t)P.stg_cap * world);
   }
-  if (rc == SWIM_OK) {
-    size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, h->ck[0], h->ck[1], h->cv[0], h->cv[1],
-                                             (int)(P.stg_cap * world), 0, 64, h->stream);
-    h->sort_tmp_bytes = tb;
-    char* tmp = nullptr;
-    rc = dalloc(h, &tmp, tb);
-    h->sort_tmp = tmp;
-  }
+  h->cs_maxt = (uint32_t)((P.stg_cap * (uint64_t)world + CS_TILE - 1) / CS_TILE);
+  ALLOC(h->cs_ghist, CS_MAXPASS * 256);
+  ALLOC(h->cs_ctr, CS_MAXPASS);
+  ALLOC(h->cs_stat, (size_t)CS_MAXPASS * h->cs_maxt * 256);
   ALLOC(h->d_blx, 2);
   ALLOC(P.wlast, h->GC / 32);
   ALLOC(P.in_cnt, N);
@@ -785,6 +779,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   }
   ALLOC(P.ih, NL * IHCAP);
   ALLOC(P.ih_head, N);
+  ALLOC(P.dbg_send, 2ull * N);
+  ALLOC(P.dbg_log, 256 * 8);
   ALLOC(P.rec_hdr, P.rcap);
   ALLOC(P.rec_len, P.rcap);
   ALLOC(P.rec_body, P.bcap);
@@ -858,6 +854,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.dbg_send, 0, (size_t)N * 16, s);
+  (void)hipMemsetAsync(P.dbg_log, 0, 256 * 8 * 4, s);
+  {
+    const char* w = std::getenv("SWIMHIP_DEBUG_WATCH");
+    P.dbg_watch = w ? (uint32_t)std::strtoul(w, nullptr, 10) : NONE;
+  }
   hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
                      NONE);
   {  // every started member of this shard starts with others = n0 - 1; n0 members alive
@@ -1350,6 +1352,21 @@ int swim_debug_member_state(swim_handle* h, uint32_t* out6n, uint32_t n) {
   for (int k = 0; k < 6; ++k)
     HIPC(h, hipMemcpyAsync(out6n + (size_t)k * n, src[k], (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+int swim_debug_sends(swim_handle* h, uint64_t* out2n, uint32_t n) {
+  if (!h || !out2n || n != h->N) return SWIM_EINVAL;
+  HIPC(h, hipMemcpyAsync(out2n, h->base.dbg_send, (size_t)n * 16, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (h->base.dbg_watch != NONE) {  // the watched member's per-round log, to stderr
+    std::vector<uint32_t> L(256 * 8);
+    HIPC(h, hipMemcpy(L.data(), h->base.dbg_log, L.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < 256; ++k)
+      if (L[8 * k] || L[8 * k + 3])
+        std::fprintf(stderr, "gpu watch r=%u win=%u alive=%u np=%u peers=%d,%d,%d supp=%u\n", L[8 * k], L[8 * k + 1],
+                     L[8 * k + 2], L[8 * k + 3], (int)L[8 * k + 4], (int)L[8 * k + 5], (int)L[8 * k + 6], L[8 * k + 7]);
+  }
   return SWIM_OK;
 }
 

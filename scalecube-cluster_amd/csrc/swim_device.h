@@ -237,6 +237,9 @@ struct KP {
   uint32_t* ack_ref;    // [2N] requester side: record index of the SYNC_ACK of remote request q
   // GossipState.infectedFrom (GossipState.java:17, GossipProtocolImpl.java:181,248), DESIGN.md §3.9
   uint32_t hzn;        // rounds a delivery can still suppress a send: gossipPeriodsToSpread(N) + 1
+  unsigned long long* dbg_send;  // [2N] debug: per sender, GossipRequests to alive peers before / by infectedFrom
+  uint32_t dbg_watch;            // debug: member whose per-round sends go to dbg_log (NONE: off)
+  uint32_t* dbg_log;             // [256][8] round, window bits, alive peers, peers, peer ids x3, suppressed
   uint4* ih;           // [nloc][IHCAP] in-history ring: {sender, round, record or NONE, 0}
   uint32_t* ih_head;   // [N] entries ever appended
   uint4* rec_hdr;      // [RCAP] delivery records: {deliverer, owner (receiver), round, body offset}

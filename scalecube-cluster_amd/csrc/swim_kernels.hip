@@ -18,6 +18,12 @@
 
 namespace swim {
 
+// A run whose buffers overflowed is dead (swim_sync reports SWIM_EOVERFLOW): every later kernel
+// of it returns at once, so nothing runs on state an overflow left inconsistent (an N x K subject
+// without a column, a wrapped ring) and the host never has to wait for a count mid-period.
+#define SWIM_GUARD(P) \
+  if ((P).ctl->overflow) return
+
 constexpr int MAXF = 32;       // max gossipFanout handled on device
 constexpr int MAXK = 16;       // max pingReqMembers handled on device
 constexpr int BUCKET_MAX = 2048;  // SYNC requests one member can merge in one period
@@ -30,6 +36,7 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
 }
 
 __global__ void k_finalize(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.row0 + P.nloc) {
     const int32_t d = P.cnt_delta[i];
@@ -51,6 +58,7 @@ __global__ void k_finalize(KP P) {
 // the transport, ClusterImpl.java:376-388): the same as a crash. Leaves are rare, so each stopped
 // member's row is walked by one thread.
 __global__ void k_leave_stop(KP P) {
+  SWIM_GUARD(P);
   const uint32_t c = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P.row0 + P.nloc || !P.stopf[c]) return;
   P.stopf[c] = 0;
@@ -157,48 +165,311 @@ __global__ void k_stage_keys(const uint4* ents, uint32_t n, uint32_t out_off, un
   }
 }
 
-// Step 2: the n sorted gossips get ids gcount + i (every shard commits the same sorted batch, so
+// Step 2: sorted gossip i gets id gcount + i (every shard commits the same sorted batch, so
 // the ring stays replicated), runs of one subject are marked in runw, and the origin's shard
-// marks each gossip held with infectionPeriod = create_round.
-__global__ void k_gossip_commit(KP P, const unsigned long long* keys, const unsigned long long* vals, uint32_t n) {
-  const uint32_t g0 = P.ctl->gcount;
+// marks the gossip held with infectionPeriod = create_round.
+__device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t i, unsigned long long k,
+                                           unsigned long long v, bool start) {
   const uint32_t W32 = P.GC >> 5;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const unsigned long long k = keys[i], v = vals[i];
-    const uint32_t subject = (uint32_t)(k >> 32), record = (uint32_t)k;
-    const uint32_t origin = (uint32_t)(v >> 32), hash = (uint32_t)v;
-    const uint32_t id = g0 + i;
-    const uint32_t s = id & P.gmask;
-    // the live id range must stay below GC - 64 slots so bitmap words never alias across the
-    // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
-    if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
-    P.g_sr[s] = make_uint2(subject, record);
-    P.g_hash[s] = hash;
-    P.g_create[s] = P.create_round;
-    const bool start = i == 0 || (uint32_t)(keys[i - 1] >> 32) != subject;
-    if (start)
-      atomicOr(&P.runw[s >> 5], 1u << (s & 31u));
-    else
-      atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
-    // a reused word's stale maximum is older than any live creation round, so max() resets it
-    if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
-    // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
-    if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
-    if (is_local(P, origin)) {
-      P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
-      const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
-      if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
-      // newest/oldest infection round the origin holds in the word (same value for the batch)
-      P.mmax[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
-      if (old == 0u) P.mmin[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
-    }
+  const uint32_t subject = (uint32_t)(k >> 32), record = (uint32_t)k;
+  const uint32_t origin = (uint32_t)(v >> 32), hash = (uint32_t)v;
+  const uint32_t id = g0 + i;
+  const uint32_t s = id & P.gmask;
+  // the live id range must stay below GC - 64 slots so bitmap words never alias across the
+  // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
+  if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  P.g_sr[s] = make_uint2(subject, record);
+  P.g_hash[s] = hash;
+  P.g_create[s] = P.create_round;
+  if (start)
+    atomicOr(&P.runw[s >> 5], 1u << (s & 31u));
+  else
+    atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
+  // a reused word's stale maximum is older than any live creation round, so max() resets it
+  if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
+  // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
+  if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
+  if (is_local(P, origin)) {
+    P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
+    const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
+    if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
+    // newest/oldest infection round the origin holds in the word (same value for the batch)
+    P.mmax[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
+    if (old == 0u) P.mmin[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
   }
 }
 
-// after the commit of a phase: advance the id counter, empty the local stage
-__global__ void k_gossip_commit_fin(KP P, uint32_t n) {
+// A phase's commit, sized on the device: n = the staged count (world 1, read by every kernel
+// below, so the host never waits for it) or the gathered batch of every shard (n_host). The
+// gossips are ordered by key (subject << 32 | record): a subject's gossips take consecutive slots
+// with ascending records, which k_gossip_apply's subject runs rely on; ties (the same record from
+// several origins) take any order, as slots are unobservable.
+//   * n <= CS_SMALL (nearly every phase): k_commit alone, a bitonic sort in one workgroup's LDS;
+//   * larger (storm phases): a least-significant-digit radix sort over 8-bit digits across the
+//     chip: k_rs_hist (every pass's digit counts at once), one k_rs_pass per digit (tiles of
+//     CS_TILE keys, tile order from an atomic counter, each tile's digit offsets from its
+//     predecessors by decoupled look-back, stable ranks by wave ballots), k_rs_commit, k_rs_fin.
+//     The look-back status word carries its value (flag | count, one agent-scope atomic store and
+//     load), so no payload crosses workgroups inside a launch; spins are bounded (OV_BUG).
+// Every kernel reads n itself and returns at once when the batch is not its size class.
+#ifndef SWIM_CS_SMALL
+#define SWIM_CS_SMALL 4096
+#endif
+constexpr uint32_t CS_SMALL = SWIM_CS_SMALL;  // LDS sort capacity (tests build a variant with a tiny one)
+static_assert(CS_SMALL >= 1 && CS_SMALL <= 4096 && (CS_SMALL & (CS_SMALL - 1)) == 0, "CS_SMALL: a power of two <= 4096");
+constexpr uint32_t CS_THREADS = 1024;
+constexpr uint32_t CS_WAVES = CS_THREADS / 64u;
+constexpr uint32_t CS_PER = 4;  // keys per thread in a radix tile
+constexpr uint32_t CS_TILE = CS_THREADS * CS_PER;
+constexpr uint32_t CS_MAXPASS = 8;
+constexpr uint32_t CS_AGG = 0x40000000u, CS_INC = 0x80000000u, CS_CNT = 0x3FFFFFFFu;
+
+struct CSort {
+  unsigned long long *k0, *v0, *k1, *v1;  // ping-pong key / value buffers
+  uint32_t* ghist;  // [CS_MAXPASS][256] digit counts of the whole batch per pass
+  uint32_t* ctr;    // [CS_MAXPASS] tiles handed out per pass
+  uint32_t* stat;   // [CS_MAXPASS][maxt][256] look-back status: flag | count
+  uint32_t maxt, npass;
+};
+
+__device__ __forceinline__ uint32_t cs_n(const KP& P, const uint4* stg, uint32_t n_host) {
+  return stg ? min(P.ctl->stg_count, P.stg_cap) : n_host;
+}
+
+__device__ __forceinline__ uint32_t cs_block_scan(uint32_t v, uint32_t* total, uint32_t* lds) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63u) lds[w] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64u; ++k) {
+    const uint32_t t = lds[k];
+    if (k < w) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+  __shared__ unsigned long long s_key[CS_SMALL];
+  __shared__ uint32_t s_idx[CS_SMALL];
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n > CS_SMALL) {  // a storm phase: reset the radix sort's counters for this batch
+    const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
+    for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) C.ghist[i] = 0u;
+    if (t < CS_MAXPASS) C.ctr[t] = 0u;
+    for (uint32_t p = 0; p < C.npass; ++p)
+      for (uint32_t i = t; i < nt * 256u; i += CS_THREADS) C.stat[(size_t)p * C.maxt * 256u + i] = 0u;
+    return;
+  }
+  const uint32_t g0 = P.ctl->gcount;
+  uint32_t m = 1;
+  while (m < n) m <<= 1;
+  for (uint32_t i = t; i < m; i += CS_THREADS) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      if (stg) {
+        const uint4 e = stg[i];
+        k = ((unsigned long long)e.y << 32) | e.z;
+      } else {
+        k = C.k0[i];
+      }
+    }
+    s_key[i] = k;
+    s_idx[i] = i;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= m; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = t; i < m; i += CS_THREADS) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = s_key[i], b = s_key[l];
+          const uint32_t ia = s_idx[i], ib = s_idx[l];
+          const bool gt = a > b || (a == b && ia > ib);
+          if (gt == ((i & k) == 0)) {
+            s_key[i] = b;
+            s_key[l] = a;
+            s_idx[i] = ib;
+            s_idx[l] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (uint32_t i = t; i < n; i += CS_THREADS) {
+    unsigned long long v;
+    if (stg) {
+      const uint4 e = stg[s_idx[i]];
+      v = ((unsigned long long)e.x << 32) | e.w;
+    } else {
+      v = C.v0[s_idx[i]];
+    }
+    commit_one(P, g0, i, s_key[i], v, i == 0 || (s_key[i - 1] >> 32) != (s_key[i] >> 32));
+  }
+  __syncthreads();
+  if (t == 0) {
+    P.ctl->gcount = g0 + n;
+    if (stg) P.ctl->stg_count = 0u;
+  }
+}
+
+// every pass's digit counts (a tile per workgroup); the stage moves into (k0, v0)
+__global__ void __launch_bounds__(CS_THREADS) k_rs_hist(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+  __shared__ uint32_t s_h[CS_MAXPASS][256];
+  const uint32_t n = cs_n(P, stg, n_host), t = threadIdx.x;
+  const uint32_t base = blockIdx.x * CS_TILE;
+  if (n <= CS_SMALL || base >= n) return;
+  for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) (&s_h[0][0])[i] = 0u;
+  __syncthreads();
+  for (uint32_t q = 0; q < CS_PER; ++q) {
+    const uint32_t i = base + q * CS_THREADS + t;
+    if (i >= n) break;
+    unsigned long long k;
+    if (stg) {
+      const uint4 e = stg[i];
+      k = ((unsigned long long)e.y << 32) | e.z;
+      C.k0[i] = k;
+      C.v0[i] = ((unsigned long long)e.x << 32) | e.w;
+    } else {
+      k = C.k0[i];
+    }
+    for (uint32_t p = 0; p < C.npass; ++p) atomicAdd(&s_h[p][(uint32_t)(k >> (8u * p)) & 255u], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < C.npass * 256u; i += CS_THREADS) {
+    const uint32_t c = (&s_h[0][0])[i];
+    if (c) atomicAdd(&C.ghist[i], c);
+  }
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_rs_pass(KP P, const uint4* stg, uint32_t n_host, CSort C, uint32_t p,
+                                                        const unsigned long long* sk, const unsigned long long* sv,
+                                                        unsigned long long* dk, unsigned long long* dv) {
+  __shared__ uint32_t s_h[256], s_off[256], s_cnt[CS_WAVES][256], s_lds[CS_WAVES];
+  __shared__ uint32_t s_tile;
+  const uint32_t n = cs_n(P, stg, n_host), t = threadIdx.x;
+  if (n <= CS_SMALL) return;
+  if (t == 0) s_tile = atomicAdd(&C.ctr[p], 1u);  // tiles in start order: predecessors are running
+  if (t < 256u) s_h[t] = 0u;
+  __syncthreads();
+  const uint32_t tile = s_tile, base = tile * CS_TILE;
+  if (base >= n) return;  // uniform
+  const uint32_t sh = 8u * p;
+  unsigned long long key[CS_PER];
+  uint32_t dg[CS_PER];
+#pragma unroll
+  for (uint32_t q = 0; q < CS_PER; ++q) {
+    const uint32_t i = base + q * CS_THREADS + t;
+    key[q] = i < n ? sk[i] : 0ull;
+    dg[q] = (uint32_t)(key[q] >> sh) & 255u;
+    if (i < n) atomicAdd(&s_h[dg[q]], 1u);
+  }
+  __syncthreads();
+  // digit t: this tile's count, published at once; then the keys of digit t in earlier tiles
+  uint32_t excl = 0;
+  uint32_t* st = C.stat + (size_t)p * C.maxt * 256u;
+  if (t < 256u) {
+    const uint32_t own = s_h[t];
+    __hip_atomic_store(&st[(size_t)tile * 256u + t], (tile == 0 ? CS_INC : CS_AGG) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (tile > 0) {
+      uint32_t j = tile - 1u, spins = 0;
+      for (;;) {
+        const uint32_t v = __hip_atomic_load(&st[(size_t)j * 256u + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(v & (CS_AGG | CS_INC))) {
+          if (++spins > (1u << 22)) {  // a predecessor never published: fail loudly, never hang
+            atomicOr(&P.ctl->overflow, OV_BUG);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += v & CS_CNT;
+        if ((v & CS_INC) || j == 0u) break;
+        --j;
+      }
+      __hip_atomic_store(&st[(size_t)tile * 256u + t], CS_INC | (excl + own), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // + keys of smaller digits in the whole batch
+  uint32_t all;
+  const uint32_t gpre = cs_block_scan(t < 256u ? C.ghist[p * 256u + t] : 0u, &all, s_lds);
+  if (t < 256u) s_off[t] = gpre + excl;
+  __syncthreads();
+  const uint32_t lane = t & 63u, w = t >> 6;
+#pragma unroll
+  for (uint32_t q = 0; q < CS_PER; ++q) {
+    const uint32_t i = base + q * CS_THREADS + t;
+    const bool ok = i < n;
+    const uint32_t d = dg[q];
+    // lanes of this wave with the same digit (8 ballots), and this lane's rank among them
+    unsigned long long same = __ballot(ok);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 8u; ++bit) {
+      const unsigned long long bb = __ballot(ok && ((d >> bit) & 1u));
+      same &= ((d >> bit) & 1u) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    for (uint32_t x = t; x < CS_WAVES * 256u; x += CS_THREADS) (&s_cnt[0][0])[x] = 0u;
+    __syncthreads();
+    if (ok && rank == 0u) s_cnt[w][d] = (uint32_t)__popcll(same);
+    __syncthreads();
+    if (ok) {
+      uint32_t pos = s_off[d] + rank;
+      for (uint32_t y = 0; y < w; ++y) pos += s_cnt[y][d];
+      dk[pos] = key[q];
+      dv[pos] = sv[i];
+    }
+    __syncthreads();
+    if (t < 256u) {
+      uint32_t add = 0;
+      for (uint32_t y = 0; y < CS_WAVES; ++y) add += s_cnt[y][t];
+      s_off[t] += add;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rs_commit(KP P, const uint4* stg, uint32_t n_host,
+                                                   const unsigned long long* k, const unsigned long long* v) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n <= CS_SMALL) return;
+  const uint32_t g0 = P.ctl->gcount;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    commit_one(P, g0, i, k[i], v[i], i == 0 || (k[i - 1] >> 32) != (k[i] >> 32));
+}
+
+__global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n <= CS_SMALL) return;
   P.ctl->gcount += n;
-  P.ctl->stg_count = 0u;
+  if (stg) P.ctl->stg_count = 0u;
+}
+
+// Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
+__global__ void __launch_bounds__(CS_THREADS) k_excl_scan(const uint32_t* in, uint32_t* out, uint32_t n) {
+  __shared__ uint32_t s_lds4[CS_WAVES];
+  const uint32_t per = (n + CS_THREADS - 1u) / CS_THREADS;
+  const uint32_t a = min(n, threadIdx.x * per), e = min(n, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < e; ++i) sum += in[i];
+  uint32_t tot;
+  uint32_t run = cs_block_scan(sum, &tot, s_lds4);
+  for (uint32_t i = a; i < e; ++i) {
+    const uint32_t v = in[i];
+    out[i] = run;
+    run += v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -286,6 +557,7 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
 // (the only way a subject's record first leaves the baseline: every later change — gossip,
 // SYNC, timeout, refutation — concerns a subject some record already changed) needs a column.
 __global__ void __launch_bounds__(256) k_fd_track(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
     const Probe pr = fd_probe(P, i, false);
@@ -297,6 +569,7 @@ __global__ void __launch_bounds__(256) k_fd_track(KP P) {
 // One thread per requested subject: the next free column (pre-filled with BASELINE cells), its
 // presence materialised (every alive observer but itself holds it), no deadline.
 __global__ void k_track_alloc(KP P) {
+  SWIM_GUARD(P);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= P.N || !P.track_req[j]) return;
   P.track_req[j] = 0;
@@ -313,6 +586,7 @@ __global__ void k_track_alloc(KP P) {
 
 // the allocated columns in subject order (SYNC merges assign gossip sequence numbers in it)
 __global__ void __launch_bounds__(256) k_colorder(KP P) {
+  SWIM_GUARD(P);
   const uint32_t n = P.ctl->ncols < P.W ? P.ctl->ncols : P.W;
   for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
     const uint32_t sj = P.colsubj[c];
@@ -331,6 +605,7 @@ __global__ void k_track_one(KP P, uint32_t j) {
 // Phase 0: failure detector, one thread per observer.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_fd(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t probes = 0, direct = 0, preq = 0, sev = 0, aev = 0, dev = 0, created = 0;
   Tally T;
@@ -516,6 +791,14 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
   __shared__ uint32_t s_lo, s_hi, s_blo, s_bhi, s_first;
   __shared__ uint32_t s_part[16];
   Ctl* c = P.ctl;
+  if (c->overflow) {  // the run has failed (reported at the next swim_sync): list nothing, touch nothing
+    if (threadIdx.x == 0) {
+      c->n_act = 0;
+      c->n_alist = c->n_inov = c->sp_cnt = c->rp_cnt = c->pw_used = 0;
+      c->scan_lo = c->scan_hi = c->gcount;
+    }
+    return;
+  }
   if (threadIdx.x == 0) s_first = NONE;
   __syncthreads();
   {  // the first word (from glo) that may still be held: wlast bounds every slot's infection round
@@ -651,6 +934,7 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
@@ -956,6 +1240,15 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   if (mine && lane == 0) P.npeers[m] = reg ? np : 0u;
   add_stat(P, ST_G_SCANNED, (any && lane == 0) ? n_act : 0u);
   add_stat(P, ST_GOSSIP_SENDS, (reg && lane == 0) ? winbits * alive_peers : 0u);
+  if (reg && lane == 0) P.dbg_send[2 * m] += (unsigned long long)winbits * alive_peers;
+  if (m == P.dbg_watch && lane == 0) {
+    uint32_t* L = P.dbg_log + (r & 255u) * 8u;
+    L[0] = r;
+    L[1] = reg ? winbits : 0u;
+    L[2] = reg ? alive_peers : 0u;
+    L[3] = np;
+    for (uint32_t q = 0; q < 3u; ++q) L[4 + q] = q < np ? s_peers[w][q] : NONE;
+  }
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
 }
@@ -980,6 +1273,7 @@ __device__ __forceinline__ uint32_t own_window(const KP& P, uint32_t m, uint32_t
 // the pair's pw slot, k_gossip_pairprune clears the recorded gossips; k_gossip_pull (or the shard
 // exchange) then reads pw instead of wb/hb. Work is split in PCHUNK-position pieces, one wave each.
 __global__ void __launch_bounds__(256) k_gossip_pairfill(KP P) {
+  SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
@@ -994,6 +1288,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairfill(KP P) {
 }
 
 __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
+  SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
@@ -1024,7 +1319,11 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t);
       if (supp) removed += (uint32_t)__popc(atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
-    if (route(P, sp.y) != NONE) removed_alive += removed;  // the send counter covers alive peers only
+    if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
+      removed_alive += removed;
+      if (removed) atomicAdd(&P.dbg_send[2 * sp.x + 1], (unsigned long long)removed);
+      if (removed && sp.x == P.dbg_watch) atomicAdd(&P.dbg_log[(P.round & 255u) * 8u + 7u], removed);
+    }
   }
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
   add_stat(P, ST_IF_PAIRS, (blockIdx.x == 0 && threadIdx.x == 0) ? n : 0u);
@@ -1063,6 +1362,7 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
 // position of this round's active list (kept in act_ring for the record's lifetime). Runs before
 // k_gossip_apply changes any holdings; PCHUNK positions per wave.
 __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
+  SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->rp_cnt < P.spcap ? P.ctl->rp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
@@ -1082,6 +1382,7 @@ __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
 // of its own within the horizon (may_select on p's post-selection cursor) gets a record, which
 // k_gossip_record fills after k_gossip_pull (GossipState.addToInfected, GPI:181).
 __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
+  SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
@@ -1170,6 +1471,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
 #define SWIM_PULL_WAVES 1
 #endif
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
@@ -1396,6 +1698,7 @@ static_assert(4 * (2 * HCAP + SPILL_CAP + PRES_WORDS + 17) <= 160 * 1024, "k_gos
 // goes to the global inbox instead (consistently for the whole round) and onto an LDS list.
 // Then one updateMembership per subject.
 __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_key[HCAP];
   __shared__ uint32_t s_val[HCAP];
   __shared__ uint32_t s_spl[SPILL_CAP];
@@ -1624,6 +1927,7 @@ __device__ __forceinline__ bool xrec_locate(const KP& P, const uint32_t* cnt, ui
 
 // (1) registrations [sender, receiver], destination shards in rank order
 __global__ void k_gossip_pack_pairs(KP P, uint32_t n_rec) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t dst, i;
   if (g < n_rec && xrec_locate(P, P.ctl->xg_cnt, g, &dst, &i)) {
@@ -1648,6 +1952,7 @@ __device__ __forceinline__ void scan4_256(const uint32_t v[4], uint32_t out[4], 
 // (2) receiver shard: keep the received pairs, compute each pair's need bitmap (kept for the
 // pull, and sent back), its per-word prefix counts and its total
 __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uint32_t nneed) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const uint32_t W32 = P.GC >> 5;
@@ -1695,6 +2000,7 @@ __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uin
 
 // (3a) sender shard: words each of its pairs must ship (the need bitmaps came back in send order)
 __global__ void k_gossip_wcount(KP P, uint32_t n_pairs, uint32_t nneed) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_pairs) {
     uint32_t c = 0;
@@ -1705,6 +2011,7 @@ __global__ void k_gossip_wcount(KP P, uint32_t n_pairs, uint32_t nneed) {
 
 // (3b) the needed window words of each pair, in need-bit order, at woff[g]
 __global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pairs, uint32_t nneed) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
   const uint32_t w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const uint32_t W32 = P.GC >> 5;
@@ -1743,6 +2050,7 @@ __global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pai
 
 // received sparse windows join their receivers' sender lists
 __global__ void k_gossip_unpack(KP P, uint32_t n_pairs) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_pairs) register_sender(P, P.rpairs[2 * g + 1], XREC | g);
 }
@@ -1757,6 +2065,7 @@ __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint3
 
 // SYNC request records [q, receiver, requester's table at phase start]
 __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
+  SWIM_GUARD(P);
   const uint32_t N = P.N;
   for (uint32_t g = blockIdx.x; g < n_rec; g += gridDim.x) {
     uint32_t dst, i;
@@ -1774,6 +2083,7 @@ __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
 
 // received SYNC requests join their receivers' buckets (k_scan / k_sync_scatter_remote)
 __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
@@ -1783,6 +2093,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
 }
 
 __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
@@ -1793,6 +2104,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
 
 // requester side: where the SYNC_ACK of remote request q landed
 __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
+  SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.N + 2u)]] = g;
 }
@@ -1836,6 +2148,7 @@ __global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
 // Suspicion timeouts: stream due subject columns of the deadline matrix.
 // ---------------------------------------------------------------------------------------
 __global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
+  SWIM_GUARD(P);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < ncells(P) && P.colmin[j] <= P.period) {
     const uint32_t idx = atomicAdd(&P.ctl->due_count, 1u);
@@ -1866,6 +2179,7 @@ __device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t
 // chip), 16 B per thread; each piece folds the deadlines it leaves standing into colmin.
 constexpr uint32_t SWEEP_CHUNK = 4096;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_min[4];
   Tally T;
   uint32_t fired = 0, cells = 0;
@@ -1947,6 +2261,7 @@ __device__ uint32_t select_sync_address(const KP& P, uint32_t i) {
 }
 
 __global__ void k_sync_select(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
   if (i < P.row0 + P.nloc) {
@@ -1997,6 +2312,7 @@ __global__ void k_sync_select(KP P) {
 // merge only the first SYNC_ACK to come back (take(1), :244-247), canonically the lowest seed address
 // whose round trip is delivered (jwin). Thread per member; launched only when some member joins.
 __global__ void k_join_select(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
   if (i < P.N && P.joining[i] && P.alive[i]) {
@@ -2030,6 +2346,7 @@ __global__ void k_join_select(KP P) {
 // bucket entries are 4 * sender + kind (kind 2 = initial SYNC), so a receiver's requests sort in
 // (sender, kind) order
 __global__ void k_join_scatter(KP P) {
+  SWIM_GUARD(P);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.N && P.joining[i] && P.alive[i] && P.jslot[i] != NONE && P.jslot[i] < P.scap) {
     const uint32_t nseeds = P.n_seeds < P.N ? P.n_seeds : P.N, own = addr_of(P, i);
@@ -2043,6 +2360,7 @@ __global__ void k_join_scatter(KP P) {
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:457-461): payload = sender's table at phase start.
 __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
+  SWIM_GUARD(P);
   uint32_t n = P.ctl->stage_count;
   if (n > P.scap) n = P.scap;
   const uint32_t W = ncells(P), nv = (P.W & 3u) ? 0u : W / 4u;  // a row = the first ncells cells
@@ -2058,6 +2376,7 @@ __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
 
 // exclusive scan of recv_count -> recv_off (single workgroup of 1024)
 __global__ void __launch_bounds__(1024) k_scan(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_part[1024];
   const uint32_t N = P.N;
   const uint32_t per = (N + 1023u) / 1024u;
@@ -2083,6 +2402,7 @@ __global__ void __launch_bounds__(1024) k_scan(KP P) {
 }
 
 __global__ void k_sync_scatter(KP P) {
+  SWIM_GUARD(P);
   const uint32_t q = 2u * P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (q < 2u * (P.row0 + P.nloc) && P.req_stage[q] != NONE && P.req_stage[q] != REMOTE) {
     const uint32_t to = P.req_to[q];
@@ -2174,6 +2494,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 // onSync (MembershipProtocolImpl.java:352-373) at receiver j = blockIdx, requests in
 // (sender, kind) order; each SYNC_ACK payload is j's table right after that request's merge.
 __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
   const uint32_t j = P.row0 + blockIdx.x;
@@ -2238,6 +2559,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
 
 // onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
 __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
+  SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
   const uint32_t i = P.row0 + blockIdx.x;
   if (i >= P.row0 + P.nloc) return;

@@ -175,6 +175,7 @@ SWIM_ONLY = [
     ("swim_kat_philox4", _I, [_U64, _U32, _pU32, _pU32, _U64]),
     ("swim_debug_holdings", _I, [_P, _U32, _pU32, _pU32, _U32, _pU32]),
     ("swim_debug_member_state", _I, [_P, _pU32, _U32]),
+    ("swim_debug_sends", _I, [_P, _pU64, _U32]),
     ("swim_kernel_time", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double), _pU64]),
     ("swim_kernel_time_reset", _I, [_P, _I]),
     ("swim_shard_buffer_words", _I, [_P, _pU64, _pU64]),

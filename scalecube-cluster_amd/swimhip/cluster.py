@@ -265,6 +265,12 @@ class SwimCluster:
         names = ["fd_epoch", "fd_cursor", "g_epoch", "g_cursor", "gossip_seq", "others"]
         return {k: out[i * self.n:(i + 1) * self.n] for i, k in enumerate(names)}
 
+    def debug_sends(self):
+        """Per sender (debug): cumulative GossipRequests to alive peers before infectedFrom, and suppressed."""
+        out = np.zeros(2 * self.n, dtype=np.uint64)
+        self._call("debug_sends", self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), self.n)
+        return out[0::2], out[1::2]
+
     # -- bench helpers (HIP library only) ---------------------------------------------------
     KERNEL_CLASSES = ["k_fd", "k_gossip_pull", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
                       "k_sync_snapshot", "bookkeeping", "k_gossip_select", "k_gossip_inhist", "k_gossip_pairwin",

@@ -179,6 +179,33 @@ print("SPILLS", spills)
 """
 
 
+def _run_variant(name, script):
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib = os.path.join(repo, "variants", name)
+    assert os.path.exists(lib), "variant not built: run __graft_entry__.build()"
+    paths = [here, repo, os.path.join(repo, "oracle"), os.path.join(repo, "scalecube-cluster_amd")]
+    env = dict(os.environ, SWIMHIP_LIB=lib)
+    out = subprocess.run([sys.executable, "-c", script.format(paths=paths)], env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    return out.stdout
+
+
+def test_commit_radix_path_parity():
+    """Phases that stage more gossips than k_commit's LDS bitonic sort holds (4,096) go through the
+    chip-wide radix sort (k_rs_hist, k_rs_pass with decoupled look-back, k_rs_commit). At the
+    parity sizes only storm phases get there, so a variant built with a 32-gossip LDS sort
+    (-DSWIM_CS_SMALL=32) runs the churn scenario and the C3 storm at N = 1,024 through it: bit-exact
+    with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable)."""
+    out = _run_variant("libswimhip_cs32.so", _SPILL_SCRIPT)
+    assert "SPILLS" in out
+
+
 def test_apply_spill_path_parity():
     """k_gossip_apply's overflow paths (a subject that finds no LDS hash slot within HPROBE probes
     goes through the global inbox and the LDS spill list; the summary walk without compaction when
