@@ -59,6 +59,10 @@ WORKLOADS = {
     "c5s": dict(desc="C5 geometry at 262,144 members: N x K tracked-subject views (K = 256), LAN defaults, 256 "
                      "simultaneous crashes",
                 n=1 << 18, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
+    # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows
+    "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
+                    "0.1% simultaneous crash",
+               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 19, scap=4096),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }

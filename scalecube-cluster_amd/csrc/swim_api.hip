@@ -1378,8 +1378,15 @@ int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv
   const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
   const uint64_t rows = (uint64_t)h->scap * (h->N + 2ull);
   const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2;  // commits carry the liveness maxima too
-  *send_words = std::max({win, rows, stg});
-  *recv_words = std::max({(uint64_t)(h->N - nloc) * h->base.f * (2 + W32), rows, stg * h->world});
+  // The window bounds assume every pair ships every active word; the need bitmaps ship only the
+  // words a receiver lacks something in, far fewer (k_gossip_need), so both buffers are capped at
+  // 2^31 words (8 GiB): C4's shards (32,768 rows of 262,144) would otherwise reserve ~90 GB for a
+  // worst case that never occurs. A round that would exceed the cap fails loudly on every rank
+  // (the sender checks its packed volume; swimhip/sharded.py checks every rank's receive volume).
+  const uint64_t cap = 1ull << 31;
+  *send_words = std::min(cap, std::max({win, rows, stg}));
+  *recv_words = std::min(cap, std::max({(uint64_t)(h->N - nloc) * h->base.f * (2 + W32), rows, stg * h->world}));
+  if (rows > cap || stg * h->world > cap) return fail(h, SWIM_EINVAL, "shard buffers: SYNC rows or commits exceed 2^31 words");
   return SWIM_OK;
 }
 

@@ -725,42 +725,68 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* to
 //     that failed) raises OV_IFROM instead of silently diverging.
 // hzn = gossipPeriodsToSpread(N) + 1: a record made in round t can only suppress sends in rounds
 // t+1 .. t+1+spread, the last rounds the receiver can still have those gossips in its window.
-__device__ __forceinline__ bool may_select(const KP& P, uint32_t p, uint32_t s) {
+// 0: s is out of p's reach within the horizon; 1: within it; 2: near enough that the present
+// members ahead of it decide (pos / wrap: s's position in the shuffle the cursor will reach)
+__device__ __forceinline__ uint32_t may_select_pre(const KP& P, uint32_t p, uint32_t s, uint32_t* pos_out,
+                                                   bool* wrap_out) {
   const uint32_t others = P.cnt[p];
-  if (others < P.f + 64u) return true;  // small views: "select all" is never far away
+  if (others < P.f + 64u) return 1u;  // small views: "select all" is never far away
   const uint32_t N = P.N;
   const uint64_t kappa = (2ull * N + others) / (others + 1ull);  // >= 2 positions per present member
   const uint64_t reach = (uint64_t)(P.hzn + 1u) * P.f * kappa + 64u;
-  if (reach >= N) return true;
+  if (reach >= N) return 1u;
   const uint32_t half = perm_half_bits(N);
   const uint32_t ep = P.g_epoch[p], cur = P.g_cursor[p];
-  const PermKey k0 = perm_key(P.seed, K_GOSSIP_PERM, p, ep);
-  uint32_t pos = perm_inverse(s, N, half, k0);
+  uint32_t pos = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep));
   bool wrap = false;
-  PermKey k1;
   if (!(pos >= cur && pos - cur < reach)) {
-    if (cur + reach <= N) return false;
+    if (cur + reach <= N) return 0u;
     // the cursor may wrap into the next shuffle within the horizon
-    k1 = perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u);
-    pos = perm_inverse(s, N, half, k1);
-    if (pos >= cur + reach - N) return false;
+    pos = perm_inverse(s, N, half, perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u));
+    if (pos >= cur + reach - N) return 0u;
     wrap = true;
   }
-  // Exact refinement: selectGossipMembers takes the first f present members from the cursor each
-  // round, so s comes up once the present members ahead of it are used up. Members removed in
-  // the meantime only bring it closer: a quarter of margin (a misprediction raises OV_IFROM).
+  *pos_out = pos;
+  *wrap_out = wrap;
+  return 2u;
+}
+
+// Exact refinement: selectGossipMembers takes the first f present members from the cursor each
+// round, so s comes up once the present members ahead of it are used up. Members removed in
+// the meantime only bring it closer: a quarter of margin (a misprediction raises OV_IFROM).
+// `stride` threads starting at `first` share the count (a wave: 64; one thread: 1).
+__device__ __forceinline__ uint32_t may_select_ahead(const KP& P, uint32_t p, uint32_t pos, bool wrap, uint32_t first,
+                                                     uint32_t stride) {
+  const uint32_t N = P.N, half = perm_half_bits(N);
+  const uint32_t ep = P.g_epoch[p], cur = P.g_cursor[p];
+  const PermKey k0 = perm_key(P.seed, K_GOSSIP_PERM, p, ep);
   uint32_t ahead = 0;
   const uint32_t end0 = wrap ? N : pos;
-  for (uint32_t x = cur; x < end0; ++x) {
+  for (uint32_t x = cur + first; x < end0; x += stride) {
     const uint32_t m = perm_apply(x, N, half, k0);
     ahead += (m != p && cell_get(P, p, m) != 0u) ? 1u : 0u;
   }
-  if (wrap)
-    for (uint32_t x = 0; x < pos; ++x) {
+  if (wrap) {
+    const PermKey k1 = perm_key(P.seed, K_GOSSIP_PERM, p, ep + 1u);
+    for (uint32_t x = first; x < pos; x += stride) {
       const uint32_t m = perm_apply(x, N, half, k1);
       ahead += (m != p && cell_get(P, p, m) != 0u) ? 1u : 0u;
     }
+  }
+  return ahead;
+}
+
+__device__ __forceinline__ bool may_select_within(const KP& P, uint32_t ahead) {
   return ahead < (P.f * P.hzn * 5u) / 4u + 16u;
+}
+
+// one thread's decision (k_gossip_need)
+__device__ __forceinline__ bool may_select(const KP& P, uint32_t p, uint32_t s) {
+  uint32_t pos = 0;
+  bool wrap = false;
+  const uint32_t pre = may_select_pre(P, p, s, &pos, &wrap);
+  if (pre != 2u) return pre == 1u;
+  return may_select_within(P, may_select_ahead(P, p, pos, wrap, 0u, 1u));
 }
 
 __device__ __forceinline__ uint32_t bytes_sub(uint32_t r, uint32_t d);
@@ -1330,13 +1356,12 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
 }
 
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
-// position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull)
+// position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull).
+// (Drawing lazily at pruning time instead was measured slower: a record is pruned against
+// several times within its horizon, C2 5.7 vs 5.1 ms/period.)
 __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, uint32_t sid, uint32_t p, uint32_t k,
-                                                   uint32_t w_beg, uint32_t lo, uint32_t hi, uint32_t* wi_out) {
+                                                   uint32_t w_beg, uint32_t lo, uint32_t hi) {
   const uint32_t ea = P.act[k];
-  const uint32_t W32 = P.GC >> 5;
-  const uint32_t wi = w_beg + (ea & ACT_OFF_MASK);
-  *wi_out = wi;
   if (((ea >> 26) & 3u) == WC_NONE) return 0u;
   uint32_t v;
   if (sreg & XREC)
@@ -1346,6 +1371,7 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
   else
     v = own_window(P, sreg, k, w_beg, lo, hi);
   if (v && P.loss_mode == 1u) {
+    const uint32_t W32 = P.GC >> 5, wi = w_beg + (ea & ACT_OFF_MASK);
     uint32_t need = v;
     v = 0u;
     while (need) {
@@ -1371,9 +1397,8 @@ __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
     const uint4 rp = P.rp_list[u / nch];  // {in_list entry, receiver, record, sender id}
     const uint32_t off = P.rec_hdr[rp.z & (P.rcap - 1u)].w;
     const uint32_t k1 = min(n_act, (u % nch + 1u) * PCHUNK);
-    uint32_t wi;
     for (uint32_t k = (u % nch) * PCHUNK + lane; k < k1; k += 64u)
-      P.rec_body[(off + k) & (P.bcap - 1u)] = delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi, &wi);
+      P.rec_body[(off + k) & (P.bcap - 1u)] = delivered_word(P, rp.x, rp.w, rp.y, k, w_beg, lo, hi);
   }
 }
 
@@ -1432,7 +1457,19 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
     const bool ok_l = lane < cdeg && link_open(P, sid, p);
     const unsigned long long reach = __ballot(ok_l);
     uint32_t rec = NONE;
-    if (ok_l && may_select(P, p, sid)) {
+    // may_select per lane; the refinements (a count over up to ~10^3 shuffle positions) by the
+    // whole wave, one sender at a time, instead of one long serial loop per lane
+    uint32_t mpos = 0;
+    bool mwrap = false;
+    uint32_t ms = ok_l ? may_select_pre(P, p, sid, &mpos, &mwrap) : 0u;
+    for (unsigned long long need = __ballot(ms == 2u); need; need &= need - 1ull) {
+      const int q = __builtin_ctzll(need);
+      const uint32_t pq = __shfl(mpos, q, 64);
+      const bool wq = __shfl((uint32_t)mwrap, q, 64) != 0u;
+      const uint32_t ahead = wave_sum(may_select_ahead(P, p, pq, wq, lane, 64u));
+      if (lane == (uint32_t)q) ms = may_select_within(P, ahead) ? 1u : 0u;
+    }
+    if (ok_l && ms == 1u) {
       rec = atomicAdd(&P.ctl->rec_cnt, 1u);
       const uint32_t o = atomicAdd(&P.ctl->rp_cnt, 1u);
       const uint32_t body = atomicAdd(&P.ctl->body_cnt, n_act);
@@ -1746,8 +1783,12 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
         const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
         if (!nb16) continue;
-        uint4 v = q == 0 ? v0 : v1;
         const uint32_t rb = ((r + 1u) & 0xFFu) * 0x01010101u;
+        if (!((prior >> (16 * q)) & 0xFFFFu)) {  // nothing held in these 16 slots: bytes of slots not
+          dp[q] = make_uint4(rb, rb, rb, rb);   // held are never read, so no read-modify-write
+          continue;
+        }
+        uint4 v = q == 0 ? v0 : v1;
         const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
         const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
         v.x = (v.x & ~m0) | (rb & m0);
@@ -1849,9 +1890,10 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         if (bv[j]) {
           pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
           rv[j] = P.runw[wsv[j]];
+          // the infection rounds of a 16-slot half are read only when it keeps some (see process)
           const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
-          v0[j] = dp[0];
-          v1[j] = dp[1];
+          if ((bv[j] & 0xFFFFu) && (pv[j] & 0xFFFFu)) v0[j] = dp[0];
+          if ((bv[j] >> 16) && (pv[j] >> 16)) v1[j] = dp[1];
         }
       }
 #pragma unroll

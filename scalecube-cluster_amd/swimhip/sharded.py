@@ -79,6 +79,11 @@ class ShardedSwimCluster(SwimCluster):
             sc = allc[self.rank]
             rc = [allc[q][self.rank] for q in range(W)]
             si, ri = sum(sc), sum(rc)
+            # every rank checks every rank's volumes (same buffer sizes everywhere): all raise together
+            over = [r for r in range(W) if sum(allc[r]) > self._send.numel()
+                    or sum(allc[q][r] for q in range(W)) > self._recv.numel()]
+            if over:
+                raise SwimError(-75, f"shard exchange over the buffer capacity on rank(s) {over}")
             if max(max(row) for row in allc):
                 src, dst = self._send[:si], self._recv[:ri]
                 if self._gloo:
