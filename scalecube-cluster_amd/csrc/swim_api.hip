@@ -716,6 +716,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
   ALLOC(P.nsum, NL * NSUM);
+  ALLOC(P.lack, NL * NSUM);
+  ALLOC(P.lack_round, N);
   ALLOC(P.stg, P.stg_cap);
   ALLOC(P.xg_pend, 2ull * world * NL * c.gossip_fanout);
   ALLOC(P.xs_pend, 2ull * world * NL);
@@ -854,6 +856,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.lack_round, (size_t)N, NONE);
   (void)hipMemsetAsync(P.dbg_send, 0, (size_t)N * 16, s);
   (void)hipMemsetAsync(P.dbg_log, 0, 256 * 8 * 4, s);
   {

@@ -174,6 +174,9 @@ struct KP {
   uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select (act-indexed)
   uint32_t* nb;  // [N][GC/32] first receipts of the round found by k_gossip_pull (act-indexed)
   uint32_t* nsum;  // [N][NSUM] bit k: nb[k] != 0 this round (written for receivers with receipts)
+  uint32_t* lack;  // [N][NSUM] bit k: after its sweep the member lacks a live gossip of word k of
+                   // this round's list that someone may send (k_gossip_select); k_gossip_pull visits only those
+  uint32_t* lack_round;  // [N] the round `lack` was last written for the member (otherwise no bitmap)
   uint32_t* cnt;
   int32_t* cnt_delta;
   uint8_t* alive;

@@ -986,6 +986,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
     uint8_t* mminr = P.mmin + lrow(P, m) * W32;
     const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
+    const bool lack_ok = (n_act + 31u) / 32u <= NSUM;  // the list fits the bitmap (as nsum)
     // SEL_BATCH aligned quads of list entries per lane per step: one 16-B list load and (for a
     // quad of consecutive aligned words, the padded layout of k_gossip_prep) one 16-B holdings
     // load each, all issued together (bytes in flight). Words whose class the member's own age
@@ -1021,6 +1022,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         }
       }
       uint32_t mixm = 0;  // entries whose infection rounds must be read
+      uint32_t lackm = 0;  // entries (sent words) in which the member lacks a live gossip
 #pragma unroll 1
       for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
         // quad jq's values by select chains (no dynamically indexed register arrays: no scratch)
@@ -1044,7 +1046,8 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
         const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t held = k < n_act ? word & range_mask(wi << 5, lo, hi) : 0u;
+        const uint32_t live = k < n_act ? range_mask(wi << 5, lo, hi) : 0u;
+        const uint32_t held = word & live;
         uint32_t clear = 0, win = 0;
         if (held) {
           uint32_t wcm = wc, scm = sc;
@@ -1067,6 +1070,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           }
         }
         if (k < n_act && wc != WC_NONE) {
+          if ((held & ~clear) != live) lackm |= 1u << j;  // a sender may bring it something here
           // a globally ALL word's window is the member's holdings after the sweep, which receivers
           // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
           if (wc == WC_MIXED) {
@@ -1105,6 +1109,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         }
         const uint32_t clear = held & over_sweep;  // sweepGossips
         const uint32_t win = held & ~over_spread;
+        if (wc != WC_NONE && (held & ~clear) != range_mask(wi << 5, lo, hi)) lackm |= 1u << j;
         uint32_t oldest_kept = 0;
         const uint32_t kept = held & ~clear;
         if (clear && kept) {
@@ -1129,7 +1134,19 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           winbits += (uint32_t)__popc(win);
         }
       }
+      if (lack_ok) {  // positions k0 + 256 jq + 4 lane + i: eight lanes fill one bitmap word
+#pragma unroll
+        for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
+          uint32_t v = ((lackm >> (4u * jq)) & 0xFu) << (4u * (lane & 7u));
+          v |= __shfl_xor(v, 1, 64);
+          v |= __shfl_xor(v, 2, 64);
+          v |= __shfl_xor(v, 4, 64);
+          const uint32_t wq = (k0 + 256u * jq) / 32u + lane / 8u;
+          if ((lane & 7u) == 0u && 32u * wq < n_act) P.lack[lrow(P, m) * NSUM + wq] = v;
+        }
+      }
     }
+    if (lack_ok && lane == 0) P.lack_round[m] = r;
   }
   uint32_t np = 0;
   if (any) {
@@ -1526,6 +1543,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   if (deg && P.alive[p] && n_act) {  // a stopped transport loses every message
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
+    const uint32_t* lackr = (nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
     if (nsw <= NSUM)
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
@@ -1582,6 +1600,10 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
       // consecutive aligned words): the receiver's holdings, its receipts so far and each
       // sender's window words then come in 16-B loads; other quads fall back to per-word loads
       for (uint32_t kq = 4u * lane; kq < n_act; kq += 256u) {
+        // the receiver's own select pass marked the sent words it lacks something in: skip the
+        // rest without reading the list or the holdings (most of them once a storm has spread;
+        // compacting the marked quads first measured no faster: the visits are latency-bound)
+        if (lackr && !((lackr[kq >> 5] >> (kq & 31u)) & 0xFu)) continue;
         const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
         const uint32_t ea[4] = {a.x, a.y, a.z, a.w};
         const uint32_t o0 = a.x & ACT_OFF_MASK;
@@ -1681,7 +1703,8 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
             sbits |= 1u << ((kq + i) & 31u);
           }
         if (sbits && nsw <= NSUM) atomicOr(&sum[kq >> 5], sbits);
-      }
+            }
+
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
     const uint32_t total = wave_sum(receipts);

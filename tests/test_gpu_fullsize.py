@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import bench
-from swimhip import SwimCluster
+from swimhip import MembershipEvent, SwimCluster
 
 pytestmark = pytest.mark.gpu
 
@@ -66,3 +66,63 @@ def test_c3_fullsize_properties_and_determinism():
     assert (d_a, d_b) == (d_a2, d_b2)
     assert {k: st_b[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")} == \
            {k: st_b2[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")}
+
+
+def test_c2_convergence_tail_is_fd_driven():
+    """C2 (4,096 dense, LAN, 5 % loss, 1 % crash) leaves a few (observer, crashed subject) pairs
+    long after the suspicion timeout (65 periods). Why, under the reference's own rules: such an
+    observer missed every SUSPECT gossip about the subject (each message lost with 5 %), and once
+    every other member has removed it (MembershipProtocolImpl.onDeadMemberDetected, :571-587,
+    deletes the record; no tombstone) nobody gossips or SYNCs it any more (SyncData carries only
+    present records, :463-473; an absent cell never overrides). The straggler's record stays ALIVE
+    until its own round-robin FD reaches the subject (FailureDetectorImpl.selectPingMember,
+    :340-349: within two passes of a reshuffled list, <= 2N periods), then SUSPECT -> DEAD after
+    the suspicion timeout. Pinned: the GPU matches the oracle's digests and counters every 15
+    periods up to t0 + 75 and has the same stragglers (tests/golden/c2_tail_oracle.json, made by
+    make_c2_tail_fixture.py: the oracle needs ~15 min for it); then each straggler's record stays
+    ALIVE until at most one suspicion timeout before it is removed, and all are removed within
+    2N + 65 periods."""
+    import json
+    import os
+
+    import scenarios
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2_tail_oracle.json")
+    if not os.path.exists(path) or os.path.getsize(path) == 0:
+        pytest.fail("tests/golden/c2_tail_oracle.json missing: run tests/golden/make_c2_tail_fixture.py")
+    fx = json.load(open(path))
+    w = bench.WORKLOADS["c2"]
+    n = w["n"]
+    a = bench.make_cluster("c2", 0, seed=fx["seed"], event_capacity=1 << 20)
+    a.step(fx["t0"])
+    crashed = bench.inject_faults(a, "c2", fx["t0"], fx["seed"], n=n)
+    assert [int(x) for x in crashed] == fx["crashed"]
+    for cp in fx["checkpoints"]:
+        a.step(cp["period"] - a.stats()["period"])
+        assert list(a.digest()) == cp["digest"], cp["period"]
+        st = a.stats()
+        assert {k: int(st[k]) for k in scenarios.PARITY_KEYS} == cp["stats"], cp["period"]
+        print(f"period {cp['period']}: digests and counters equal the oracle's", flush=True)
+    pairs = [(i, s) for i, s, _ in fx["stragglers"]]
+    assert 0 < len(pairs) == a.stats()["not_converged"] < 16
+    for i, s, rec in fx["stragglers"]:
+        # ALIVE (at the subject's last incarnation): no SUSPECT record ever reached the observer
+        assert int(a.view(i)[s]) == rec and (rec & 3) == 1, (i, s, rec)
+    susp_seen = {}
+    t = fx["checkpoints"][-1]["period"] - fx["t0"]
+    limit = 2 * n + 65 + 10
+    while a.stats()["not_converged"] and t < limit:
+        a.step(5)
+        t += 5
+        for i, s in pairs:
+            if (i, s) not in susp_seen and (int(a.view(i)[s]) & 3) == 2:
+                susp_seen[(i, s)] = t
+        if t % 500 == 0:
+            print(f"t0+{t}: not_converged={a.stats()['not_converged']}", flush=True)
+    assert a.stats()["not_converged"] == 0, f"stragglers left after {t} periods"
+    ev = {(e.observer, e.member): e.period - fx["t0"] for e in a.events(1 << 22) if e.type == MembershipEvent.REMOVED}
+    for i, s in pairs:
+        removed = ev[(i, s)]
+        first_suspect = susp_seen.get((i, s), removed)
+        print(f"straggler ({i}, {s}): SUSPECT by its own FD at t0+{first_suspect}, removed at t0+{removed}", flush=True)
+        assert removed - first_suspect <= 65 + 5, (i, s, first_suspect, removed)

@@ -9,7 +9,7 @@ mkdir -p $out
 echo "start $(date +%T)" > $out/status.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 \
   && echo "smoke ok $(date +%T)" >> $out/status.log \
-  && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+  && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS} \
        > $out/pytest_gpu.log 2>&1 \
   && echo "pytest ok $(date +%T)" >> $out/status.log \
   && timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $out/bench.json 2> $out/bench.err \
