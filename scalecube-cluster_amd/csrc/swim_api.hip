@@ -887,6 +887,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
 int swim_destroy(swim_handle* h) {
   if (!h) return SWIM_EINVAL;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+#ifdef SWIM_APPLY_PROF
+  {  // k_gossip_apply phase profile (wall clock at 100 MHz, summed over workgroups)
+    unsigned long long ph[4] = {0, 0, 0, 0};
+    if (hipMemcpy(ph, h->base.dbg_log, sizeof ph, hipMemcpyDeviceToHost) == hipSuccess)
+      std::fprintf(stderr, "apply phases (workgroup-ms): init %.1f compact %.1f items %.1f subjects %.1f\n",
+                   ph[0] / 1e5, ph[1] / 1e5, ph[2] / 1e5, ph[3] / 1e5);
+  }
+#endif
   free_all(h);
   delete h;
   return SWIM_OK;
@@ -1136,10 +1144,10 @@ int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n)
 
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
   if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
-  // cell-major storage: strided 2D copy of one observer column
+  // observer-major storage: the observer's row
+  const uint32_t* drow = h->base.dl + (size_t)(observer - h->base.row0) * h->base.W;
   if (!h->base.nxk) {
-    HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
-                             hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipMemcpyAsync(row, drow, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
     HIPC(h, hipStreamSynchronize(h->stream));
     return SWIM_OK;
   }
@@ -1148,8 +1156,7 @@ int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32
   if (rc) return rc;
   cells.resize(subj.size());
   if (!subj.empty())
-    HIPC(h, hipMemcpy2DAsync(cells.data(), 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4,
-                             subj.size(), hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipMemcpyAsync(cells.data(), drow, subj.size() * 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   std::fill(row, row + n, 0u);
   for (size_t c = 0; c < subj.size(); ++c) row[subj[c]] = cells[c];

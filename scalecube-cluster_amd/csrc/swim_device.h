@@ -163,7 +163,7 @@ struct KP {
   uint32_t* jwin;     // [N] the seed member whose SYNC_ACK the joiner merges (first round trip), or NONE
   // state
   uint32_t* view;
-  uint32_t* dl;
+  uint32_t* dl;  // [nloc observers][W cells] suspicion deadline + 1 (0 = none), observer-major
   uint32_t* colmin;
   uint32_t* inbox;
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
@@ -436,7 +436,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.refut++;
     return r2;
   }
-  uint32_t* dlp = P.dl + (size_t)col * P.nloc + lrow(P, obs);
+  uint32_t* dlp = P.dl + lrow(P, obs) * P.W + col;  // observer-major, like the view row
   if (r1 == SWIM_DEAD) {
     *dlp = 0u;
     *cellp = SWIM_ABSENT;
@@ -454,7 +454,9 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     if (*dlp == 0u) {
       const uint32_t dl = P.period + susp_periods(P, others_snap);
       *dlp = dl + 1u;
-      atomicMin(&P.colmin[col], dl);
+      // every observer scheduling in a round computes the same deadline: read first, so the hot
+      // column minimum takes one atomic per round instead of one per observer
+      if (P.colmin[col] > dl) atomicMin(&P.colmin[col], dl);
     }
     return spread ? r1 : 0u;
   }

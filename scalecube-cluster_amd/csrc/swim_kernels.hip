@@ -69,7 +69,7 @@ __global__ void k_leave_stop(KP P) {
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t j = subj_of(P, cc);
     if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
+    P.dl[lrow(P, c) * P.W + cc] = 0u;
   }
   P.alive[c] = 0;
   if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
@@ -114,7 +114,7 @@ __global__ void k_stop_addr(KP P, uint32_t c) {
 __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
   for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
     P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
-    P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
+    P.dl[lrow(P, x) * P.W + c] = 0u;
   }
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;
@@ -149,7 +149,7 @@ __global__ void k_crash(KP P, uint32_t c) {
   for (uint32_t cc = blockIdx.x * blockDim.x + threadIdx.x; cc < nc; cc += gridDim.x * blockDim.x) {
     const uint32_t j = subj_of(P, cc);
     if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
+    P.dl[lrow(P, c) * P.W + cc] = 0u;
   }
 }
 
@@ -964,6 +964,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
+  __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t m = P.row0 + blockIdx.x * 4u + w;
@@ -1059,6 +1060,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           }
           if (wcm == WC_MIXED || scm == WC_MIXED) {
             mixm |= 1u << j;
+            s_mw[w][j][lane] = make_uint2(e, word);  // for the pass below: no list or holdings re-read
             continue;
           }
           if (wcm == WC_ALL) win = held;
@@ -1082,20 +1084,37 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         }
         }
       }
+      // entries one at a time from the mask, the next one's infection rounds (32 B) loaded
+      // before the current one is evaluated: two reads in flight per lane
+      uint32_t jn = 0, en = 0;
+      uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+      if (mixm) {
+        jn = (uint32_t)__builtin_ctz(mixm);
+        en = s_mw[w][jn][lane].x;
+        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (en & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
+        n0 = dp[0];
+        n1 = dp[1];
+      }
       while (mixm) {
-        const uint32_t j = (uint32_t)__builtin_ctz(mixm);
+        const uint32_t j = jn;
         mixm &= mixm - 1u;
         const uint32_t k = k0 + 256u * (j >> 2) + 4u * lane + (j & 3u);
-        const uint32_t e = P.act[k];  // re-read (cache-resident) rather than index registers
+        const uint32_t e = en;
+        const uint4 d0 = n0, d1 = n1;
+        if (mixm) {
+          jn = (uint32_t)__builtin_ctz(mixm);
+          en = s_mw[w][jn][lane].x;
+          const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (en & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
+          n0 = dp[0];
+          n1 = dp[1];
+        }
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u;
         const uint32_t ws = wi & (W32 - 1u);
-        const uint32_t word = hbr[ws];
+        const uint32_t word = s_mw[w][j][lane].y;
         const uint32_t held = word & range_mask(wi << 5, lo, hi);
         // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
         ++hdw;
-        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)ws * 32u);
-        const uint4 d0 = dp[0], d1 = dp[1];
         const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
         // four ages per dword at once (byte-wise r - round, then 16-bit-lane threshold tests)
         uint32_t over_sweep = 0, over_spread = 0;
@@ -1770,6 +1789,17 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   const uint32_t W32 = P.GC >> 5;
   Tally T;
   uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0;
+#ifdef SWIM_APPLY_PROF
+  unsigned long long tp = wall_clock64();
+#define APPLY_MARK(q)                                                                      \
+  if (threadIdx.x == 0) {                                                                  \
+    const unsigned long long tn = wall_clock64();                                          \
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + (q), tn - tp);            \
+    tp = tn;                                                                               \
+  }
+#else
+#define APPLY_MARK(q)
+#endif
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
@@ -1785,6 +1815,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     if (pres)
       for (uint32_t t = threadIdx.x; t < (P.N + 31u) / 32u; t += blockDim.x) s_pres[t] = 0u;
     __syncthreads();
+    APPLY_MARK(0)
     // infection rounds, word liveness, and the lattice max per subject, over the words the
     // receipt summary lists (or every active word when the list is too long to summarize)
     const uint32_t nsw = (n_act + 31u) >> 5;
@@ -1886,6 +1917,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       }
       __syncthreads();
     }
+    APPLY_MARK(1)
     const uint32_t n_it = compact ? n_comp : n_items;
     for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * blockDim.x) {
       // four items per thread: their loads are issued together, stage by stage
@@ -1924,6 +1956,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         if (bv[j]) process(kv[j], wsv[j], bv[j], pv[j], rv[j], v0[j], v1[j]);
     }
     __syncthreads();
+    APPLY_MARK(2)
     const uint32_t snap = P.cnt[p];
     auto apply = [&](uint32_t subj, uint32_t r1) {
       ++nsubj;
@@ -1958,6 +1991,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
     nspills += threadIdx.x == 0 ? nsp : 0u;
     __syncthreads();  // the table is reused by the next receiver
+    APPLY_MARK(3)
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   add_stat(P, ST_APPLY_WORDS, nwords);
@@ -2250,27 +2284,25 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   uint32_t fired = 0, cells = 0;
   const uint32_t n = P.ctl->due_count;
   const uint32_t nch = (P.nloc + SWEEP_CHUNK - 1u) / SWEEP_CHUNK;
-  const bool vec = (P.nloc & 3u) == 0u;  // columns 16-B aligned
   for (uint32_t u = blockIdx.x; u < n * nch; u += gridDim.x) {
     const uint32_t j = P.due[u / nch];  // the cell; its subject is subj_of(j)
     const uint32_t c0 = (u % nch) * SWEEP_CHUNK, c1 = min(P.nloc, c0 + SWEEP_CHUNK);
-    uint32_t* col = P.dl + (size_t)j * P.nloc;
+    // the column is strided (observer-major rows, which the per-round writers stream): one 4-B
+    // load per observer, four in flight per thread
     uint32_t mn = NONE;
-    if (vec) {
-      for (uint32_t li = c0 + 4u * threadIdx.x; li < c1; li += 4u * blockDim.x) {
-        uint4 v = *reinterpret_cast<const uint4*>(col + li);
-        if ((v.x | v.y | v.z | v.w) == 0u) continue;
-        const uint4 w = make_uint4(sweep_cell(P, j, li, v.x, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 1u, v.y, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 2u, v.z, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 3u, v.w, &mn, &fired, T));
-        if (w.x != v.x || w.y != v.y || w.z != v.z || w.w != v.w) *reinterpret_cast<uint4*>(col + li) = w;
+    for (uint32_t l0 = c0 + threadIdx.x; l0 < c1; l0 += 4u * blockDim.x) {
+      uint32_t v[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q) {
+        const uint32_t li = l0 + q * blockDim.x;
+        v[q] = li < c1 ? P.dl[(size_t)li * P.W + j] : 0u;
       }
-    } else {
-      for (uint32_t li = c0 + threadIdx.x; li < c1; li += blockDim.x) {
-        const uint32_t v = col[li];
-        const uint32_t w = sweep_cell(P, j, li, v, &mn, &fired, T);
-        if (w != v) col[li] = w;
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q) {
+        const uint32_t li = l0 + q * blockDim.x;
+        if (!v[q]) continue;
+        const uint32_t w = sweep_cell(P, j, li, v[q], &mn, &fired, T);
+        if (w != v[q]) P.dl[(size_t)li * P.W + j] = w;
       }
     }
     cells += c1 - c0;
@@ -2693,11 +2725,13 @@ __global__ void k_digest(KP P, unsigned long long* out) {
     const uint32_t v = cell_get(P, row0 + li, j);
     if (v) a += fmix64(((uint64_t)row0 * N + x) * K + v);
   }
-  const size_t dtot = (size_t)nc * nloc;
+  const size_t dtot = (size_t)nloc * P.W;
   for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < dtot; x += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t d = P.dl[x];  // x = cell * nloc + local observer
+    const uint32_t c = (uint32_t)(x % P.W);  // x = local observer * W + cell
+    if (c >= nc) continue;
+    const uint32_t d = P.dl[x];
     if (d) {
-      const uint64_t subj = subj_of(P, (uint32_t)(x / nloc)), obs = row0 + x % nloc;
+      const uint64_t subj = subj_of(P, c), obs = row0 + x / P.W;
       b += fmix64((obs * N + subj) * K + d);
     }
   }
