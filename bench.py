@@ -41,6 +41,14 @@ WORKLOADS = {
     "c3": dict(desc="C3: 65,536 members, dense N x N views, LAN defaults, 10% simultaneous crash + 2-way "
                     "partition (16-member group) for 40 periods healed via SYNC",
                n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16, gcap=1 << 20, scap=8192),
+    # SURVEY §8(d) C3 variant: the partition outlasts the 85-period suspicion timeout, so both
+    # sides remove each other; the cut group rejoins through the seed addresses (ids 0..15) after
+    # the heal (MembershipProtocolTest.testLongNetworkPartitionNoOutboundThenRemoved, :844-918)
+    "c3long": dict(desc="C3 variant: 65,536 members, LAN defaults, seeds 0..15, 10% simultaneous crash + a "
+                        "16-member group partitioned for 120 periods (past the suspicion timeout), rejoining "
+                        "through the seeds",
+                   n=65536, preset="lan", loss=0.0, crash=0.10, part=120, part_group=16, gcap=1 << 20,
+                   scap=8192, seeds=16),
     "c3s": dict(desc="C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash",
                 n=65536, preset="lan", loss=0.0, crash=0.001, part=0, gcap=1 << 16),
     "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",
@@ -158,7 +166,10 @@ def make_cluster(workload, device, seed, event_capacity=0, sharded=False):
     w = WORKLOADS[workload]
     cls = ShardedSwimCluster if sharded else SwimCluster
     kw = {"tracked_subjects": w["tracked"]} if w.get("tracked") else {}
-    c = cls(preset_config(w["preset"]), w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
+    cfg = preset_config(w["preset"])
+    if w.get("seeds"):  # the first `seeds` member ids are the seed addresses
+        cfg = cfg.membership(lambda o: o.seedMembers(list(range(w["seeds"]))))
+    c = cls(cfg, w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
             event_capacity=event_capacity, sync_capacity=w.get("scap", 0), **kw)
     if w["loss"]:
         c.set_loss(w["loss"])

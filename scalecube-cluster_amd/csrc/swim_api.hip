@@ -1144,10 +1144,10 @@ int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n)
 
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
   if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
-  // observer-major storage: the observer's row
-  const uint32_t* drow = h->base.dl + (size_t)(observer - h->base.row0) * h->base.W;
+  // cell-major storage: strided 2D copy of one observer column
   if (!h->base.nxk) {
-    HIPC(h, hipMemcpyAsync(row, drow, (size_t)h->N * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
+                             hipMemcpyDeviceToHost, h->stream));
     HIPC(h, hipStreamSynchronize(h->stream));
     return SWIM_OK;
   }
@@ -1156,7 +1156,8 @@ int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32
   if (rc) return rc;
   cells.resize(subj.size());
   if (!subj.empty())
-    HIPC(h, hipMemcpyAsync(cells.data(), drow, subj.size() * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipMemcpy2DAsync(cells.data(), 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4,
+                             subj.size(), hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   std::fill(row, row + n, 0u);
   for (size_t c = 0; c < subj.size(); ++c) row[subj[c]] = cells[c];

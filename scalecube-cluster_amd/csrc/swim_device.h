@@ -163,7 +163,7 @@ struct KP {
   uint32_t* jwin;     // [N] the seed member whose SYNC_ACK the joiner merges (first round trip), or NONE
   // state
   uint32_t* view;
-  uint32_t* dl;  // [nloc observers][W cells] suspicion deadline + 1 (0 = none), observer-major
+  uint32_t* dl;  // [W cells][nloc observers] suspicion deadline + 1 (0 = none), subject-major
   uint32_t* colmin;
   uint32_t* inbox;
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
@@ -436,7 +436,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.refut++;
     return r2;
   }
-  uint32_t* dlp = P.dl + lrow(P, obs) * P.W + col;  // observer-major, like the view row
+  uint32_t* dlp = P.dl + (size_t)col * P.nloc + lrow(P, obs);  // subject-major: a due column streams
   if (r1 == SWIM_DEAD) {
     *dlp = 0u;
     *cellp = SWIM_ABSENT;

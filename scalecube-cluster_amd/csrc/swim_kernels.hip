@@ -69,7 +69,7 @@ __global__ void k_leave_stop(KP P) {
   for (uint32_t cc = 0; cc < nc; ++cc) {
     const uint32_t j = subj_of(P, cc);
     if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[lrow(P, c) * P.W + cc] = 0u;
+    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
   }
   P.alive[c] = 0;
   if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
@@ -114,7 +114,7 @@ __global__ void k_stop_addr(KP P, uint32_t c) {
 __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
   for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
     P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
-    P.dl[lrow(P, x) * P.W + c] = 0u;
+    P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
   }
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;
@@ -149,7 +149,7 @@ __global__ void k_crash(KP P, uint32_t c) {
   for (uint32_t cc = blockIdx.x * blockDim.x + threadIdx.x; cc < nc; cc += gridDim.x * blockDim.x) {
     const uint32_t j = subj_of(P, cc);
     if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
-    P.dl[lrow(P, c) * P.W + cc] = 0u;
+    P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
   }
 }
 
@@ -2284,25 +2284,27 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   uint32_t fired = 0, cells = 0;
   const uint32_t n = P.ctl->due_count;
   const uint32_t nch = (P.nloc + SWEEP_CHUNK - 1u) / SWEEP_CHUNK;
+  const bool vec = (P.nloc & 3u) == 0u;  // columns 16-B aligned
   for (uint32_t u = blockIdx.x; u < n * nch; u += gridDim.x) {
     const uint32_t j = P.due[u / nch];  // the cell; its subject is subj_of(j)
     const uint32_t c0 = (u % nch) * SWEEP_CHUNK, c1 = min(P.nloc, c0 + SWEEP_CHUNK);
-    // the column is strided (observer-major rows, which the per-round writers stream): one 4-B
-    // load per observer, four in flight per thread
+    uint32_t* col = P.dl + (size_t)j * P.nloc;
     uint32_t mn = NONE;
-    for (uint32_t l0 = c0 + threadIdx.x; l0 < c1; l0 += 4u * blockDim.x) {
-      uint32_t v[4];
-#pragma unroll
-      for (uint32_t q = 0; q < 4u; ++q) {
-        const uint32_t li = l0 + q * blockDim.x;
-        v[q] = li < c1 ? P.dl[(size_t)li * P.W + j] : 0u;
+    if (vec) {
+      for (uint32_t li = c0 + 4u * threadIdx.x; li < c1; li += 4u * blockDim.x) {
+        uint4 v = *reinterpret_cast<const uint4*>(col + li);
+        if ((v.x | v.y | v.z | v.w) == 0u) continue;
+        const uint4 w = make_uint4(sweep_cell(P, j, li, v.x, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 1u, v.y, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 2u, v.z, &mn, &fired, T),
+                                   sweep_cell(P, j, li + 3u, v.w, &mn, &fired, T));
+        if (w.x != v.x || w.y != v.y || w.z != v.z || w.w != v.w) *reinterpret_cast<uint4*>(col + li) = w;
       }
-#pragma unroll
-      for (uint32_t q = 0; q < 4u; ++q) {
-        const uint32_t li = l0 + q * blockDim.x;
-        if (!v[q]) continue;
-        const uint32_t w = sweep_cell(P, j, li, v[q], &mn, &fired, T);
-        if (w != v[q]) P.dl[(size_t)li * P.W + j] = w;
+    } else {
+      for (uint32_t li = c0 + threadIdx.x; li < c1; li += blockDim.x) {
+        const uint32_t v = col[li];
+        const uint32_t w = sweep_cell(P, j, li, v, &mn, &fired, T);
+        if (w != v) col[li] = w;
       }
     }
     cells += c1 - c0;
@@ -2725,13 +2727,11 @@ __global__ void k_digest(KP P, unsigned long long* out) {
     const uint32_t v = cell_get(P, row0 + li, j);
     if (v) a += fmix64(((uint64_t)row0 * N + x) * K + v);
   }
-  const size_t dtot = (size_t)nloc * P.W;
+  const size_t dtot = (size_t)nc * nloc;
   for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < dtot; x += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t c = (uint32_t)(x % P.W);  // x = local observer * W + cell
-    if (c >= nc) continue;
-    const uint32_t d = P.dl[x];
+    const uint32_t d = P.dl[x];  // x = cell * nloc + local observer
     if (d) {
-      const uint64_t subj = subj_of(P, c), obs = row0 + x / P.W;
+      const uint64_t subj = subj_of(P, (uint32_t)(x / nloc)), obs = row0 + x % nloc;
       b += fmix64((obs * N + subj) * K + d);
     }
   }
