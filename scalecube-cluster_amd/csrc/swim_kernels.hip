@@ -957,6 +957,17 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 #ifndef SWIM_SEL_WAVES
 #define SWIM_SEL_WAVES 8
 #endif
+#ifndef SWIM_SEL_AHEAD
+#define SWIM_SEL_AHEAD 1
+#endif
+#ifndef SWIM_SEL_MW_WORD
+#define SWIM_SEL_MW_WORD 1
+#endif
+#if SWIM_SEL_MW_WORD
+#define SEL_ME(j_) s_mw[w][j_][lane].x
+#else
+#define SEL_ME(j_) s_me[w][j_][lane]
+#endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
@@ -964,7 +975,11 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
+#if SWIM_SEL_MW_WORD
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
+#else
+  __shared__ uint32_t s_me[4][4 * SEL_BATCH][64];  // list entries of this step's MIXED entries
+#endif
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t m = P.row0 + blockIdx.x * 4u + w;
@@ -1060,7 +1075,11 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           }
           if (wcm == WC_MIXED || scm == WC_MIXED) {
             mixm |= 1u << j;
+#if SWIM_SEL_MW_WORD
             s_mw[w][j][lane] = make_uint2(e, word);  // for the pass below: no list or holdings re-read
+#else
+            s_me[w][j][lane] = e;  // for the pass below: no list re-read
+#endif
             continue;
           }
           if (wcm == WC_ALL) win = held;
@@ -1084,16 +1103,33 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         }
         }
       }
-      // entries one at a time from the mask, the next one's infection rounds (32 B) loaded
-      // before the current one is evaluated: two reads in flight per lane
+      // entries one at a time from the mask, the infection rounds (32 B) of the next
+      // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
+      auto hd_of = [&](uint32_t e_) {
+        return reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (e_ & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
+      };
       uint32_t jn = 0, en = 0;
       uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+#if SWIM_SEL_AHEAD >= 2
+      uint32_t jm = 0, em = 0;
+      uint4 m0 = n0, m1 = n0;
+      uint32_t rest = mixm;  // entries not yet loaded
+#endif
       if (mixm) {
         jn = (uint32_t)__builtin_ctz(mixm);
-        en = s_mw[w][jn][lane].x;
-        const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (en & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
-        n0 = dp[0];
-        n1 = dp[1];
+        en = SEL_ME(jn);
+        n0 = hd_of(en)[0];
+        n1 = hd_of(en)[1];
+#if SWIM_SEL_AHEAD >= 2
+        rest &= rest - 1u;
+        if (rest) {
+          jm = (uint32_t)__builtin_ctz(rest);
+          em = SEL_ME(jm);
+          m0 = hd_of(em)[0];
+          m1 = hd_of(em)[1];
+          rest &= rest - 1u;
+        }
+#endif
       }
       while (mixm) {
         const uint32_t j = jn;
@@ -1101,17 +1137,34 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         const uint32_t k = k0 + 256u * (j >> 2) + 4u * lane + (j & 3u);
         const uint32_t e = en;
         const uint4 d0 = n0, d1 = n1;
+#if SWIM_SEL_AHEAD >= 2
+        jn = jm;
+        en = em;
+        n0 = m0;
+        n1 = m1;
+        if (rest) {
+          jm = (uint32_t)__builtin_ctz(rest);
+          em = SEL_ME(jm);
+          m0 = hd_of(em)[0];
+          m1 = hd_of(em)[1];
+          rest &= rest - 1u;
+        }
+#else
         if (mixm) {
           jn = (uint32_t)__builtin_ctz(mixm);
-          en = s_mw[w][jn][lane].x;
-          const uint4* dp = reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (en & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
-          n0 = dp[0];
-          n1 = dp[1];
+          en = SEL_ME(jn);
+          n0 = hd_of(en)[0];
+          n1 = hd_of(en)[1];
         }
+#endif
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u;
         const uint32_t ws = wi & (W32 - 1u);
+#if SWIM_SEL_MW_WORD
         const uint32_t word = s_mw[w][j][lane].y;
+#else
+        const uint32_t word = hbr[ws];  // cache-resident: read in the pass above
+#endif
         const uint32_t held = word & range_mask(wi << 5, lo, hi);
         // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
         ++hdw;

@@ -228,3 +228,27 @@ def test_apply_spill_path_parity():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     spills = int(out.stdout.split("SPILLS")[-1])
     assert spills > 0, "the spill path never ran"
+
+
+def test_c3long_schedule_small_parity():
+    """SURVEY §8(d)'s C3 variant at N = 1,024: 10 % crash + a 16-member group cut for 120 periods,
+    past the suspicion timeout, seeds 0..15 (MembershipProtocolTest.testLongNetworkPartition...
+    Removed, :320-371, scaled up). Both sides remove each other, the group rejoins through the
+    seeds after the heal, and the crashed members the group never probed stay in its views until
+    its own FD reaches them. Digests and counters equal the oracle's every 25 periods for 250."""
+    import bench
+
+    n = 1024
+    cfg = bench.preset_config("lan").membership(lambda o: o.seedMembers(list(range(16))))
+    a = SwimCluster(cfg, n, seed=1, gossip_capacity=1 << 18)
+    b = OracleCluster(cfg, n, seed=1)
+    for c in (a, b):
+        c.step(3)
+        bench.inject_faults(c, "c3long", 3, 1, n=n)
+    for _ in range(10):
+        for c in (a, b):
+            c.step(25)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+    assert 0 < a.stats()["not_converged"] < 1322  # the cut group's unprobed crashed members, draining
