@@ -232,12 +232,15 @@ int check_overflow(swim_handle* h);
 
 // Order the phase's gossips by (subject, record) and commit them: one k_commit launch. stg != nullptr: the local stage, counted on the device (no host round trip); otherwise
 // the n gathered gossips already in h->ck[0] / h->cv[0].
-int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n) {
+int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n, uint32_t bound = NONE) {
   hipStream_t s = h->stream;
-  CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u};
+  CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u, 0u};
   C.npass = (32u + bitlen(h->N - 1u) + 7u) / 8u;  // key = subject << 32 | record
-  // the sharded batch size is known here: launch the radix kernels only when they have work
-  const bool big = stg != nullptr || n > CS_SMALL;
+  // launch the radix kernels only when the batch may need them: the sharded batch size is known
+  // here; a local stage is bounded by the phase (`bound`: a gossip round stages at most one
+  // refutation per member, MPI:549-569; k_commit fails loudly if a bound is ever exceeded)
+  const bool big = stg != nullptr ? bound > CS_SMALL : n > CS_SMALL;
+  C.radix = big ? 1u : 0u;
   const uint32_t tiles = stg ? h->cs_maxt : std::max<uint32_t>(1, (n + CS_TILE - 1) / CS_TILE);
   timed(h, 7, "k_commit", [&] {
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
@@ -260,10 +263,10 @@ int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n) {
 // reported at the next swim_sync; k_gossip_prep lists nothing once it is set, so a run never
 // feeds a wrapped ring to the gossip kernels). Sharded: the host all-gathers every shard's stage
 // first (returns true: exchange pending); all shards then sort the same batch.
-bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc) {
+bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t bound = NONE) {
   hipStream_t s = h->stream;
   if (h->world == 1) {
-    *rc = commit_sorted(h, P, P.stg, 0u);
+    *rc = commit_sorted(h, P, P.stg, 0u, bound);
     return false;
   }
   // {overflow, stg_count} in one copy: a sharded run stops at the first phase whose buffers
@@ -438,7 +441,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;
-        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        if (commit_begin(h, P, x, &rc, nloc)) return SWIM_OK;
         if (rc) return rc;
         break;
       case PC_R_C:

@@ -230,6 +230,7 @@ struct CSort {
   uint32_t* ctr;    // [CS_MAXPASS] tiles handed out per pass
   uint32_t* stat;   // [CS_MAXPASS][maxt][256] look-back status: flag | count
   uint32_t maxt, npass;
+  uint32_t radix;   // 0: the host launched no radix kernels (the phase cannot stage > CS_SMALL)
 };
 
 __device__ __forceinline__ uint32_t cs_n(const KP& P, const uint4* stg, uint32_t n_host) {
@@ -263,6 +264,10 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
   const uint32_t t = threadIdx.x;
   const uint32_t n = cs_n(P, stg, n_host);
   if (n > CS_SMALL) {  // a storm phase: reset the radix sort's counters for this batch
+    if (!C.radix) {  // the host's bound on this phase's gossips was wrong: fail loudly
+      if (t == 0) atomicOr(&P.ctl->overflow, OV_BUG);
+      return;
+    }
     const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
     for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) C.ghist[i] = 0u;
     if (t < CS_MAXPASS) C.ctr[t] = 0u;
