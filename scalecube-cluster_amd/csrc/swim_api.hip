@@ -54,6 +54,9 @@ struct swim_handle {
   // gossip commits: sort keys/values (ping-pong) and the radix sort's counters (k_commit, k_rs_*)
   uint32_t *cs_ghist = nullptr, *cs_ctr = nullptr, *cs_stat = nullptr;
   uint32_t cs_maxt = 1;
+  // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
+  uint32_t apply_blocks = 1;
+  size_t apply_lds = 0;
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
@@ -437,7 +440,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 1, "k_gossip_pull", [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
-        timed(h, 2, "k_gossip_apply", [&] { hipLaunchKernelGGL(k_gossip_apply, dim3(APPLY_BLOCKS), dim3(APPLY_THREADS), 0, s, P); });
+        timed(h, 2, "k_gossip_apply", [&] {
+          hipLaunchKernelGGL(k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
+        });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;
@@ -644,6 +649,20 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // infectedFrom horizon: a delivery of round t can suppress sends up to round
   // t + 1 + gossipPeriodsToSpread
   P.hzn = P.rm * bitlen(N) + 1u;
+  {  // apply's LDS table: >= 2 slots per possible distinct subject (N), at most the build's cap;
+     // a smaller table lets two 1,024-thread workgroups share a CU
+    uint32_t lg = 6;
+    while (lg < HCAP_LOG && (1ull << lg) < 2ull * N) ++lg;
+    P.apply_hlog = lg;
+    const uint64_t pres_words = N <= 32u * PRES_WORDS ? (N + 31u) / 32u : 0u;
+    h->apply_lds = 4ull * (2ull * (1ull << lg) + SPILL_CAP + pres_words);
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
+    const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU
+    h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
+  }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
                  P.rm, N, P.sweepmax, P.hzn);

@@ -240,6 +240,7 @@ struct KP {
   uint32_t* ack_ref;    // [2N] requester side: record index of the SYNC_ACK of remote request q
   // GossipState.infectedFrom (GossipState.java:17, GossipProtocolImpl.java:181,248), DESIGN.md §3.9
   uint32_t hzn;        // rounds a delivery can still suppress a send: gossipPeriodsToSpread(N) + 1
+  uint32_t apply_hlog; // k_gossip_apply's LDS table: 2^apply_hlog slots (<= 2^SWIM_APPLY_HLOG)
   unsigned long long* dbg_send;  // [2N] debug: per sender, GossipRequests to alive peers before / by infectedFrom
   uint32_t dbg_watch;            // debug: member whose per-round sends go to dbg_log (NONE: off)
   uint32_t* dbg_log;             // [256][8] round, window bits, alive peers, peers, peer ids x3, suppressed

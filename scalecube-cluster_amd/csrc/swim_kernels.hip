@@ -1808,16 +1808,12 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
 #ifndef SWIM_APPLY_THREADS
 #define SWIM_APPLY_THREADS 1024
 #endif
-#ifndef SWIM_APPLY_BLOCKS
-#define SWIM_APPLY_BLOCKS 256
-#endif
 constexpr uint32_t HCAP_LOG = SWIM_APPLY_HLOG;
 constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 128 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
 constexpr uint32_t SPILL_CAP = 1024;       // spilled subjects per receiver and round (LDS list)
 constexpr uint32_t PRES_WORDS = 2048;     // subject-presence bitmap for N <= 65,536
 constexpr uint32_t APPLY_THREADS = SWIM_APPLY_THREADS;
-constexpr uint32_t APPLY_BLOCKS = SWIM_APPLY_BLOCKS;  // persistent: one 16-wave workgroup per CU (LDS-bound)
 // build-time tunables (-DSWIM_APPLY_HLOG / _THREADS): the table init starts at 64 slots, the
 // block scan keeps one partial per wave (16 at most), and the kernel's LDS must fit gfx950's 160 KiB
 static_assert(HCAP_LOG >= 6 && HCAP_LOG <= 14, "SWIM_APPLY_HLOG out of range");
@@ -1836,10 +1832,15 @@ static_assert(4 * (2 * HCAP + SPILL_CAP + PRES_WORDS + 17) <= 160 * 1024, "k_gos
 // Then one updateMembership per subject.
 __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   SWIM_GUARD(P);
-  __shared__ uint32_t s_key[HCAP];
-  __shared__ uint32_t s_val[HCAP];
-  __shared__ uint32_t s_spl[SPILL_CAP];
-  __shared__ uint32_t s_pres[PRES_WORDS];  // subjects in the table (N <= 65,536): row-order apply
+  // dynamic LDS sized for the cluster (apply_lds_words): small clusters get a smaller table and
+  // two workgroups per CU; 2^apply_hlog table slots (keys, values), the spill list, and (N <=
+  // 65,536) the subject-presence bitmap for row-order apply
+  extern __shared__ uint32_t s_dyn[];
+  const uint32_t hcap_log = P.apply_hlog, hcap = 1u << hcap_log;
+  uint32_t* s_key = s_dyn;
+  uint32_t* s_val = s_dyn + hcap;
+  uint32_t* s_spl = s_dyn + 2u * hcap;
+  uint32_t* s_pres = s_spl + SPILL_CAP;
   __shared__ uint32_t s_nspill;
   __shared__ uint32_t s_part[16];
   const uint32_t r = P.round;
@@ -1861,8 +1862,8 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
-    uint32_t lg = 6;  // table size >= 2x receipts, 64 .. HCAP
-    while (lg < HCAP_LOG && (1u << lg) < 2u * total) ++lg;
+    uint32_t lg = 6;  // table size >= 2x receipts, 64 .. hcap
+    while (lg < hcap_log && (1u << lg) < 2u * total) ++lg;
     const uint32_t hm = (1u << lg) - 1u;
     for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x) {
       s_key[t] = NONE;
@@ -1956,9 +1957,9 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
     // The list positions with receipts, compacted from the summary into the table's unused tail:
     // the table has 2^lg >= 2 * total slots and a receipt word holds >= 1 receipt, so when
-    // 2^lg < HCAP the <= total positions fit in HCAP - 2^lg >= 2^lg slots. Otherwise every summary
+    // 2^lg < hcap the <= total positions fit in hcap - 2^lg >= 2^lg slots. Otherwise every summary
     // bit is an item and threads test their own.
-    const bool compact = summ && lg < HCAP_LOG;
+    const bool compact = summ && lg < hcap_log;
     uint32_t* s_items = s_key + (1u << lg);
     uint32_t n_comp = 0;
     if (compact) {
