@@ -3,7 +3,9 @@
 // Phase order per period, all on one HIP stream, no host round trips:
 //   k_fd             FailureDetectorImpl.doPing/doPingReq (FailureDetectorImpl.java:126-209)
 //                    + onFailureDetectorEvent (MembershipProtocolImpl.java:376-404)
-//   G x { k_gossip_prep, k_gossip_select, k_gossip_send, k_gossip_apply, k_finalize }
+//   k_commit (+ k_rs_* for storm phases) after every phase that creates gossips
+//   G x { k_gossip_prep, k_gossip_select, k_gossip_pairfill/pairprune, k_gossip_inhist,
+//         k_gossip_pull, k_gossip_record, k_gossip_apply, k_finalize }
 //                    GossipProtocolImpl.doSpreadGossip/onGossipReq/sweepGossips
 //                    (GossipProtocolImpl.java:139-304) + onMembershipGossip (MPI:407-414)
 //   k_due, k_susp_sweep, k_finalize
@@ -846,7 +848,7 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     const uint32_t hi = c->gcount;
     uint32_t lo = c->glo;
     if (hi - lo > P.GC) lo = hi - P.GC;
-    // a full ring (k_gossip_commit has raised OV_GOSSIP): keep the listed words within one lap of
+    // a full ring (k_commit has raised OV_GOSSIP): keep the listed words within one lap of
     // the ring, so no list position reaches past a W32-word row of wb / nb
     const uint32_t lo_w = (((hi + 31u) >> 5) - (P.GC >> 5)) << 5;
     if (((hi + 31u) >> 5) - (lo >> 5) > (P.GC >> 5)) lo = lo_w;
@@ -2267,7 +2269,6 @@ __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
   if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.N + 2u)]] = g;
 }
 
-// the all-reduce MAX operand of a round: per-word gossip liveness + the bit_length bounds
 // Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
 // bit-length bounds after the words of its staged gossips: [gossips | wlast | bhi | 32 - blo]
 __global__ void k_round_max_pack(KP P, uint32_t off) {
