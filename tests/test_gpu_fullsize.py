@@ -126,3 +126,35 @@ def test_c2_convergence_tail_is_fd_driven():
         first_suspect = susp_seen.get((i, s), removed)
         print(f"straggler ({i}, {s}): SUSPECT by its own FD at t0+{first_suspect}, removed at t0+{removed}", flush=True)
         assert removed - first_suspect <= 65 + 5, (i, s, first_suspect, removed)
+
+
+def test_c5_geometry_fullsize_properties():
+    """C5's geometry at full size (BASELINE configs[4]: 1,048,576 members, N x K views with K = 256,
+    LAN defaults) with the churn one GPU's holdings can carry (8 simultaneous crashes; the full
+    256-crash storm overflows the 2^17-slot ring loudly): after 120 periods every
+    crashed member is gone from every alive view (suspicion timeout 105 periods), no alive member
+    was removed, no buffer overflowed, and a second handle with the same seed reaches the same
+    digests."""
+
+    def run():
+        c = bench.make_cluster("c5g", 0, seed=1)
+        c.step(3)
+        crashed = bench.inject_faults(c, "c5g", 3, 1)
+        c.step(120)
+        out = (c.digest(), c.stats(), c.presence(), crashed, c.view(12345))
+        c.close()
+        return out
+
+    d1, st, (pres, last), crashed, row = run()
+    n = bench.WORKLOADS["c5g"]["n"]
+    alive = np.ones(n, dtype=bool)
+    alive[crashed] = False
+    n_alive = int(alive.sum())
+    assert st["overflow"] == 0
+    assert st["not_converged"] == 0
+    assert np.all(pres[crashed] == 0)
+    assert np.all(pres[alive] == n_alive - 1) and np.all(last[alive] == 0)
+    assert st["events_removed"] == len(crashed) * n_alive
+    assert np.all(row[crashed] == 0) and np.all(row[alive] != 0)
+    d2, st2, _, _, _ = run()
+    assert d1 == d2 and st["gossips_created"] == st2["gossips_created"]
