@@ -101,8 +101,8 @@ def kernel_bytes(name, d, n):
         # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4);
         # per subject run one ring record (8 B); per subject the table cell and its deadline (8 B)
         return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
-    if name == "k_susp_sweep":  # stream a deadline column
-        return 4 * d["sweep_cells"]
+    if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write and
+        return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"]  # the view cell read + write
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
         return 24 * d["fd_probes"]
     # infectedFrom bookkeeping: in-history ring entries (16 B per registration,

@@ -2318,7 +2318,7 @@ __global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
 
 // onSuspicionTimeout (MembershipProtocolImpl.java:637-647) for one deadline cell of column j
 __device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t li, uint32_t v, uint32_t* mn,
-                                               uint32_t* fired, Tally& T) {
+                                               uint32_t* fired, uint32_t* removed, Tally& T) {
   if (v == 0u) return 0u;
   const uint32_t i = P.row0 + li;
   if (!P.alive[i]) return 0u;  // a stopped member's timers never fire: dropped
@@ -2327,9 +2327,24 @@ __device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t
     *mn = dl < *mn ? dl : *mn;
     return v;
   }
-  if (P.view[(size_t)li * P.W + j] != 0u) {
+  uint32_t* cellp = P.view + (size_t)li * P.W + j;
+  const uint32_t r0 = *cellp;
+  if (r0 != 0u) {
     ++*fired;
-    apply_record(P, i, subj_of(P, j), SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
+    const uint32_t subj = subj_of(P, j);
+    if (subj == i || (P.rerouted && P.addr[subj] == P.addr[i])) {  // the general path (never taken
+      apply_record(P, i, subj, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);  // in practice)
+    } else {
+      // updateMembership(DEAD) -> onDeadMemberDetected (MPI:571-587) as in apply_record, with the
+      // subject's presence count and last-removal period left to the caller: every cell of a
+      // swept column has the same subject, so the workgroup applies them once (no hot atomics)
+      *cellp = SWIM_ABSENT;
+      atomicSub(&P.cnt_delta[i], 1);
+      T.accepted++;
+      T.removed++;
+      ++*removed;
+      push_event(P, i, subj, SWIM_EV_REMOVED, SWIM_R_SUSPICION_TIMEOUT, r0);
+    }
   }
   return 0u;
 }
@@ -2339,7 +2354,7 @@ __device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t
 constexpr uint32_t SWEEP_CHUNK = 4096;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   SWIM_GUARD(P);
-  __shared__ uint32_t s_min[4];
+  __shared__ uint32_t s_min[4], s_rem[4];
   Tally T;
   uint32_t fired = 0, cells = 0;
   const uint32_t n = P.ctl->due_count;
@@ -2349,21 +2364,21 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     const uint32_t j = P.due[u / nch];  // the cell; its subject is subj_of(j)
     const uint32_t c0 = (u % nch) * SWEEP_CHUNK, c1 = min(P.nloc, c0 + SWEEP_CHUNK);
     uint32_t* col = P.dl + (size_t)j * P.nloc;
-    uint32_t mn = NONE;
+    uint32_t mn = NONE, rem = 0;
     if (vec) {
       for (uint32_t li = c0 + 4u * threadIdx.x; li < c1; li += 4u * blockDim.x) {
         uint4 v = *reinterpret_cast<const uint4*>(col + li);
         if ((v.x | v.y | v.z | v.w) == 0u) continue;
-        const uint4 w = make_uint4(sweep_cell(P, j, li, v.x, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 1u, v.y, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 2u, v.z, &mn, &fired, T),
-                                   sweep_cell(P, j, li + 3u, v.w, &mn, &fired, T));
+        const uint4 w = make_uint4(sweep_cell(P, j, li, v.x, &mn, &fired, &rem, T),
+                                   sweep_cell(P, j, li + 1u, v.y, &mn, &fired, &rem, T),
+                                   sweep_cell(P, j, li + 2u, v.z, &mn, &fired, &rem, T),
+                                   sweep_cell(P, j, li + 3u, v.w, &mn, &fired, &rem, T));
         if (w.x != v.x || w.y != v.y || w.z != v.z || w.w != v.w) *reinterpret_cast<uint4*>(col + li) = w;
       }
     } else {
       for (uint32_t li = c0 + threadIdx.x; li < c1; li += blockDim.x) {
         const uint32_t v = col[li];
-        const uint32_t w = sweep_cell(P, j, li, v, &mn, &fired, T);
+        const uint32_t w = sweep_cell(P, j, li, v, &mn, &fired, &rem, T);
         if (w != v) col[li] = w;
       }
     }
@@ -2372,13 +2387,25 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     for (int o = 32; o > 0; o >>= 1) {
       const uint32_t y = __shfl_xor(mn, o, 64);
       mn = y < mn ? y : mn;
+      rem += __shfl_xor(rem, o, 64);
     }
-    if ((threadIdx.x & 63u) == 0) s_min[threadIdx.x >> 6] = mn;
+    if ((threadIdx.x & 63u) == 0) {
+      s_min[threadIdx.x >> 6] = mn;
+      s_rem[threadIdx.x >> 6] = rem;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      uint32_t b = s_min[0];
-      for (uint32_t q = 1; q < blockDim.x / 64u; ++q) b = s_min[q] < b ? s_min[q] : b;
+      uint32_t b = s_min[0], nr = s_rem[0];
+      for (uint32_t q = 1; q < blockDim.x / 64u; ++q) {
+        b = s_min[q] < b ? s_min[q] : b;
+        nr += s_rem[q];
+      }
       if (b != NONE) atomicMin(&P.colmin[j], b);
+      if (nr) {  // the removals of this piece of the column: presence and last-removal period once
+        const uint32_t subj = subj_of(P, j);
+        atomicSub(&P.pres[subj], nr);
+        atomicMax(&P.last_removed[subj], P.period + 1u);
+      }
     }
     __syncthreads();
   }
