@@ -338,7 +338,7 @@ def main():
         extra = 0
         # the suspicion sweep only has work in the periods whose deadlines fall due: its roofline is
         # taken over those launches (one period at a time, kernel-time and sweep_cells deltas)
-        fire_ms, fire_n, fire_cells = 0.0, 0, 0
+        fire_ms, fire_n, fire_cells, fire_dead = 0.0, 0, 0, 0
         st = c.stats()
         while extra < args.converge and st["not_converged"]:
             k0 = c.kernel_times().get("k_susp_sweep", (0.0, 0))
@@ -350,6 +350,7 @@ def main():
                 fire_ms += k1[0] - k0[0]
                 fire_n += k1[1] - k0[1]
                 fire_cells += st1["sweep_cells"] - st["sweep_cells"]
+                fire_dead += st1["suspicion_timeouts"] - st["suspicion_timeouts"]
             st = st1
             if extra % 5 == 0:
                 log(f"converge: +{extra} periods, not_converged={st['not_converged']}")
@@ -362,7 +363,7 @@ def main():
                 for v in [roofline_of(k, kt2, dc, world)] if v}
         if fire_n:
             sweep_rl = roofline_of("k_susp_sweep", {"k_susp_sweep": (fire_ms, fire_n)},
-                                   {"sweep_cells": fire_cells}, world)
+                                   {"sweep_cells": fire_cells, "suspicion_timeouts": fire_dead}, world)
             conv["k_susp_sweep"] = round(sweep_rl["frac"], 4)
         c.kernel_timing(False)
 

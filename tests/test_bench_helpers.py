@@ -28,7 +28,8 @@ def test_kernel_bytes_covers_every_timed_class():
 
     d = {k: 1 for k in ("merge_cells", "ack_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                         "gossip_pull_words", "gossip_probes", "gossip_first_receipts", "sweep_cells", "fd_probes",
-                        "infected_pruned_pairs", "infected_records", "apply_words", "apply_runs", "apply_subjects")}
+                        "infected_pruned_pairs", "infected_records", "apply_words", "apply_runs", "apply_subjects",
+                        "suspicion_timeouts")}
     for name in SwimCluster.KERNEL_CLASSES:
         if name != "bookkeeping":
             assert bench.kernel_bytes(name, d, 1) > 0, name
