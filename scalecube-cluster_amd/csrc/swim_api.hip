@@ -655,7 +655,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     while (lg < HCAP_LOG && (1ull << lg) < 2ull * N) ++lg;
     P.apply_hlog = lg;
     const uint64_t pres_words = N <= 32u * PRES_WORDS ? (N + 31u) / 32u : 0u;
-    h->apply_lds = 4ull * (2ull * (1ull << lg) + SPILL_CAP + pres_words);
+    h->apply_lds = 4ull * (2ull * (1ull << lg) + SPILL_CAP + (SWIM_APPLY_PAIR ? 2u : 1u) * pres_words);
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
     const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU

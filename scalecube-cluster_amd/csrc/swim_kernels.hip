@@ -1810,6 +1810,9 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
 #ifndef SWIM_APPLY_THREADS
 #define SWIM_APPLY_THREADS 1024
 #endif
+#ifndef SWIM_APPLY_PAIR
+#define SWIM_APPLY_PAIR 1
+#endif
 constexpr uint32_t HCAP_LOG = SWIM_APPLY_HLOG;
 constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 128 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
@@ -1821,6 +1824,30 @@ constexpr uint32_t APPLY_THREADS = SWIM_APPLY_THREADS;
 static_assert(HCAP_LOG >= 6 && HCAP_LOG <= 14, "SWIM_APPLY_HLOG out of range");
 static_assert(APPLY_THREADS % 64 == 0 && APPLY_THREADS <= 1024, "SWIM_APPLY_THREADS must be a multiple of 64, <= 1024");
 static_assert(4 * (2 * HCAP + SPILL_CAP + PRES_WORDS + 17) <= 160 * 1024, "k_gossip_apply LDS over 160 KiB");
+
+// exclusive scan over a whole 1,024-thread workgroup, or (pair) over each 512-thread half on its own
+__device__ __forceinline__ uint32_t block_excl_scan_part(uint32_t v, uint32_t* total, uint32_t* lds16, bool pair,
+                                                         uint32_t half) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63u) lds16[w] = x;
+  __syncthreads();
+  const uint32_t k0 = pair ? 8u * half : 0u, k1 = pair ? k0 + 8u : blockDim.x / 64u;
+  uint32_t base = 0, tot = 0;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t t = lds16[k];
+    if (k < w) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
 
 // Membership apply of a round's first receipts: onGossipReq's new-gossip branch
 // (GossipProtocolImpl.java:175-180) and onMembershipGossip (MPI:407-414) with the lattice max of
@@ -1839,11 +1866,8 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   // 65,536) the subject-presence bitmap for row-order apply
   extern __shared__ uint32_t s_dyn[];
   const uint32_t hcap_log = P.apply_hlog, hcap = 1u << hcap_log;
-  uint32_t* s_key = s_dyn;
-  uint32_t* s_val = s_dyn + hcap;
-  uint32_t* s_spl = s_dyn + 2u * hcap;
-  uint32_t* s_pres = s_spl + SPILL_CAP;
-  __shared__ uint32_t s_nspill;
+  const uint32_t pres_words = P.N <= 32u * PRES_WORDS ? (P.N + 31u) / 32u : 0u;
+  __shared__ uint32_t s_nsp[2];
   __shared__ uint32_t s_part[16];
   const uint32_t r = P.round;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
@@ -1861,20 +1885,39 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
 #else
 #define APPLY_MARK(q)
 #endif
-  for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
-    const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
+  for (uint32_t li = blockIdx.x; li < n_list;) {
+    // SWIM_APPLY_PAIR: two receivers at once when both fit half the table, one per half-block
+    // (every barrier below is reached by both halves: same phases, same scan count)
+    const uint32_t li2 = li + gridDim.x;
+    // (8 x receipts <= table: each half's table has room for its compacted items too, so both
+    // halves take the same compaction path and meet the same barriers)
+    // (a half-table must hold the 64-slot minimum: tables of 128 slots and up)
+    const bool pair = SWIM_APPLY_PAIR && hcap_log >= 7u && li2 < n_list && 8u * P.alist[2 * li + 1] <= hcap &&
+                      8u * P.alist[2 * li2 + 1] <= hcap && (n_act + 31u) / 32u <= NSUM;  // uniform
+    const uint32_t half = pair ? (threadIdx.x >> 9) : 0u;
+    const uint32_t tid = pair ? (threadIdx.x & 511u) : threadIdx.x, nthr = pair ? 512u : blockDim.x;
+    const uint32_t mli = half ? li2 : li;
+    li += pair ? 2u * gridDim.x : gridDim.x;
+    const uint32_t hc_log = pair ? hcap_log - 1u : hcap_log;  // this receiver's table: 2^hc_log slots
+    uint32_t* s_key = s_dyn + half * (hcap >> 1);
+    uint32_t* s_val = s_dyn + hcap + half * (hcap >> 1);
+    const uint32_t spill_cap = pair ? SPILL_CAP / 2u : SPILL_CAP;
+    uint32_t* s_spl = s_dyn + 2u * hcap + half * (SPILL_CAP / 2u);
+    uint32_t* s_pres = s_dyn + 2u * hcap + SPILL_CAP + half * pres_words;
+    uint32_t& s_nspill = s_nsp[half];
+    const uint32_t p = P.alist[2 * mli], total = P.alist[2 * mli + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
-    uint32_t lg = 6;  // table size >= 2x receipts, 64 .. hcap
-    while (lg < hcap_log && (1u << lg) < 2u * total) ++lg;
+    uint32_t lg = 6;  // table size >= 2x receipts, 64 .. 2^hc_log
+    while (lg < hc_log && (1u << lg) < 2u * total) ++lg;
     const uint32_t hm = (1u << lg) - 1u;
-    for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x) {
+    for (uint32_t t = tid; t <= hm; t += nthr) {
       s_key[t] = NONE;
       s_val[t] = 0u;
     }
-    if (threadIdx.x == 0) s_nspill = 0u;
+    if (tid == 0) s_nspill = 0u;
     const bool pres = P.N <= 32u * PRES_WORDS;
     if (pres)
-      for (uint32_t t = threadIdx.x; t < (P.N + 31u) / 32u; t += blockDim.x) s_pres[t] = 0u;
+      for (uint32_t t = tid; t < (P.N + 31u) / 32u; t += nthr) s_pres[t] = 0u;
     __syncthreads();
     APPLY_MARK(0)
     // infection rounds, word liveness, and the lattice max per subject, over the words the
@@ -1947,7 +1990,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
             if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr[j].x)], sr[j].y) == 0u) {
               const uint32_t o = atomicAdd(&s_nspill, 1u);
-              if (o < SPILL_CAP)
+              if (o < spill_cap)
                 s_spl[o] = sr[j].x;
               else
                 atomicOr(&P.ctl->overflow, OV_SPILL);
@@ -1961,15 +2004,15 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     // the table has 2^lg >= 2 * total slots and a receipt word holds >= 1 receipt, so when
     // 2^lg < hcap the <= total positions fit in hcap - 2^lg >= 2^lg slots. Otherwise every summary
     // bit is an item and threads test their own.
-    const bool compact = summ && lg < hcap_log;
+    const bool compact = summ && lg < hc_log;
     uint32_t* s_items = s_key + (1u << lg);
     uint32_t n_comp = 0;
     if (compact) {
-      for (uint32_t c0 = 0; c0 < nsw; c0 += blockDim.x) {
-        const uint32_t t = c0 + threadIdx.x;
+      for (uint32_t c0 = 0; c0 < nsw; c0 += nthr) {
+        const uint32_t t = c0 + tid;
         uint32_t bits = t < nsw ? sumr[t] : 0u;
         uint32_t tot;
-        uint32_t o = n_comp + block_excl_scan1024((uint32_t)__popc(bits), &tot, s_part);
+        uint32_t o = n_comp + block_excl_scan_part((uint32_t)__popc(bits), &tot, s_part, pair, half);
         while (bits) {
           s_items[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
           bits &= bits - 1u;
@@ -1980,13 +2023,13 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     }
     APPLY_MARK(1)
     const uint32_t n_it = compact ? n_comp : n_items;
-    for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * blockDim.x) {
+    for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * nthr) {
       // four items per thread: their loads are issued together, stage by stage
       uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
       uint4 v0[4], v1[4];
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t it = it0 + j * blockDim.x + threadIdx.x;
+        const uint32_t it = it0 + j * nthr + tid;
         if (compact) {
           kv[j] = it < n_it ? s_items[it] : NONE;
         } else {
@@ -2029,7 +2072,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     };
     if (pres) {  // one updateMembership per subject, in subject order: neighbouring threads touch
                  // neighbouring cells of the receiver's row (coalesced, line reuse)
-      for (uint32_t t = threadIdx.x; t < (P.N + 31u) / 32u; t += blockDim.x) {
+      for (uint32_t t = tid; t < (P.N + 31u) / 32u; t += nthr) {
         uint32_t bits = s_pres[t];
         while (bits) {
           const uint32_t subj = 32u * t + (uint32_t)__builtin_ctz(bits);
@@ -2040,17 +2083,17 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         }
       }
     } else {
-      for (uint32_t t = threadIdx.x; t <= hm; t += blockDim.x)  // one updateMembership per subject
+      for (uint32_t t = tid; t <= hm; t += nthr)  // one updateMembership per subject
         if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
     }
-    const uint32_t nsp = s_nspill < SPILL_CAP ? s_nspill : SPILL_CAP;
+    const uint32_t nsp = s_nspill < spill_cap ? s_nspill : spill_cap;
     if (nsp) __threadfence();
-    for (uint32_t t = threadIdx.x; t < nsp; t += blockDim.x) {
+    for (uint32_t t = tid; t < nsp; t += nthr) {
       const uint32_t subj = s_spl[t];
       apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
     }
-    if (threadIdx.x == 0) atomicAdd(&P.held[p], total);
-    nspills += threadIdx.x == 0 ? nsp : 0u;
+    if (tid == 0) atomicAdd(&P.held[p], total);
+    nspills += tid == 0 ? nsp : 0u;
     __syncthreads();  // the table is reused by the next receiver
     APPLY_MARK(3)
   }
