@@ -309,7 +309,13 @@ __device__ __forceinline__ void ifrom_overflow(const KP& P, uint32_t why) {
   atomicOr(&P.ctl->ov_detail, why);
 }
 
-__device__ __forceinline__ uint32_t ncells(const KP& P) { return P.nxk ? P.ctl->ncols : P.N; }
+// ctl->ncols counts every column request, including the ones k_track_alloc refused with OV_TRACK:
+// clamp to the K columns that exist, so no kernel run after an overflow indexes past them
+__device__ __forceinline__ uint32_t ncells(const KP& P) {
+  if (!P.nxk) return P.N;
+  const uint32_t n = P.ctl->ncols;
+  return n < P.W ? n : P.W;
+}
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {
   return bm && (bm[bit >> 3] & (1u << (bit & 7)));

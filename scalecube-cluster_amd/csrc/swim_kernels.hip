@@ -84,8 +84,11 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
   if (threadIdx.x == 0 && !P.leaving[i] && P.alive[i]) {
     P.leaving[i] = 1;
     P.leave_slot[i] = NONE;
-    if (is_local(P, i)) {
-      P.view[lrow(P, i) * P.W + col_of(P, i)] = SWIM_DEAD;  // N x K: k_track_one gave i a column
+    const uint32_t col = col_of(P, i);  // N x K: k_track_one asked for a column
+    if (col == NONE) {                   // no column left (OV_TRACK): the run has failed
+      atomicOr(&P.ctl->overflow, OV_TRACK);
+    } else if (is_local(P, i)) {
+      P.view[lrow(P, i) * P.W + col] = SWIM_DEAD;
       emit_gossip(P, i, i, SWIM_DEAD, P.gseq[i]++);
       created = 1;
     }
@@ -1823,7 +1826,10 @@ constexpr uint32_t APPLY_THREADS = SWIM_APPLY_THREADS;
 // block scan keeps one partial per wave (16 at most), and the kernel's LDS must fit gfx950's 160 KiB
 static_assert(HCAP_LOG >= 6 && HCAP_LOG <= 14, "SWIM_APPLY_HLOG out of range");
 static_assert(APPLY_THREADS % 64 == 0 && APPLY_THREADS <= 1024, "SWIM_APPLY_THREADS must be a multiple of 64, <= 1024");
-static_assert(4 * (2 * HCAP + SPILL_CAP + PRES_WORDS + 17) <= 160 * 1024, "k_gossip_apply LDS over 160 KiB");
+static_assert(4 * (2 * HCAP + SPILL_CAP + (SWIM_APPLY_PAIR ? 2 : 1) * PRES_WORDS + 17) <= 160 * 1024,
+              "k_gossip_apply LDS over 160 KiB");
+// paired receivers split the workgroup into two 512-thread halves of 8 waves each
+static_assert(!SWIM_APPLY_PAIR || APPLY_THREADS == 1024, "SWIM_APPLY_PAIR needs SWIM_APPLY_THREADS == 1024");
 
 // exclusive scan over a whole 1,024-thread workgroup, or (pair) over each 512-thread half on its own
 __device__ __forceinline__ uint32_t block_excl_scan_part(uint32_t v, uint32_t* total, uint32_t* lds16, bool pair,

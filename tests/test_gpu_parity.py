@@ -74,6 +74,21 @@ def test_nxk_column_overflow_is_loud():
     with pytest.raises(SwimError) as ei:
         c.step(10)
     assert ei.value.code == -75
+    # the failed run stays inspectable and every entry point stays memory-safe: ncells() is
+    # clamped to the K columns that exist (ctl->ncols counts the refused requests too), k_crash /
+    # k_digest / k_leave never index a column past K (round-2 r02_k illegal memory access)
+    c.crash([6, 7])
+    c.leave([8])
+    dg = c.digest()
+    assert len(dg) == 2
+    for obs in (0, 9, 63):
+        assert c.view(obs).shape == (64,)
+        assert c.deadlines(obs).shape == (64,)
+    pres, last = c.presence()
+    assert pres.shape == (64,) and last.shape == (64,)
+    with pytest.raises(SwimError) as ei2:  # still failed, still loud, and no HIP error
+        c.step(1)
+    assert ei2.value.code == -75
 
 
 def test_philox_device_matches_oracle():
