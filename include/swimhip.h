@@ -112,6 +112,10 @@ typedef struct swim_config {
   int32_t device;           /* HIP device ordinal the handle lives on                     */
   uint32_t shard_rank;      /* observer-row shard of this handle (0 .. shard_world-1)     */
   uint32_t shard_world;     /* shards of the cluster (0 or 1 = unsharded); see swim_shard_step */
+  uint32_t gossip_batching; /* 0 = gossips one member creates in one phase share one ring slot while
+                               no probabilistic loss is set (exact: they travel identically, DESIGN.md
+                               §3.12); 1 = one slot per gossip always                             */
+  uint32_t record_capacity; /* gossip records live at once in batch slots (power of two; 0 = default) */
 } swim_config;
 
 typedef struct swim_stats {
@@ -155,6 +159,8 @@ typedef struct swim_stats {
   uint64_t apply_subjects;    /* updateMembership calls (one per subject per receiver)        */
   uint64_t fd_dead_events;    /* FailureDetectorEvent(DEAD): an ACK with DEST_GONE (FDI:231-235,383) */
   uint64_t apply_spills;      /* subjects k_gossip_apply merged through the global inbox (LDS hash full); 0 in the oracle */
+  uint64_t apply_records;     /* gossip records of batch slots expanded by k_gossip_apply; 0 in the oracle */
+  uint64_t live_gossip_records; /* gossips held in the live ring slots (live_gossip_slots counts batches) */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -165,7 +171,10 @@ int swim_create(const swim_config* cfg, swim_handle** out);
 int swim_destroy(swim_handle* h);
 
 /* Fault injection (NetworkEmulator.java:81-98,166-180): uniform outbound loss in basis
- * points (0..10000; 10000 = blockAllOutbound). */
+ * points (0..10000; 10000 = blockAllOutbound). A probabilistic loss (0 < loss < 10000) draws
+ * per gossip, so batch slots cannot follow it: setting one while a slot holding several gossips
+ * is still live returns SWIM_EINVAL (set the loss before the gossips are created, or create the
+ * handle with gossip_batching = 1). */
 int swim_set_loss(swim_handle* h, uint32_t loss_bp);
 /* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
  * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */

@@ -57,6 +57,7 @@ struct swim_handle {
   // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
   uint32_t apply_blocks = 1;
   size_t apply_lds = 0;
+  uint32_t CC = 0;  // record ring of the gossip batches
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
@@ -235,8 +236,14 @@ int check_overflow(swim_handle* h);
 
 // Order the phase's gossips by (subject, record) and commit them: one k_commit launch. stg != nullptr: the local stage, counted on the device (no host round trip); otherwise
 // the n gathered gossips already in h->ck[0] / h->cv[0].
-int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n, uint32_t bound = NONE) {
+int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, uint32_t bound = NONE) {
   hipStream_t s = h->stream;
+  KP P = P0;
+  if (P.batch_commit && !h->base.batched) {  // from now on the ring may hold batch slots
+    h->base.batched = 1u;
+    h->cur.batched = 1u;
+    P.batched = 1u;
+  }
   CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u, 0u};
   C.npass = (32u + bitlen(h->N - 1u) + 7u) / 8u;  // key = subject << 32 | record
   // launch the radix kernels only when the batch may need them: the sharded batch size is known
@@ -255,9 +262,14 @@ int commit_sorted(swim_handle* h, const KP& P, const uint4* stg, uint32_t n, uin
                            even ? C.v0 : C.v1, even ? C.k1 : C.k0, even ? C.v1 : C.v0);
       }
       const bool in0 = (C.npass & 1u) == 0u;
-      hipLaunchKernelGGL(k_rs_commit, dim3(1024), dim3(256), 0, s, P, stg, n, in0 ? C.k0 : C.k1, in0 ? C.v0 : C.v1);
-      hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n);
+      const unsigned long long* ks = in0 ? C.k0 : C.k1;
+      hipLaunchKernelGGL(k_rs_slots, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C, ks);
+      hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(CS_THREADS), 0, s, C.stat, C.stat + C.maxt, C.maxt);
+      hipLaunchKernelGGL(k_rs_commit, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C, ks, in0 ? C.v0 : C.v1);
+      hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n, C);
     }
+    // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights)
+    if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P);
   });
   return SWIM_OK;
 }
@@ -304,7 +316,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
     const uint32_t c = (uint32_t)((x->recv_counts[q] - tail) / 4);
     offs[q] = (uint32_t)(q * x->recv_stride + 4ull * c);
     if (c)
-      hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(c, 256)), dim3(256), 0, s,
+      hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(c, 256)), dim3(256), 0, s, P,
                          reinterpret_cast<const uint4*>(xr + q * x->recv_stride), c, total, h->ck[0], h->cv[0]);
     total += c;
   }
@@ -441,7 +453,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 1, "k_gossip_pull", [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
-          hipLaunchKernelGGL(k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
+          if (P.batched)  // batch slots in the ring: expand their records
+            hipLaunchKernelGGL(k_gossip_apply_b, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
+          else
+            hipLaunchKernelGGL(k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
         });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
@@ -592,6 +607,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
   if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
     return SWIM_EINVAL;
+  if (c.gossip_batching > 1u ||
+      (c.record_capacity && ((c.record_capacity & (c.record_capacity - 1)) || c.record_capacity < 1024u)))
+    return SWIM_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EHIP;
   if (c.device < 0 || c.device >= ndev) return SWIM_EINVAL;
@@ -662,6 +680,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply_b),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
@@ -682,7 +702,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.nxk = c.mode == 1 ? 1u : 0u;
   P.W = P.nxk ? c.tracked_subjects : N;  // cells per view row
   P.blx = nullptr;
-  P.stg_cap = h->GC;
+  // gossip records: batch slots keep their gossips in a ring of their own; a phase stages at most
+  // as many gossips as can be live (the commit raises OV_GOSSIP beyond the ring)
+  h->CC = c.record_capacity ? c.record_capacity
+                            : std::min<uint32_t>(1u << 24, std::max<uint32_t>(1u << 21, 4u * h->GC));
+  P.cmask = h->CC - 1u;
+  P.batch_commit = c.gossip_batching == 0 ? 1u : 0u;  // no loss set yet
+  P.batched = 0u;  // set by the first batch commit (swim_api: commit_sorted)
+  P.stg_cap = h->CC;
   P.loss_mode = 0;
   P.loss_thr = 0;
   P.link = nullptr;
@@ -735,6 +762,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.npeers, N);
   ALLOC(P.g_sr, h->GC);
   ALLOC(P.g_hash, h->GC);
+  ALLOC(P.g_cref, h->GC);
+  ALLOC(P.c_sr, h->CC);
+  ALLOC(P.c_hash, h->CC);
+  ALLOC(P.wsum, h->GC / 32);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
   ALLOC(P.nsum, NL * NSUM);
@@ -876,6 +907,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.g_cref, 0, (size_t)h->GC * 8, s);
+  (void)hipMemsetAsync(P.wsum, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.lack_round, (size_t)N, NONE);
@@ -925,6 +958,20 @@ int swim_destroy(swim_handle* h) {
 int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
   if (!h || loss_bp > 10000) return SWIM_EINVAL;
   KP& P = h->base;
+  if (loss_bp > 0 && loss_bp < 10000 && P.batched) {
+    // NetworkEmulator draws per message, i.e. per gossip: a live slot of several gossips would
+    // have to split. Refuse loudly instead.
+    uint32_t* d = reinterpret_cast<uint32_t*>(h->d_digest);  // scratch word
+    HIPC(h, hipMemsetAsync(d, 0, 4, h->stream));
+    hipLaunchKernelGGL(k_multi_live, dim3(256), dim3(256), 0, h->stream, P, d);
+    uint32_t multi = 0;
+    HIPC(h, hipMemcpyAsync(&multi, d, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    if (multi)
+      return fail(h, SWIM_EINVAL,
+                  "swim_set_loss: a probabilistic loss draws per gossip, but live ring slots hold batches of several "
+                  "gossips (DESIGN.md 3.12): set the loss before they are created, or create with gossip_batching = 1");
+  }
   if (loss_bp == 0) {
     P.loss_mode = 0;
   } else if (loss_bp >= 10000) {
@@ -933,6 +980,7 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
     P.loss_mode = 1;
     P.loss_thr = (uint32_t)(((uint64_t)loss_bp << 32) / 10000u);
   }
+  P.batch_commit = (h->cfg.gossip_batching == 0 && P.loss_mode != 1u) ? 1u : 0u;
   return SWIM_OK;
 }
 
@@ -1286,6 +1334,16 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->apply_subjects = stats[ST_APPLY_SUBJ];
   out->fd_dead_events = stats[ST_FD_DEAD_EV];
   out->apply_spills = stats[ST_APPLY_SPILL];
+  out->apply_records = stats[ST_APPLY_RECS];
+  {  // gossips in the live slots: the record ring from the oldest live slot's first record
+    uint32_t c_lo = ctl.ccount;
+    if (ctl.gcount != ctl.glo && ctl.gcount - ctl.glo <= h->GC) {
+      uint2 cr;
+      HIPC(h, hipMemcpy(&cr, h->base.g_cref + (ctl.glo & (h->GC - 1)), 8, hipMemcpyDeviceToHost));
+      c_lo = cr.x;
+    }
+    out->live_gossip_records = ctl.ccount - c_lo;
+  }
   uint64_t nc = 0;
   for (uint32_t j = 0; j < h->N; ++j)
     if (!alive[j]) nc += pres[j];
@@ -1355,24 +1413,27 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
   Ctl ctl;
   HIPC(h, hipMemcpyAsync(&ctl, h->base.ctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
-  const uint32_t GC = h->GC;
-  std::vector<uint32_t> bits(GC / 32), cr(GC), hs(GC);
+  const uint32_t GC = h->GC, CC = h->CC;
+  std::vector<uint32_t> bits(GC / 32), ch(CC);
+  std::vector<uint2> cref(GC);
   std::vector<uint8_t> d(GC);
   HIPC(h, hipMemcpy(bits.data(), h->base.hb + lr * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(d.data(), h->base.hd + lr * GC, (size_t)GC, hipMemcpyDeviceToHost));
-  HIPC(h, hipMemcpy(cr.data(), h->base.g_create, (size_t)GC * 4, hipMemcpyDeviceToHost));
-  HIPC(h, hipMemcpy(hs.data(), h->base.g_hash, (size_t)GC * 4, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(cref.data(), h->base.g_cref, (size_t)GC * 8, hipMemcpyDeviceToHost));
+  HIPC(h, hipMemcpy(ch.data(), h->base.c_hash, (size_t)CC * 4, hipMemcpyDeviceToHost));
   uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;
   const uint32_t rnow = (uint32_t)(h->period * h->G);  // next round to run
   if (hi - lo > GC) lo = hi - GC;
   for (uint32_t id = lo; id < hi; ++id) {
     const uint32_t s = id & (GC - 1);
     if (!((bits[s >> 5] >> (s & 31)) & 1u)) continue;
-    if (n < cap) {
-      out_hash[n] = hs[s];
-      out_inf[n] = rnow - (uint8_t)(rnow - d[s]);  // hd = infection round mod 2^8, age < 2^8
+    for (uint32_t x = cref[s].x; x != cref[s].y; ++x) {  // every gossip of the slot's batch
+      if (n < cap) {
+        out_hash[n] = ch[x & (CC - 1)];
+        out_inf[n] = rnow - (uint8_t)(rnow - d[s]);  // hd = infection round mod 2^8, age < 2^8
+      }
+      ++n;
     }
-    ++n;
   }
   *n_out = n;
   return SWIM_OK;

@@ -57,6 +57,7 @@ enum StatIdx : int {
   ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
   ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
   ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
+  ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply expanded into its LDS table
   ST_COUNT
 };
 
@@ -84,7 +85,7 @@ enum IfromOverflow : uint32_t {
 constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
-constexpr uint32_t STAT_STRIDE = 32;  // u64 per shard (256 B), >= ST_COUNT
+constexpr uint32_t STAT_STRIDE = 64;  // u64 per shard (512 B), >= ST_COUNT
 static_assert(ST_COUNT <= (int)STAT_STRIDE, "stat shard too small");
 
 struct Ctl {
@@ -112,6 +113,9 @@ struct Ctl {
   uint32_t ncols;        // N x K: columns allocated
   uint32_t alive_count;  // alive members (N x K: presence of untracked subjects)
   uint32_t ov_detail;    // which infectedFrom bound OV_IFROM hit (IfromOverflow bits)
+  // gossip batches: records ever committed (the record ring's unwrapped end),
+  // the ring id count before the last commit, and the batches the last chip-wide commit made
+  uint32_t ccount, g_prev, rs_ncls, rsv1;
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -191,7 +195,19 @@ struct KP {
   uint32_t* sync_fd;
   uint32_t* peers;   // [N][f] gossip peers chosen this round
   uint32_t* npeers;  // [N]
-  uint2* g_sr;        // [GC] (subject, packed record) of each gossip
+  // Gossip batches. A ring slot holds one batch: the gossips one origin created
+  // in one commit phase while no probabilistic loss is set (they travel identically), or a single
+  // gossip (loss set, or batching off). Its records live in the record ring c_sr / c_hash at
+  // absolute indices [g_cref.x, g_cref.y).
+  uint2* g_cref;      // [GC] record range of each slot (absolute indices into c_sr, mod CC)
+  uint2* c_sr;        // [CC] (subject, packed record) of every gossip of a live slot
+  uint32_t* c_hash;   // [CC] its canonical id hash (GossipProtocolImpl.generateGossipId, :211-213)
+  uint32_t cmask;     // CC - 1
+  uint32_t* wsum;     // [GC/32] gossips in a word's slots (counters weight a slot by its gossips)
+  uint32_t batch_commit;  // this phase's commit groups gossips into batches by origin (loss_mode != 1)
+  uint32_t batched;       // batching is on and has been used: counters weight slots, apply expands records
+  uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
+                      // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
                       // by (subject, record), so within a run records ascend)
   uint32_t* g_hash;
@@ -315,6 +331,22 @@ __device__ __forceinline__ uint32_t ncells(const KP& P) {
   if (!P.nxk) return P.N;
   const uint32_t n = P.ctl->ncols;
   return n < P.W ? n : P.W;
+}
+
+// gossips in the slots `bits` of bitmap word ws (GossipRequest / receipt counters count gossips,
+// not slots): popcount while every slot holds one gossip, else the word's total when the mask
+// covers it, else the slots' record ranges one by one
+__device__ __forceinline__ uint32_t slot_gossips(const KP& P, uint32_t ws, uint32_t bits) {
+  if (!P.batched || !bits) return (uint32_t)__popc(bits);
+  if (bits == 0xFFFFFFFFu) return P.wsum[ws];
+  uint32_t n = 0;
+  while (bits) {
+    const uint32_t b = (uint32_t)__builtin_ctz(bits);
+    bits &= bits - 1u;
+    const uint2 r = P.g_cref[ws * 32u + b];
+    n += r.y - r.x;
+  }
+  return n;
 }
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {

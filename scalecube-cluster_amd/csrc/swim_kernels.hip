@@ -158,42 +158,79 @@ __global__ void k_crash(KP P, uint32_t c) {
   }
 }
 
-// Second half of emit_gossip, step 1: sort keys of the phase's gossips, (subject, record) and
-// (origin, id hash). Sorting only permutes ring slots, which nothing observable depends on.
-__global__ void k_stage_keys(const uint4* ents, uint32_t n, uint32_t out_off, unsigned long long* keys,
+// Second half of emit_gossip, step 1: sort keys of the phase's gossips. A batch commit
+//  sorts by (origin, subject), so each origin's gossips form one run that becomes
+// one ring slot; a one-gossip-per-slot commit sorts by (subject, record), so a subject's gossips
+// take consecutive slots with ascending records (k_gossip_apply's subject runs). Sorting only
+// permutes ring slots, which nothing observable depends on.
+__device__ __forceinline__ unsigned long long stg_key(const KP& P, uint4 e) {  // e = {origin, subject, record, hash}
+  return P.batch_commit ? (((unsigned long long)e.x << 32) | e.y) : (((unsigned long long)e.y << 32) | e.z);
+}
+__device__ __forceinline__ unsigned long long stg_val(const KP& P, uint4 e) {
+  return P.batch_commit ? (((unsigned long long)e.z << 32) | e.w) : (((unsigned long long)e.x << 32) | e.w);
+}
+// back to {origin, subject, record, hash}
+__device__ __forceinline__ uint4 kv_decode(const KP& P, unsigned long long k, unsigned long long v) {
+  return P.batch_commit ? make_uint4((uint32_t)(k >> 32), (uint32_t)k, (uint32_t)(v >> 32), (uint32_t)v)
+                        : make_uint4((uint32_t)(v >> 32), (uint32_t)(k >> 32), (uint32_t)k, (uint32_t)v);
+}
+// does sorted element i (key k, predecessor kp) open a new ring slot? a batch at each new origin,
+// otherwise every gossip
+__device__ __forceinline__ bool slot_start(const KP& P, uint32_t i, unsigned long long kp, unsigned long long k) {
+  return i == 0u || !P.batch_commit || (kp >> 32) != (k >> 32);
+}
+
+__global__ void k_stage_keys(KP P, const uint4* ents, uint32_t n, uint32_t out_off, unsigned long long* keys,
                              unsigned long long* vals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const uint4 e = ents[i];
-    keys[out_off + i] = ((unsigned long long)e.y << 32) | e.z;
-    vals[out_off + i] = ((unsigned long long)e.x << 32) | e.w;
+    keys[out_off + i] = stg_key(P, e);
+    vals[out_off + i] = stg_val(P, e);
   }
 }
 
-// Step 2: sorted gossip i gets id gcount + i (every shard commits the same sorted batch, so
-// the ring stays replicated), runs of one subject are marked in runw, and the origin's shard
-// marks the gossip held with infectionPeriod = create_round.
-__device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t i, unsigned long long k,
-                                           unsigned long long v, bool start) {
+// Step 2: sorted gossip i is record c0 + i of the record ring, in slot g0 + ci (ci = the slots
+// opened before it, minus one); every shard commits the same sorted batch, so the ring stays
+// replicated. The element that opens a slot publishes it (record range start, first record, id
+// hash, creation round, run mark) and, on the origin's shard, marks it held with infectionPeriod
+// = create_round; the element that closes it sets the range's end. One-gossip slots mark runs of
+// one subject in runw; a batch slot is a run of its own.
+__device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t c0, uint32_t i, uint32_t ci,
+                                           unsigned long long k, unsigned long long v, bool open, bool close,
+                                           bool run) {
   const uint32_t W32 = P.GC >> 5;
-  const uint32_t subject = (uint32_t)(k >> 32), record = (uint32_t)k;
-  const uint32_t origin = (uint32_t)(v >> 32), hash = (uint32_t)v;
-  const uint32_t id = g0 + i;
+  const uint4 e = kv_decode(P, k, v);
+  const uint32_t origin = e.x, subject = e.y, record = e.z, hash = e.w;
+  const uint32_t x = c0 + i;  // absolute record index
+  P.c_sr[x & P.cmask] = make_uint2(subject, record);
+  P.c_hash[x & P.cmask] = hash;
+  const uint32_t id = g0 + ci;
   const uint32_t s = id & P.gmask;
+  uint32_t* cref = reinterpret_cast<uint32_t*>(P.g_cref);
+  // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
+  if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
+  if (close) {
+    cref[2u * s + 1u] = x + 1u;
+    // the live records start at the oldest live slot's first one: they must fit the record ring
+    const uint32_t glo = P.ctl->glo;
+    const uint32_t c_lo = (g0 != glo && g0 - glo <= P.GC) ? cref[2u * (glo & P.gmask)] : c0;
+    if (x + 1u - c_lo > P.cmask + 1u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  }
+  if (!open) return;
   // the live id range must stay below GC - 64 slots so bitmap words never alias across the
   // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
   if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  cref[2u * s] = x;
   P.g_sr[s] = make_uint2(subject, record);
   P.g_hash[s] = hash;
   P.g_create[s] = P.create_round;
-  if (start)
+  if (run)
     atomicOr(&P.runw[s >> 5], 1u << (s & 31u));
   else
     atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
   // a reused word's stale maximum is older than any live creation round, so max() resets it
   if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
-  // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
-  if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
   if (is_local(P, origin)) {
     P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
     const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
@@ -263,6 +300,39 @@ __device__ __forceinline__ uint32_t cs_block_scan(uint32_t v, uint32_t* total, u
   return base + x - v;
 }
 
+// Elements 4t .. 4t+3 of a sorted block of CS_PER * CS_THREADS keys (at `base` of the batch,
+// `cbase` slots opened before the block) committed by thread t; returns the slots the block opened.
+// key(i) reads sorted key i of the batch (LDS or global).
+template <typename KeyF, typename ValF>
+__device__ __forceinline__ uint32_t commit_block(const KP& P, uint32_t g0, uint32_t c0, uint32_t n, uint32_t base,
+                                                 uint32_t cbase, KeyF key, ValF val, uint32_t* lds) {
+  const uint32_t t = threadIdx.x;
+  unsigned long long kk[CS_PER + 1];
+  bool op[CS_PER + 1];
+  uint32_t cnt = 0;
+  const uint32_t i0 = base + CS_PER * t;
+  unsigned long long kp = (i0 > 0u && i0 <= n) ? key(i0 - 1u) : 0ull;
+#pragma unroll
+  for (uint32_t q = 0; q <= CS_PER; ++q) {
+    const uint32_t i = i0 + q;
+    kk[q] = i < n ? key(i) : 0ull;
+    op[q] = i < n && slot_start(P, i, q ? kk[q - 1] : kp, kk[q]);
+    if (q < CS_PER && op[q]) ++cnt;
+  }
+  uint32_t tot;
+  uint32_t ci = cbase + cs_block_scan(cnt, &tot, lds);
+#pragma unroll
+  for (uint32_t q = 0; q < CS_PER; ++q) {
+    const uint32_t i = i0 + q;
+    if (i >= n) break;
+    if (op[q]) ++ci;
+    const unsigned long long prev = q ? kk[q - 1] : kp;
+    const bool run = P.batch_commit || i == 0u || (prev >> 32) != (kk[q] >> 32);  // a subject run starts
+    commit_one(P, g0, c0, i, ci - 1u, kk[q], val(i), op[q], i + 1u == n || op[q + 1], run);
+  }
+  return tot;
+}
+
 __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, uint32_t n_host, CSort C) {
   __shared__ unsigned long long s_key[CS_SMALL];
   __shared__ uint32_t s_idx[CS_SMALL];
@@ -280,19 +350,13 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
       for (uint32_t i = t; i < nt * 256u; i += CS_THREADS) C.stat[(size_t)p * C.maxt * 256u + i] = 0u;
     return;
   }
-  const uint32_t g0 = P.ctl->gcount;
+  __shared__ uint32_t s_lds[CS_WAVES];
+  const uint32_t g0 = P.ctl->gcount, c0 = P.ctl->ccount;
   uint32_t m = 1;
   while (m < n) m <<= 1;
   for (uint32_t i = t; i < m; i += CS_THREADS) {
     unsigned long long k = ~0ull;
-    if (i < n) {
-      if (stg) {
-        const uint4 e = stg[i];
-        k = ((unsigned long long)e.y << 32) | e.z;
-      } else {
-        k = C.k0[i];
-      }
-    }
+    if (i < n) k = stg ? stg_key(P, stg[i]) : C.k0[i];
     s_key[i] = k;
     s_idx[i] = i;
   }
@@ -315,19 +379,15 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
       }
       __syncthreads();
     }
-  for (uint32_t i = t; i < n; i += CS_THREADS) {
-    unsigned long long v;
-    if (stg) {
-      const uint4 e = stg[s_idx[i]];
-      v = ((unsigned long long)e.x << 32) | e.w;
-    } else {
-      v = C.v0[s_idx[i]];
-    }
-    commit_one(P, g0, i, s_key[i], v, i == 0 || (s_key[i - 1] >> 32) != (s_key[i] >> 32));
-  }
+  static_assert(CS_SMALL <= CS_PER * CS_THREADS, "k_commit: one commit_block covers the LDS sort");
+  const uint32_t nslots = commit_block(
+      P, g0, c0, n, 0u, 0u, [&](uint32_t i) { return s_key[i]; },
+      [&](uint32_t i) { return stg ? stg_val(P, stg[s_idx[i]]) : C.v0[s_idx[i]]; }, s_lds);
   __syncthreads();
   if (t == 0) {
-    P.ctl->gcount = g0 + n;
+    P.ctl->g_prev = g0;
+    P.ctl->gcount = g0 + nslots;
+    P.ctl->ccount = c0 + n;
     if (stg) P.ctl->stg_count = 0u;
   }
 }
@@ -346,9 +406,9 @@ __global__ void __launch_bounds__(CS_THREADS) k_rs_hist(KP P, const uint4* stg, 
     unsigned long long k;
     if (stg) {
       const uint4 e = stg[i];
-      k = ((unsigned long long)e.y << 32) | e.z;
+      k = stg_key(P, e);
       C.k0[i] = k;
-      C.v0[i] = ((unsigned long long)e.x << 32) | e.w;
+      C.v0[i] = stg_val(P, e);
     } else {
       k = C.k0[i];
     }
@@ -450,20 +510,68 @@ __global__ void __launch_bounds__(CS_THREADS) k_rs_pass(KP P, const uint4* stg, 
   }
 }
 
-__global__ void __launch_bounds__(256) k_rs_commit(KP P, const uint4* stg, uint32_t n_host,
-                                                   const unsigned long long* k, const unsigned long long* v) {
+// Slots opened per tile of the sorted batch (C.stat is free once the passes are done: tile
+// counts in stat[0 .. nt), their exclusive scan in stat[maxt .. maxt + nt), k_excl_scan)
+__global__ void __launch_bounds__(CS_THREADS) k_rs_slots(KP P, const uint4* stg, uint32_t n_host, CSort C,
+                                                         const unsigned long long* k) {
+  __shared__ uint32_t s_lds[CS_WAVES];
   const uint32_t n = cs_n(P, stg, n_host);
-  if (n <= CS_SMALL) return;
-  const uint32_t g0 = P.ctl->gcount;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    commit_one(P, g0, i, k[i], v[i], i == 0 || (k[i - 1] >> 32) != (k[i] >> 32));
+  if (n <= CS_SMALL || blockIdx.x * CS_TILE >= n) return;
+  const uint32_t i0 = blockIdx.x * CS_TILE + CS_PER * threadIdx.x;
+  uint32_t cnt = 0;
+  for (uint32_t q = 0; q < CS_PER; ++q) {
+    const uint32_t i = i0 + q;
+    if (i < n && slot_start(P, i, i ? k[i - 1] : 0ull, k[i])) ++cnt;
+  }
+  uint32_t tot;
+  cs_block_scan(cnt, &tot, s_lds);
+  if (threadIdx.x == 0) C.stat[blockIdx.x] = tot;
 }
 
-__global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host) {
+__global__ void __launch_bounds__(CS_THREADS) k_rs_commit(KP P, const uint4* stg, uint32_t n_host, CSort C,
+                                                          const unsigned long long* k, const unsigned long long* v) {
+  __shared__ uint32_t s_lds[CS_WAVES];
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n <= CS_SMALL || blockIdx.x * CS_TILE >= n) return;
+  commit_block(P, P.ctl->gcount, P.ctl->ccount, n, blockIdx.x * CS_TILE, C.stat[C.maxt + blockIdx.x],
+               [&](uint32_t i) { return k[i]; }, [&](uint32_t i) { return v[i]; }, s_lds);
+}
+
+__global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
   const uint32_t n = cs_n(P, stg, n_host);
   if (n <= CS_SMALL) return;
-  P.ctl->gcount += n;
+  const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
+  P.ctl->g_prev = P.ctl->gcount;
+  P.ctl->gcount += C.stat[C.maxt + nt - 1u] + C.stat[nt - 1u];
+  P.ctl->ccount += n;
   if (stg) P.ctl->stg_count = 0u;
+}
+
+// Does a possibly-live ring slot hold a batch of several gossips? (swim_set_loss)
+__global__ void k_multi_live(KP P, uint32_t* out) {
+  const uint32_t lo = P.ctl->glo, hi = P.ctl->gcount;
+  const uint32_t n = hi - lo > P.GC ? P.GC : hi - lo;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint2 r = P.g_cref[(lo + i) & P.gmask];
+    if (r.y - r.x > 1u) atomicOr(out, 1u);
+  }
+}
+
+// Gossips per bitmap word (wsum) of the words the last commit wrote slots into
+__global__ void k_commit_wsum(KP P) {
+  const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount;
+  const uint32_t w0 = g0 >> 5, w1 = (g1 + 31u) >> 5;
+  const uint32_t* cref = reinterpret_cast<const uint32_t*>(P.g_cref);
+  for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += gridDim.x * blockDim.x) {
+    uint32_t sum = 0;
+    for (uint32_t b = 0; b < 32u; ++b) {
+      const uint32_t id = (w << 5) + b;
+      if ((int32_t)(g1 - id) <= 0) continue;  // not created yet (the word's slots from earlier commits count)
+      const uint32_t s = id & P.gmask;
+      sum += cref[2u * s + 1u] - cref[2u * s];
+    }
+    P.wsum[w & ((P.GC >> 5) - 1u)] = sum;
+  }
 }
 
 // Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
@@ -1109,7 +1217,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
             wbr[DBG_IDX(k, W32, "select wbr")] = win;
           }
           win_l |= win != 0u;
-          winbits += (uint32_t)__popc(win);
+          winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
         }
         }
       }
@@ -1213,7 +1321,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
             wbr[DBG_IDX(k, W32, "select wbr")] = win;
           }
           win_l |= win != 0u;
-          winbits += (uint32_t)__popc(win);
+          winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
         }
       }
       if (lack_ok) {  // positions k0 + 256 jq + 4 lane + i: eight lanes fill one bitmap word
@@ -1442,7 +1550,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       const uint32_t ea = P.act[ap.y];
       if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
       const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t);
-      if (supp) removed += (uint32_t)__popc(atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
+      if (supp) removed += slot_gossips(P, wi & (W32 - 1u), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
       removed_alive += removed;
@@ -1802,8 +1910,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
     }
   }
   if (lane == 0) P.in_cnt[p] = 0u;  // ready for the next round
-  add_stat(P, ST_G_PROBES, probes);
-  add_stat(P, ST_GOSSIP_RECEIPTS, receipts);
+  add_stat(P, ST_G_PROBES, probes);  // (receipts are counted by k_gossip_apply, in gossips)
   add_stat(P, ST_G_PULLW, words);
 }
 
@@ -1879,7 +1986,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
-  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0;
+  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrcpt = 0;
 #ifdef SWIM_APPLY_PROF
   unsigned long long tp = wall_clock64();
 #define APPLY_MARK(q)                                                                      \
@@ -2100,6 +2207,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     }
     if (tid == 0) atomicAdd(&P.held[p], total);
     nspills += tid == 0 ? nsp : 0u;
+    nrcpt += tid == 0 ? total : 0u;  // one gossip per slot here (no batch slots)
     __syncthreads();  // the table is reused by the next receiver
     APPLY_MARK(3)
   }
@@ -2108,6 +2216,322 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   add_stat(P, ST_APPLY_RUNS, nruns);
   add_stat(P, ST_APPLY_SUBJ, nsubj);
   add_stat(P, ST_APPLY_SPILL, nspills);
+  add_stat(P, ST_GOSSIP_RECEIPTS, nrcpt);
+  flush_tally(P, T);
+}
+
+// ---- batch slots: k_gossip_apply for rings that hold gossip batches ----
+// The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
+// the lanes' exclusive offsets, non-decreasing; every lane calls it, each with its own q).
+__device__ __forceinline__ uint32_t wave_owner(uint32_t off, uint32_t q) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1) {
+    const uint32_t o = __shfl(off, (int)(lo + step), 64);
+    if (o <= q) lo += step;
+  }
+  return lo;
+}
+
+// position of the k-th (0-based) set bit of m, k < popcount(m)
+__device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 16; w > 0; w >>= 1) {
+    const uint32_t c = (uint32_t)__popc(m & ((1u << w) - 1u));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
+// the highest received slot of every subject run (runw: run starts; a batch slot is a run of
+// its own): the slot whose records carry the run's lattice max
+__device__ __forceinline__ uint32_t run_tops(uint32_t bits, uint32_t rs) {
+  rs |= 1u;
+  uint32_t rm = 0;
+  while (bits) {
+    const uint32_t b = 31u - (uint32_t)__builtin_clz(bits);
+    const uint32_t below = b == 31u ? 0xFFFFFFFFu : ((2u << b) - 1u);
+    const uint32_t a = 31u - (uint32_t)__builtin_clz(rs & below);
+    rm |= 1u << b;
+    bits &= (1u << a) - 1u;
+  }
+  return rm;
+}
+
+// onGossipReq's new-gossip branch for one receipt word of receiver p: it holds the slots now
+// (GossipProtocolImpl.java:175-178), with infectionPeriod r + 1, and the word's age bounds and
+// liveness move with them (k_gossip_apply's `process`, without the record merge)
+__device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t ws, uint32_t bits, uint32_t prior,
+                                             uint4 v0, uint4 v1) {
+  const uint32_t r = P.round, W32 = P.GC >> 5;
+  if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
+  const size_t mi = lrow(P, p) * W32 + ws;
+  P.hb[mi] = prior | bits;
+  P.mmax[mi] = (uint8_t)(r + 1u);
+  if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);
+  uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
+    if (!nb16) continue;
+    const uint32_t rb = ((r + 1u) & 0xFFu) * 0x01010101u;
+    if (!((prior >> (16 * q)) & 0xFFFFu)) {
+      dp[q] = make_uint4(rb, rb, rb, rb);
+      continue;
+    }
+    uint4 v = q == 0 ? v0 : v1;
+    const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
+    const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
+    v.x = (v.x & ~m0) | (rb & m0);
+    v.y = (v.y & ~m1) | (rb & m1);
+    v.z = (v.z & ~m2) | (rb & m2);
+    v.w = (v.w & ~m3) | (rb & m3);
+    dp[q] = v;
+  }
+}
+
+// k_gossip_apply when the ring holds batch slots (P.batched): a received slot stands for all
+// the gossips of its batch, so its record range is expanded into the LDS table. Two passes per
+// receiver: (1) holdings, infection rounds and age bounds of every receipt word, and the number
+// of records the received run tops carry (sizes the table); (2) the records themselves, lattice-
+// max per subject. Work is spread over the wave, not the word: each wave's run tops, then their
+// records, are flattened across its 64 lanes (wave_owner), and receipt words are dealt to the
+// waves round-robin, so one word holding a large batch does not serialize a lane.
+// Then one updateMembership per subject, as in k_gossip_apply.
+__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
+  SWIM_GUARD(P);
+  extern __shared__ uint32_t s_dyn[];
+  const uint32_t hcap_log = P.apply_hlog, hcap = 1u << hcap_log;
+  const uint32_t pres_words = P.N <= 32u * PRES_WORDS ? (P.N + 31u) / 32u : 0u;
+  const bool pres = pres_words != 0u;
+  uint32_t* s_key = s_dyn;
+  uint32_t* s_val = s_dyn + hcap;
+  uint32_t* s_spl = s_dyn + 2u * hcap;
+  uint32_t* s_pres = s_spl + SPILL_CAP;
+  __shared__ uint32_t s_nspill;
+  __shared__ uint32_t s_part[16];
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63u, nw = nthr >> 6;
+  const uint32_t slot_of_thread = lane * nw + (tid >> 6);  // items dealt to the waves round-robin
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
+  const uint32_t W32 = P.GC >> 5;
+  Tally T;
+  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrecs = 0, nrcpt = 0;
+  for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+    const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
+    uint32_t* nbr = P.nb + lrow(P, p) * W32;
+    const uint32_t nsw = (n_act + 31u) >> 5;
+    const bool summ = nsw <= NSUM;
+    const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
+    const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
+    if (tid == 0) s_nspill = 0u;
+    if (pres)
+      for (uint32_t t = tid; t < pres_words; t += nthr) s_pres[t] = 0u;
+    // the list positions with receipts, compacted from the summary (at the front of the table
+    // area, free until the table is sized)
+    uint32_t n_comp = 0;
+    if (summ) {
+      for (uint32_t c0 = 0; c0 < nsw; c0 += nthr) {
+        const uint32_t t = c0 + tid;
+        uint32_t bits = t < nsw ? sumr[t] : 0u;
+        uint32_t tot;
+        uint32_t o = n_comp + block_excl_scan1024((uint32_t)__popc(bits), &tot, s_part);
+        while (bits) {
+          s_dyn[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
+          bits &= bits - 1u;
+        }
+        n_comp += tot;
+      }
+      __syncthreads();
+    }
+    const uint32_t* items = s_dyn;
+    const uint32_t n_it = summ ? n_comp : n_act;
+    // pass 1: receive the words; count the records of the run tops
+    uint32_t ent = 0, rc = 0;
+    for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * nthr) {
+      uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
+      uint4 v0[4], v1[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t u = it0 + j * nthr + slot_of_thread;
+        kv[j] = u < n_it ? (summ ? items[u] : u) : NONE;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) ev[j] = kv[j] != NONE ? P.act[kv[j]] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        bv[j] = (kv[j] != NONE && ((ev[j] >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        wsv[j] = (w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u);
+        pv[j] = rv[j] = 0u;
+        if (bv[j]) {
+          pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
+          rv[j] = P.runw[wsv[j]];
+          const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
+          if ((bv[j] & 0xFFFFu) && (pv[j] & 0xFFFFu)) v0[j] = dp[0];
+          if ((bv[j] >> 16) && (pv[j] >> 16)) v1[j] = dp[1];
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        if (bv[j]) {
+          receive_word(P, p, wsv[j], bv[j], pv[j], v0[j], v1[j]);
+          ++nwords;
+        }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t rm = bv[j] ? run_tops(bv[j], rv[j]) : 0u;
+        rc += (uint32_t)(__popc(bv[j]) - __popc(rm));  // slots inside runs: one gossip each
+        nruns += (uint32_t)__popc(rm);
+        uint32_t tot;
+        const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
+        for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
+          const uint32_t q = q0 + lane;
+          const uint32_t o = wave_owner(off, q);
+          const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(wsv[j], (int)o, 64), oo = __shfl(off, (int)o, 64);
+          if (q < tot) {
+            const uint2 cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
+            ent += cr.y - cr.x;
+          }
+        }
+      }
+    }
+    uint32_t E, R;
+    block_excl_scan1024(ent, &E, s_part);
+    block_excl_scan1024(rc + ent, &R, s_part);
+    if (tid == 0) {
+      nrcpt += R;
+      nrecs += E;
+    }
+    uint32_t lg = 6;  // >= 2 slots per record, 64 .. 2^hcap_log
+    while (lg < hcap_log && (1u << lg) < 2u * E) ++lg;
+    const uint32_t hm = (1u << lg) - 1u;
+    // keep the compacted items for pass 2 when they fit behind the table's value half (disjoint
+    // from their place at the front, so a parallel copy is safe); otherwise pass 2 tests the
+    // summary bits again
+    const bool keep = summ && n_comp <= hcap - (1u << lg);
+    uint32_t* items2 = s_dyn + 2u * hcap - n_comp;
+    if (keep)
+      for (uint32_t t = tid; t < n_comp; t += nthr) items2[t] = items[t];
+    __syncthreads();
+    for (uint32_t t = tid; t <= hm; t += nthr) {
+      s_key[t] = NONE;
+      s_val[t] = 0u;
+    }
+    __syncthreads();
+    auto insert = [&](uint2 sr) {
+      uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
+      for (uint32_t q = 0; q < HPROBE; ++q) {
+        const uint32_t prev = atomicCAS(&s_key[h], NONE, sr.x);
+        if (prev == NONE || prev == sr.x) {
+          atomicMax(&s_val[h], sr.y);
+          if (prev == NONE && pres) atomicOr(&s_pres[sr.x >> 5], 1u << (sr.x & 31u));
+          return;
+        }
+        h = (h + 1u) & hm;
+      }
+      // slots only ever fill up, so this subject spills for the whole round
+      if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr.x)], sr.y) == 0u) {
+        const uint32_t o = atomicAdd(&s_nspill, 1u);
+        if (o < SPILL_CAP)
+          s_spl[o] = sr.x;
+        else
+          atomicOr(&P.ctl->overflow, OV_SPILL);
+      }
+    };
+    // pass 2: the records of every received run top into the table; receipts cleared
+    const uint32_t n_it2 = !summ ? n_act : (keep ? n_comp : nsw * 32u);
+    for (uint32_t it0 = 0; it0 < n_it2; it0 += 4u * nthr) {
+      uint32_t kv[4], bv[4], wsv[4], rv[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t u = it0 + j * nthr + slot_of_thread;
+        if (u >= n_it2)
+          kv[j] = NONE;
+        else if (!summ)
+          kv[j] = u;
+        else if (keep)
+          kv[j] = items2[u];
+        else
+          kv[j] = ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t e = kv[j] != NONE ? P.act[kv[j]] : 0u;
+        bv[j] = (kv[j] != NONE && ((e >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
+        wsv[j] = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+        rv[j] = bv[j] ? P.runw[wsv[j]] : 0u;
+        if (bv[j]) nbr[kv[j]] = 0u;  // nb is all-zero between rounds
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t rm = bv[j] ? run_tops(bv[j], rv[j]) : 0u;
+        uint32_t tot;
+        const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
+        for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
+          const uint32_t q = q0 + lane;
+          const uint32_t o = wave_owner(off, q);
+          const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(wsv[j], (int)o, 64), oo = __shfl(off, (int)o, 64);
+          uint2 cr = make_uint2(0u, 0u);
+          if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
+          uint32_t etot;
+          const uint32_t eoff = wave_excl_scan(cr.y - cr.x, &etot);
+          for (uint32_t e0 = 0; e0 < etot; e0 += 64u) {
+            const uint32_t e = e0 + lane;
+            const uint32_t eo = wave_owner(eoff, e);
+            const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
+            if (e < etot) insert(P.c_sr[(bx + e - bo) & P.cmask]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t snap = P.cnt[p];
+    auto apply = [&](uint32_t subj, uint32_t r1) {
+      ++nsubj;
+      const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, snap, T);
+      if (rec) {  // only onSelfMemberDetected spreads here (reason MEMBERSHIP_GOSSIP): one per round
+        emit_gossip(P, p, subj, rec, P.gseq[p]++);
+        ++created;
+      }
+    };
+    if (pres) {  // one updateMembership per subject, in subject order
+      for (uint32_t t = tid; t < pres_words; t += nthr) {
+        uint32_t bits = s_pres[t];
+        while (bits) {
+          const uint32_t subj = 32u * t + (uint32_t)__builtin_ctz(bits);
+          bits &= bits - 1u;
+          uint32_t h = (subj * 0x9E3779B1u) >> (32u - lg);
+          while (s_key[h] != subj) h = (h + 1u) & hm;  // present: placed within HPROBE probes
+          apply(subj, s_val[h]);
+        }
+      }
+    } else {
+      for (uint32_t t = tid; t <= hm; t += nthr)
+        if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
+    }
+    const uint32_t nsp = s_nspill < SPILL_CAP ? s_nspill : SPILL_CAP;
+    if (nsp) __threadfence();
+    for (uint32_t t = tid; t < nsp; t += nthr) {
+      const uint32_t subj = s_spl[t];
+      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
+    }
+    if (tid == 0) atomicAdd(&P.held[p], total);
+    nspills += tid == 0 ? nsp : 0u;
+    __syncthreads();  // the table is reused by the next receiver
+  }
+  add_stat(P, ST_GOSSIPS_CREATED, created);
+  add_stat(P, ST_APPLY_WORDS, nwords);
+  add_stat(P, ST_APPLY_RUNS, nruns);
+  add_stat(P, ST_APPLY_SUBJ, nsubj);
+  add_stat(P, ST_APPLY_SPILL, nspills);
+  add_stat(P, ST_APPLY_RECS, nrecs);
+  add_stat(P, ST_GOSSIP_RECEIPTS, nrcpt);
   flush_tally(P, T);
 }
 

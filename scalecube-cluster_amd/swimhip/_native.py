@@ -56,6 +56,8 @@ class SwimConfig(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("shard_rank", ctypes.c_uint32),
         ("shard_world", ctypes.c_uint32),
+        ("gossip_batching", ctypes.c_uint32),
+        ("record_capacity", ctypes.c_uint32),
     ]
 
 
@@ -109,6 +111,8 @@ STAT_FIELDS = [
     "apply_subjects",
     "fd_dead_events",
     "apply_spills",
+    "apply_records",
+    "live_gossip_records",
 ]
 
 
