@@ -83,9 +83,9 @@ def partition_groups(n, group_size):
     return g
 
 
-def kernel_bytes(name, d, n):
+def kernel_bytes(name, d, rounds_per_period=5):
     """Algorithmic HBM bytes of one kernel class over the timed region.
-    d = stats deltas over the timed region."""
+    d = stats deltas over the timed region; rounds_per_period = G (gossip rounds per period)."""
     if name == "k_sync_merge":  # read SYNC payload row + read table row + write SYNC_ACK payload
         return 12 * d["merge_cells"]
     if name == "k_sync_ack":  # read SYNC_ACK payload row + read table row
@@ -99,8 +99,11 @@ def kernel_bytes(name, d, n):
     if name == "k_gossip_apply":
         # per receipt word: receipts r/w (8 B: read, clear), holdings r/w (8), newest/oldest round (1),
         # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4);
-        # per subject run one ring record (8 B); per subject the table cell and its deadline (8 B)
-        return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
+        # per subject run one ring record (8 B) -- with batch slots the run top's
+        # record range instead (8 B, read in both passes) and 8 B per gossip record it expands;
+        # per subject the table cell and its deadline (8 B)
+        recs = d.get("apply_records", 0)
+        return 93 * d["apply_words"] + (16 if recs else 8) * d["apply_runs"] + 8 * recs + 8 * d["apply_subjects"]
     if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write and
         return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"]  # the view cell read + write
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
@@ -108,12 +111,14 @@ def kernel_bytes(name, d, n):
     # infectedFrom bookkeeping: in-history ring entries (16 B per registration,
     # ~gossip_probes / words per registration is not tracked, so per probe), pruned windows and
     # dense delivery records (a window word read + a word written per active position)
+    # active words per member-round: gossip_scanned counts (member, round) pairs x the round's list
+    act = max(1, d["gossip_scanned"] // max(1, d["fd_probes"] * rounds_per_period))
     if name == "k_gossip_inhist":  # in_list entry + ring entry per registered sender
         return 20 * d["fd_probes"] * 3
-    if name == "k_gossip_pairwin":
-        return 12 * d["infected_pruned_pairs"] * max(1, d["gossip_scanned"] // max(1, d["fd_probes"]))
-    if name == "k_gossip_record":
-        return 12 * d["infected_records"] * max(1, d["gossip_scanned"] // max(1, d["fd_probes"]))
+    if name == "k_gossip_pairwin":  # per pruned pair: the window copied and pruned over the list
+        return 12 * d["infected_pruned_pairs"] * act
+    if name == "k_gossip_record":  # per record: list entry + sender window read + body word written
+        return 12 * d["infected_records"] * act
     return 0
 
 
@@ -134,11 +139,11 @@ def pmc_traffic(kernel, workload="c3", world=1, steps=None, warmup=None):
     return None if k is None else k["fetch_bytes_x2"] + k["write_bytes"]
 
 
-def roofline_of(name, ktimes, d, world):
+def roofline_of(name, ktimes, d, world, rounds_per_period=5):
     """achieved GB/s = algorithmic bytes per launch (kernel_bytes) / average launch time (HIP events
     on the handle's stream), for one kernel class over a measured window."""
     ms, launches = ktimes.get(name, (0.0, 0))
-    byts = kernel_bytes(name, d, 0)
+    byts = kernel_bytes(name, d, rounds_per_period)
     if not launches or not ms or not byts:
         return None
     avg_s = ms / 1e3 / launches
@@ -285,6 +290,8 @@ def main():
 
     w = WORKLOADS[args.workload]
     n = w["n"]
+    pc = preset_config(w["preset"])
+    G = pc.failureDetectorConfig().pingInterval() // pc.gossipConfig().gossipInterval()  # rounds per period
     c = make_cluster(args.workload, local, args.seed, sharded=world > 1)
     log(f"created {args.workload}: N={n}")
     c.step(args.warmup)
@@ -322,10 +329,10 @@ def main():
 
     # dominant kernel + roofline over the timed region
     dom = max((k for k in ktimes if k != "bookkeeping"), key=lambda k: ktimes[k][0])
-    rl = roofline_of(dom, ktimes, d, world) or {"achieved": 0.0, "frac": 0.0, "bytes_per_launch": 0.0,
+    rl = roofline_of(dom, ktimes, d, world, G) or {"achieved": 0.0, "frac": 0.0, "bytes_per_launch": 0.0,
                                                  "avg_launch_ms": 0.0, "launches": 0}
     fracs = {k: round(v["frac"], 4) for k in ktimes if k != "bookkeeping"
-             for v in [roofline_of(k, ktimes, d, world)] if v}
+             for v in [roofline_of(k, ktimes, d, world, G)] if v}
 
     # periods to DEAD convergence (untimed): every alive observer removed every crashed member;
     # the kernels are timed here too, for the suspicion sweep (no timeout fires in the timed region)
@@ -360,7 +367,7 @@ def main():
         kt2 = c.kernel_times()
         dc = {k: v - sc0[k] for k, v in c.stats().items()}
         conv = {k: round(v["frac"], 4) for k in ("k_sync_merge", "k_sync_ack")
-                for v in [roofline_of(k, kt2, dc, world)] if v}
+                for v in [roofline_of(k, kt2, dc, world, G)] if v}
         if fire_n:
             sweep_rl = roofline_of("k_susp_sweep", {"k_susp_sweep": (fire_ms, fire_n)},
                                    {"sweep_cells": fire_cells, "suspicion_timeouts": fire_dead}, world)
@@ -401,7 +408,8 @@ def main():
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
                                    "infected_suppressed", "infected_pruned_pairs", "infected_records",
-                                   "apply_words", "apply_runs", "apply_subjects")},
+                                   "apply_words", "apply_runs", "apply_subjects", "apply_records")},
+        "gossip_slots": {"live_at_end": s1["live_gossip_slots"], "gossips_live_at_end": s1["live_gossip_records"]},
     }
     c.close()
     if rank == 0 and not args.no_cpu_baseline:

@@ -55,8 +55,8 @@ struct swim_handle {
   uint32_t *cs_ghist = nullptr, *cs_ctr = nullptr, *cs_stat = nullptr;
   uint32_t cs_maxt = 1;
   // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
-  uint32_t apply_blocks = 1;
-  size_t apply_lds = 0;
+  uint32_t apply_blocks = 1, apply_blocks_b = 1;
+  size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
@@ -192,7 +192,7 @@ void memset_ctl_u32(swim_handle* h, size_t offset) {
 // ---- one protocol period as a resumable sequence ---------------------
 // Unsharded handles run a period straight through. Sharded handles (world > 1) stop at each
 // cross-shard exchange, describe it in a swim_xchg, and resume after the host's collective.
-enum Pc : int { PC_FD = 0, PC_FD_C, PC_R_MAX, PC_R_SEL, PC_R_NEED, PC_R_WIN, PC_R_PULL, PC_R_C, PC_SUSP, PC_SYNC_REQ, PC_SYNC_ACK, PC_END };
+enum Pc : int { PC_FD = 0, PC_FD_TRACK, PC_FD_C, PC_R_MAX, PC_R_SEL, PC_R_NEED, PC_R_WIN, PC_R_PULL, PC_R_C, PC_SUSP, PC_SYNC_REQ, PC_SYNC_ACK, PC_END };
 
 void set_phase(swim_handle* h, KP& P, uint32_t phase) {
   const uint32_t t = (uint32_t)h->period, G = h->G, TPP = h->TPP;
@@ -216,7 +216,7 @@ void set_phase(swim_handle* h, KP& P, uint32_t phase) {
 
 // N x K: allocate the requested columns (one thread per subject), then re-sort the column order
 void track_commit(swim_handle* h, const KP& P) {
-  hipLaunchKernelGGL(k_track_alloc, dim3(blocks_for(h->N, 256)), dim3(256), 0, h->stream, P);
+  hipLaunchKernelGGL(k_track_alloc, dim3(1), dim3(1024), 0, h->stream, P);
   hipLaunchKernelGGL(k_colorder, dim3(1), dim3(256), 0, h->stream, P);
 }
 
@@ -332,6 +332,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
 // the period, or SWIM_OK with another op when an exchange must happen first (world > 1).
 int period_resume(swim_handle* h, swim_xchg* x) {
   const uint32_t N = h->N, G = h->G, W = h->world, nloc = h->base.nloc;
+  const uint32_t RL = h->base.W;  // cells of a SYNC row (dense N, N x K the K columns)
   const uint32_t gL = blocks_for(nloc, 256);
   hipStream_t s = h->stream;
   KP& P = h->cur;
@@ -340,8 +341,29 @@ int period_resume(swim_handle* h, swim_xchg* x) {
     switch (h->pc) {
       case PC_FD:  // phase 0: failure detector
         set_phase(h, P, 0);
+        h->pc = PC_FD_TRACK;
         if (P.nxk) {  // N x K: columns for the subjects this FD phase changes first
           timed(h, 0, "k_fd_track", [&] { hipLaunchKernelGGL(k_fd_track, dim3(gL), dim3(256), 0, s, P); });
+          if (W > 1) {  // every shard's requests to every shard: all allocate the same columns
+            Ctl c;
+            if ((rc = read_ctl(h, &c))) return rc;
+            P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+            hipLaunchKernelGGL(k_track_pack, dim3(1), dim3(256), 0, s, P);
+            HIPC(h, hipStreamSynchronize(s));
+            xchg_clear(x, SWIM_X_ALLGATHER, W);
+            x->send_words = std::min(c.ntrack, P.tcap);
+            return SWIM_OK;
+          }
+          track_commit(h, P);
+        }
+        break;
+      case PC_FD_TRACK:
+        if (P.nxk && W > 1) {
+          uint32_t cnt[SWIM_MAX_WORLD];
+          for (uint32_t q = 0; q < W; ++q) cnt[q] = (uint32_t)x->recv_counts[q];
+          HIPC(h, hipMemcpyAsync(h->d_xcounts, cnt, 4ull * W, hipMemcpyHostToDevice, s));
+          P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
+          hipLaunchKernelGGL(k_track_unpack, dim3(1), dim3(256), 0, s, P, h->d_xcounts, (uint32_t)x->recv_stride);
           track_commit(h, P);
         }
         timed(h, 0, "k_fd", [&] { hipLaunchKernelGGL(k_fd, dim3(gL), dim3(256), 0, s, P); });
@@ -454,7 +476,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
           if (P.batched)  // batch slots in the ring: expand their records
-            hipLaunchKernelGGL(k_gossip_apply_b, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
+            hipLaunchKernelGGL(k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES), h->apply_lds_b, s, P);
           else
             hipLaunchKernelGGL(k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
         });
@@ -491,7 +513,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           uint32_t n_rec = 0;
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
           for (uint32_t q = 0; q < W; ++q) {
-            x->send_counts[q] = (uint64_t)c.xs_cnt[q] * (N + 2u);
+            x->send_counts[q] = (uint64_t)c.xs_cnt[q] * (RL + 2u);
             n_rec += c.xs_cnt[q];
           }
           if (n_rec > h->scap) return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
@@ -506,7 +528,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (W > 1) {
           uint64_t words = 0;
           for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
-          n_rec = (uint32_t)(words / (N + 2u));
+          n_rec = (uint32_t)(words / (RL + 2u));
           if (n_rec > h->scap) return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
@@ -536,7 +558,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (W > 1) {
           uint64_t words = 0;
           for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
-          const uint32_t n_rec = (uint32_t)(words / (N + 2u));
+          const uint32_t n_rec = (uint32_t)(words / (RL + 2u));
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
@@ -597,7 +619,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   const swim_config& c = *cfg;
   if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode > 1 || c.n_initial > c.n_members ||
       (c.n_initial && c.n_initial < c.n_members && (c.mode != 0 || c.shard_world > 1)) ||
-      (c.mode == 1 && (c.tracked_subjects < 1 || c.tracked_subjects > c.n_members || c.shard_world > 1)) ||
+      (c.mode == 1 && (c.tracked_subjects < 1 || c.tracked_subjects > c.n_members)) ||
       c.ping_interval_ms <= 0 ||
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
       c.ping_req_members > MAXK || c.sync_interval_ms <= 0 || c.gossip_repeat_mult < 0 || c.suspicion_mult < 0)
@@ -678,10 +700,16 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
     const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU
     h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
+    // the batch-slot variant: one receiver per wave, AW_WAVES waves per workgroup, each with its
+    // own table; as many workgroups per CU as the 160 KiB of LDS (and 2,048 threads) allow
+    h->apply_lds_b = 4ull * AW_WAVES * AW_WORDS;
+    const uint32_t per_cu_b = std::max<uint32_t>(
+        1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
+    h->apply_blocks_b = (uint32_t)std::max(1, cus) * per_cu_b;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply_b),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
@@ -737,6 +765,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.colsubj, P.W);
     ALLOC(P.colorder, P.W);
     ALLOC(P.track_req, N);
+    P.tcap = std::min<uint32_t>(N, TRACK_SORT);
+    ALLOC(P.track_list, P.tcap);
   }
   ALLOC(P.cnt, N);
   ALLOC(P.cnt_delta, N);
@@ -875,7 +905,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.W, 256)), dim3(256), 0, s, P.colmin, (size_t)P.W, NONE);
   if (P.nxk) {
     hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmap, (size_t)N, NONE);
-    (void)hipMemsetAsync(P.track_req, 0, N, s);
+    (void)hipMemsetAsync(P.track_req, 0, (size_t)N * 4, s);
   }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, n0 - 1);
   // presence is per shard: observers of this shard holding the subject (all but the subject itself)
@@ -921,7 +951,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
                      NONE);
   {  // every started member of this shard starts with others = n0 - 1; n0 members alive
-    const uint32_t all = n0 == N ? P.nloc : n0, alive = n0;
+    const uint32_t all = n0 == N ? P.nloc : n0, alive = n0 == N ? P.nloc : n0;  // of this shard
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(n0)], &all, 4, hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(&P.ctl->alive_count, &alive, 4, hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
@@ -1261,8 +1291,8 @@ int presence_host(swim_handle* h, std::vector<uint32_t>* pres, std::vector<uint8
     HIPC(h, hipMemcpyAsync(colmap.data(), h->base.colmap, (size_t)N * 4, hipMemcpyDeviceToHost, h->stream));
     HIPC(h, hipMemcpyAsync(&alive_count, &h->base.ctl->alive_count, 4, hipMemcpyDeviceToHost, h->stream));
     HIPC(h, hipStreamSynchronize(h->stream));
-    for (uint32_t j = 0; j < N; ++j)
-      if (colmap[j] == NONE) (*pres)[j] = alive_count - ((*alive)[j] ? 1u : 0u);
+    for (uint32_t j = 0; j < N; ++j)  // alive_count: alive observers of this shard
+      if (colmap[j] == NONE) (*pres)[j] = alive_count - (((*alive)[j] && j - h->base.row0 < h->base.nloc) ? 1u : 0u);
   }
   HIPC(h, hipStreamSynchronize(h->stream));
   return SWIM_OK;
@@ -1470,7 +1500,7 @@ int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv
   // window records: <= f per local sender, 2 + active words each; SYNC rows: <= scap, 2 + N each;
   // gossip commits: 4 words per staged gossip (x world when gathered); round maxima: W32 + 2
   const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
-  const uint64_t rows = (uint64_t)h->scap * (h->N + 2ull);
+  const uint64_t rows = (uint64_t)h->scap * (h->base.W + 2ull);
   const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2;  // commits carry the liveness maxima too
   // The window bounds assume every pair ships every active word; the need bitmaps ship only the
   // words a receiver lacks something in, far fewer (k_gossip_need), so both buffers are capped at

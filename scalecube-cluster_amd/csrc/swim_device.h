@@ -115,7 +115,8 @@ struct Ctl {
   uint32_t ov_detail;    // which infectedFrom bound OV_IFROM hit (IfromOverflow bits)
   // gossip batches: records ever committed (the record ring's unwrapped end),
   // the ring id count before the last commit, and the batches the last chip-wide commit made
-  uint32_t ccount, g_prev, rs_ncls, rsv1;
+  uint32_t ccount, g_prev, rs_ncls;
+  uint32_t ntrack;       // N x K: subjects listed in track_list for the coming allocation
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -139,7 +140,9 @@ struct KP {
   uint32_t* colmap;    // [N] subject -> column, NONE while untracked (N x K only)
   uint32_t* colsubj;   // [K] column -> subject
   uint32_t* colorder;  // [K] the allocated columns in subject order (SYNC merges walk it)
-  uint8_t* track_req;  // [N] subjects the coming FD phase changes first (k_fd_track)
+  uint32_t* track_req;   // [N] subject listed for a column (k_fd_track / k_track_one)
+  uint32_t* track_list;  // [tcap] subjects the coming FD phase changes first (k_track_alloc)
+  uint32_t tcap;
   uint32_t sweepmax;  // max gossipPeriodsToSweep + 1: last round a holder may still count a gossip
   uint32_t ecap, scap;
   uint64_t seed;

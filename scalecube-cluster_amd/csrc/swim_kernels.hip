@@ -671,35 +671,119 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
   return pr;
 }
 
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* total, uint32_t* lds16);
+
 // N x K mode, before the FD phase: an untracked target whose record this probe turns SUSPECT
 // (the only way a subject's record first leaves the baseline: every later change — gossip,
 // SYNC, timeout, refutation — concerns a subject some record already changed) needs a column.
+// A requested subject is listed once (track_req flags it, track_list holds it).
+__device__ __forceinline__ void track_request(const KP& P, uint32_t j) {
+  if (P.colmap[j] != NONE || atomicExch(&P.track_req[j], 1u) != 0u) return;
+  const uint32_t o = atomicAdd(&P.ctl->ntrack, 1u);
+  if (o < P.tcap)
+    P.track_list[o] = j;
+  else
+    atomicOr(&P.ctl->overflow, OV_TRACK);  // more first changes in one phase than columns exist
+}
+
 __global__ void __launch_bounds__(256) k_fd_track(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.row0 + P.nloc && P.alive[i] && P.cnt[i] > 0u) {
     const Probe pr = fd_probe(P, i, false);
-    if (pr.nA + pr.nB > 0u && (pr.nA > 0u || pr.stB == SWIM_SUSPECT) && P.colmap[pr.j] == NONE)
-      P.track_req[pr.j] = 1;
+    if (pr.nA + pr.nB > 0u && (pr.nA > 0u || pr.stB == SWIM_SUSPECT)) track_request(P, pr.j);
   }
 }
 
-// One thread per requested subject: the next free column (pre-filled with BASELINE cells), its
-// presence materialised (every alive observer but itself holds it), no deadline.
-__global__ void k_track_alloc(KP P) {
+// Sharded: every shard's requests (its observers' probes) travel to every shard, so all of them
+// allocate the same columns (a SYNC row is a row of columns; k_sync_pack)
+__global__ void k_track_pack(KP P) {
+  const uint32_t n = min(P.ctl->ntrack, P.tcap);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) P.xsend[i] = P.track_list[i];
+}
+
+// the gathered lists (block q of `stride` words, cnt[q] entries) replace the local one
+__global__ void k_track_unpack(KP P, const uint32_t* cnt, uint32_t stride) {
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  for (uint32_t q = 0; q < P.world; ++q) {
+    const uint32_t base = s_n;
+    for (uint32_t i = threadIdx.x; i < cnt[q]; i += blockDim.x) {
+      const uint32_t j = P.xrecv[(size_t)q * stride + i];
+      P.track_req[j] = 1u;
+      if (base + i < P.tcap) P.track_list[base + i] = j;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_n = base + cnt[q];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (s_n > P.tcap) atomicOr(&P.ctl->overflow, OV_TRACK);
+    P.ctl->ntrack = min(s_n, P.tcap);
+  }
+}
+
+// One workgroup: the listed subjects get the next free columns in subject order (deterministic,
+// the same on every shard), the columns pre-filled with BASELINE cells, the subject's presence
+// materialised (every alive observer of this shard but itself holds it), no deadline.
+constexpr uint32_t TRACK_SORT = 4096;  // subjects one FD phase may start tracking (LDS sort)
+__global__ void __launch_bounds__(1024) k_track_alloc(KP P) {
   SWIM_GUARD(P);
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= P.N || !P.track_req[j]) return;
-  P.track_req[j] = 0;
-  if (P.colmap[j] != NONE) return;
-  const uint32_t c = atomicAdd(&P.ctl->ncols, 1u);
-  if (c >= P.W) {
-    atomicOr(&P.ctl->overflow, OV_TRACK);
+  __shared__ uint32_t s_j[TRACK_SORT];
+  __shared__ uint32_t s_lds[16];
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(P.ctl->ntrack, P.tcap);
+  if (n == 0u) return;
+  if (n > TRACK_SORT) {
+    if (t == 0) atomicOr(&P.ctl->overflow, OV_TRACK);
     return;
   }
-  P.colsubj[c] = j;
-  P.pres[j] = P.ctl->alive_count - (P.alive[j] ? 1u : 0u);
-  P.colmap[j] = c;
+  uint32_t m = 1;
+  while (m < n) m <<= 1;
+  for (uint32_t i = t; i < m; i += blockDim.x) s_j[i] = i < n ? P.track_list[i] : NONE;
+  __syncthreads();
+  for (uint32_t k = 2; k <= m; k <<= 1)
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = t; i < m; i += blockDim.x) {
+        const uint32_t l = i ^ jj;
+        if (l > i) {
+          const uint32_t a = s_j[i], b = s_j[l];
+          if ((a > b) == ((i & k) == 0)) {
+            s_j[i] = b;
+            s_j[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  const uint32_t c0 = P.ctl->ncols;
+  const uint32_t alive_local = P.ctl->alive_count;  // alive observers of this shard
+  uint32_t col = c0;
+  for (uint32_t b0 = 0; b0 < n; b0 += blockDim.x) {  // new = first of its value, still untracked
+    const uint32_t i = b0 + t;
+    const uint32_t j = i < n ? s_j[i] : NONE;
+    const bool fresh = i < n && (i == 0u || s_j[i - 1u] != j) && P.colmap[j] == NONE;
+    uint32_t tot;
+    const uint32_t off = block_excl_scan1024(fresh ? 1u : 0u, &tot, s_lds);
+    if (i < n) P.track_req[j] = 0u;
+    if (fresh) {
+      const uint32_t c = col + off;
+      if (c >= P.W) {
+        atomicOr(&P.ctl->overflow, OV_TRACK);
+      } else {
+        P.colsubj[c] = j;
+        P.pres[j] = alive_local - ((P.alive[j] && is_local(P, j)) ? 1u : 0u);
+        P.colmap[j] = c;
+      }
+    }
+    col += tot;
+  }
+  __syncthreads();
+  if (t == 0) {
+    P.ctl->ncols = col;
+    P.ctl->ntrack = 0u;
+  }
 }
 
 // the allocated columns in subject order (SYNC merges assign gossip sequence numbers in it)
@@ -716,7 +800,7 @@ __global__ void __launch_bounds__(256) k_colorder(KP P) {
 
 // N x K: give subject j a column now (swim_leave: the member's own record changes)
 __global__ void k_track_one(KP P, uint32_t j) {
-  if (threadIdx.x == 0) P.track_req[j] = P.colmap[j] == NONE ? 1 : 0;
+  if (threadIdx.x == 0) track_request(P, j);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2296,70 +2380,92 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 }
 
 // k_gossip_apply when the ring holds batch slots (P.batched): a received slot stands for all
-// the gossips of its batch, so its record range is expanded into the LDS table. Two passes per
-// receiver: (1) holdings, infection rounds and age bounds of every receipt word, and the number
-// of records the received run tops carry (sizes the table); (2) the records themselves, lattice-
-// max per subject. Work is spread over the wave, not the word: each wave's run tops, then their
-// records, are flattened across its 64 lanes (wave_owner), and receipt words are dealt to the
-// waves round-robin, so one word holding a large batch does not serialize a lane.
-// Then one updateMembership per subject, as in k_gossip_apply.
-__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
+// the gossips of its batch, so its record range is expanded into an LDS table. One WAVE per
+// receiver (its own table of up to 2^SWIM_APPLY_WLOG slots; several receivers in flight per CU,
+// no workgroup barriers): in a storm a receiver gets ~10^4 records of ~10^3 distinct subjects per
+// round, and a whole workgroup per receiver spent its time in barrier-separated phases (measured:
+// 570 ms per 100 C3 rounds with per-wave expansion inside a 1,024-thread receiver, 670 ms with a
+// workgroup-wide record list). Two passes per receiver: (1) holdings, infection
+// rounds and age bounds of every receipt word, and the record count of the received run tops
+// (sizes the table); (2) the records, flattened across the 64 lanes (wave_owner) four per lane at
+// a time, lattice-max per subject. Subjects that find no slot go to the global inbox row; when
+// more spill than the wave's list holds, the row is scanned at the end. Then updateMembership per
+// subject whose merged record overrides the cell (MembershipRecord.isOverrides, the only ones
+// updateMembership does anything for, MPI:489-496), cells loaded eight at a time.
+#ifndef SWIM_APPLY_WLOG
+#define SWIM_APPLY_WLOG 11
+#endif
+constexpr uint32_t AW_LOG = SWIM_APPLY_WLOG;
+constexpr uint32_t AW_SLOTS = 1u << AW_LOG;  // per-wave table slots (keys + values)
+#ifndef SWIM_APPLY_WSPILL
+#define SWIM_APPLY_WSPILL 128
+#endif
+constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
+constexpr uint32_t AW_WAVES = 4;             // waves per workgroup
+constexpr uint32_t AW_WORDS = 2u * AW_SLOTS + AW_SPILL + 4u;  // LDS words per wave
+static_assert(AW_LOG >= 6 && AW_LOG <= 13, "SWIM_APPLY_WLOG out of range");
+static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
+
+__global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
-  const uint32_t hcap_log = P.apply_hlog, hcap = 1u << hcap_log;
-  const uint32_t pres_words = P.N <= 32u * PRES_WORDS ? (P.N + 31u) / 32u : 0u;
-  const bool pres = pres_words != 0u;
-  uint32_t* s_key = s_dyn;
-  uint32_t* s_val = s_dyn + hcap;
-  uint32_t* s_spl = s_dyn + 2u * hcap;
-  uint32_t* s_pres = s_spl + SPILL_CAP;
-  __shared__ uint32_t s_nspill;
-  __shared__ uint32_t s_part[16];
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63u, nw = nthr >> 6;
-  const uint32_t slot_of_thread = lane * nw + (tid >> 6);  // items dealt to the waves round-robin
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t* s_key = s_dyn + wv * AW_WORDS;
+  uint32_t* s_val = s_key + AW_SLOTS;
+  uint32_t* s_spl = s_val + AW_SLOTS;
+  uint32_t* s_misc = s_spl + AW_SPILL;  // [0] spilled subjects
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
   Tally T;
   uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrecs = 0, nrcpt = 0;
-  for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {
+  auto wsync = [] {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  };
+  for (uint32_t li = blockIdx.x * AW_WAVES + wv; li < n_list; li += gridDim.x * AW_WAVES) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t nsw = (n_act + 31u) >> 5;
     const bool summ = nsw <= NSUM;
     const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
-    if (tid == 0) s_nspill = 0u;
-    if (pres)
-      for (uint32_t t = tid; t < pres_words; t += nthr) s_pres[t] = 0u;
-    // the list positions with receipts, compacted from the summary (at the front of the table
-    // area, free until the table is sized)
+    if (lane == 0) s_misc[0] = 0u;
+    // the list positions with receipts, compacted from the summary into the table area (free
+    // until the table is sized), as long as they fit it
     uint32_t n_comp = 0;
+    bool compact = summ;
     if (summ) {
-      for (uint32_t c0 = 0; c0 < nsw; c0 += nthr) {
-        const uint32_t t = c0 + tid;
+      for (uint32_t c0 = 0; c0 < nsw && compact; c0 += 64u) {
+        const uint32_t t = c0 + lane;
         uint32_t bits = t < nsw ? sumr[t] : 0u;
         uint32_t tot;
-        uint32_t o = n_comp + block_excl_scan1024((uint32_t)__popc(bits), &tot, s_part);
+        uint32_t o = n_comp + wave_excl_scan((uint32_t)__popc(bits), &tot);
+        if (n_comp + tot > 2u * AW_SLOTS) {
+          compact = false;  // uniform
+          break;
+        }
         while (bits) {
-          s_dyn[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
+          s_key[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
           bits &= bits - 1u;
         }
         n_comp += tot;
       }
-      __syncthreads();
+      wsync();
     }
-    const uint32_t* items = s_dyn;
-    const uint32_t n_it = summ ? n_comp : n_act;
-    // pass 1: receive the words; count the records of the run tops
+    const uint32_t n_it = !summ ? n_act : (compact ? n_comp : nsw * 32u);
+    auto item = [&](uint32_t u, const uint32_t* list) -> uint32_t {
+      if (u >= n_it) return NONE;
+      if (!summ) return u;
+      if (compact) return list[u];
+      return ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
+    };
+    // pass 1: receive the words; count the records their run tops carry
     uint32_t ent = 0, rc = 0;
-    for (uint32_t it0 = 0; it0 < n_it; it0 += 4u * nthr) {
+    for (uint32_t it0 = 0; it0 < n_it; it0 += 256u) {
       uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
       uint4 v0[4], v1[4];
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t u = it0 + j * nthr + slot_of_thread;
-        kv[j] = u < n_it ? (summ ? items[u] : u) : NONE;
-      }
+      for (uint32_t j = 0; j < 4u; ++j) kv[j] = item(it0 + 64u * j + lane, s_key);
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) ev[j] = kv[j] != NONE ? P.act[kv[j]] : 0u;
 #pragma unroll
@@ -2378,16 +2484,15 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
         }
       }
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j)
+      for (uint32_t j = 0; j < 4u; ++j) {
+        uint32_t rm = 0u;
         if (bv[j]) {
           receive_word(P, p, wsv[j], bv[j], pv[j], v0[j], v1[j]);
           ++nwords;
+          rm = run_tops(bv[j], rv[j]);
+          rc += (uint32_t)(__popc(bv[j]) - __popc(rm));  // slots inside runs: one gossip each
+          nruns += (uint32_t)__popc(rm);
         }
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t rm = bv[j] ? run_tops(bv[j], rv[j]) : 0u;
-        rc += (uint32_t)(__popc(bv[j]) - __popc(rm));  // slots inside runs: one gossip each
-        nruns += (uint32_t)__popc(rm);
         uint32_t tot;
         const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
         for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
@@ -2401,65 +2506,74 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
         }
       }
     }
-    uint32_t E, R;
-    block_excl_scan1024(ent, &E, s_part);
-    block_excl_scan1024(rc + ent, &R, s_part);
-    if (tid == 0) {
+    const uint32_t E = wave_sum(ent), R = wave_sum(rc + ent);
+    if (lane == 0) {
       nrcpt += R;
       nrecs += E;
     }
-    uint32_t lg = 6;  // >= 2 slots per record, 64 .. 2^hcap_log
-    while (lg < hcap_log && (1u << lg) < 2u * E) ++lg;
+    uint32_t lg = 6;  // >= 2 slots per record, 64 .. AW_SLOTS
+    while (lg < AW_LOG && (1u << lg) < 2u * E) ++lg;
     const uint32_t hm = (1u << lg) - 1u;
-    // keep the compacted items for pass 2 when they fit behind the table's value half (disjoint
-    // from their place at the front, so a parallel copy is safe); otherwise pass 2 tests the
-    // summary bits again
-    const bool keep = summ && n_comp <= hcap - (1u << lg);
-    uint32_t* items2 = s_dyn + 2u * hcap - n_comp;
-    if (keep)
-      for (uint32_t t = tid; t < n_comp; t += nthr) items2[t] = items[t];
-    __syncthreads();
-    for (uint32_t t = tid; t <= hm; t += nthr) {
+    // the compacted items move behind the table's keys when they fit there (otherwise pass 2
+    // tests the summary bits again); through registers, so overlapping ranges are safe
+    const bool keep = compact && n_comp <= AW_SLOTS - (1u << lg) && n_comp <= 256u;
+    uint32_t* items2 = s_key + AW_SLOTS - n_comp;
+    {
+      uint32_t tmp[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) tmp[j] = (keep && 64u * j + lane < n_comp) ? s_key[64u * j + lane] : 0u;
+      wsync();
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j)
+        if (keep && 64u * j + lane < n_comp) items2[64u * j + lane] = tmp[j];
+      wsync();
+    }
+    for (uint32_t t = lane; t <= hm; t += 64u) {
       s_key[t] = NONE;
       s_val[t] = 0u;
     }
-    __syncthreads();
+    wsync();
+    const bool compact2 = keep;
+    const uint32_t n_it2 = !summ ? n_act : (compact2 ? n_comp : nsw * 32u);
+    auto item2 = [&](uint32_t u) -> uint32_t {
+      if (u >= n_it2) return NONE;
+      if (!summ) return u;
+      if (compact2) return items2[u];
+      return ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
+    };
+    // lattice max per subject; a plain read first settles most repeats without atomics
+    bool rowscan = false;  // the spill list overflowed: scan the whole inbox row at the end
     auto insert = [&](uint2 sr) {
       uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
       for (uint32_t q = 0; q < HPROBE; ++q) {
-        const uint32_t prev = atomicCAS(&s_key[h], NONE, sr.x);
-        if (prev == NONE || prev == sr.x) {
-          atomicMax(&s_val[h], sr.y);
-          if (prev == NONE && pres) atomicOr(&s_pres[sr.x >> 5], 1u << (sr.x & 31u));
+        uint32_t k = s_key[h];
+        if (k == NONE) {
+          k = atomicCAS(&s_key[h], NONE, sr.x);
+          if (k == NONE) {
+            atomicMax(&s_val[h], sr.y);
+            return;
+          }
+        }
+        if (k == sr.x) {
+          if (s_val[h] < sr.y) atomicMax(&s_val[h], sr.y);
           return;
         }
         h = (h + 1u) & hm;
       }
       // slots only ever fill up, so this subject spills for the whole round
       if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr.x)], sr.y) == 0u) {
-        const uint32_t o = atomicAdd(&s_nspill, 1u);
-        if (o < SPILL_CAP)
+        const uint32_t o = atomicAdd(&s_misc[0], 1u);
+        if (o < AW_SPILL)
           s_spl[o] = sr.x;
         else
-          atomicOr(&P.ctl->overflow, OV_SPILL);
+          rowscan = true;
       }
     };
     // pass 2: the records of every received run top into the table; receipts cleared
-    const uint32_t n_it2 = !summ ? n_act : (keep ? n_comp : nsw * 32u);
-    for (uint32_t it0 = 0; it0 < n_it2; it0 += 4u * nthr) {
+    for (uint32_t it0 = 0; it0 < n_it2; it0 += 256u) {
       uint32_t kv[4], bv[4], wsv[4], rv[4];
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t u = it0 + j * nthr + slot_of_thread;
-        if (u >= n_it2)
-          kv[j] = NONE;
-        else if (!summ)
-          kv[j] = u;
-        else if (keep)
-          kv[j] = items2[u];
-        else
-          kv[j] = ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
-      }
+      for (uint32_t j = 0; j < 4u; ++j) kv[j] = item2(it0 + 64u * j + lane);
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
         const uint32_t e = kv[j] != NONE ? P.act[kv[j]] : 0u;
@@ -2481,16 +2595,23 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
           if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
           uint32_t etot;
           const uint32_t eoff = wave_excl_scan(cr.y - cr.x, &etot);
-          for (uint32_t e0 = 0; e0 < etot; e0 += 64u) {
-            const uint32_t e = e0 + lane;
-            const uint32_t eo = wave_owner(eoff, e);
-            const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
-            if (e < etot) insert(P.c_sr[(bx + e - bo) & P.cmask]);
+          for (uint32_t e0 = 0; e0 < etot; e0 += 256u) {  // four records per lane in flight
+            uint2 sr[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; ++u) {
+              const uint32_t e = e0 + 64u * u + lane;
+              const uint32_t eo = wave_owner(eoff, e);
+              const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
+              if (e < etot) sr[u] = P.c_sr[(bx + e - bo) & P.cmask];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; ++u)
+              if (e0 + 64u * u + lane < etot) insert(sr[u]);
           }
         }
       }
     }
-    __syncthreads();
+    wsync();
     const uint32_t snap = P.cnt[p];
     auto apply = [&](uint32_t subj, uint32_t r1) {
       ++nsubj;
@@ -2500,30 +2621,44 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_b(KP P) {
         ++created;
       }
     };
-    if (pres) {  // one updateMembership per subject, in subject order
-      for (uint32_t t = tid; t < pres_words; t += nthr) {
-        uint32_t bits = s_pres[t];
-        while (bits) {
-          const uint32_t subj = 32u * t + (uint32_t)__builtin_ctz(bits);
-          bits &= bits - 1u;
-          uint32_t h = (subj * 0x9E3779B1u) >> (32u - lg);
-          while (s_key[h] != subj) h = (h + 1u) & hm;  // present: placed within HPROBE probes
-          apply(subj, s_val[h]);
-        }
+    // updateMembership for the subjects whose merged record overrides the cell; cells of eight
+    // table slots per lane loaded together
+    for (uint32_t t0 = 0; t0 <= hm; t0 += 512u) {
+      uint32_t ks[8], vs[8], cs[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8u; ++u) {
+        const uint32_t t = t0 + 64u * u + lane;
+        ks[u] = t <= hm ? s_key[t] : NONE;
+        vs[u] = ks[u] != NONE ? s_val[t] : 0u;
       }
+#pragma unroll
+      for (uint32_t u = 0; u < 8u; ++u) cs[u] = ks[u] != NONE ? cell_get(P, p, ks[u]) : 0u;
+#pragma unroll
+      for (uint32_t u = 0; u < 8u; ++u)
+        if (ks[u] != NONE) {
+          if (is_overrides(vs[u], cs[u]) || (P.nxk && P.colmap[ks[u]] == NONE))  // (the latter: OV_TRACK)
+            apply(ks[u], vs[u]);
+          else
+            ++nsubj;
+        }
+    }
+    const uint32_t nsp = min(s_misc[0], AW_SPILL);
+    if (__any(rowscan)) {  // every spilled subject: the inbox row's nonzero cells
+      __threadfence();
+      uint32_t* row = P.inbox + lrow(P, p) * P.W;
+      const uint32_t nc = ncells(P);
+      for (uint32_t c = lane; c < nc; c += 64u)
+        if (row[c]) apply(subj_of(P, c), atomicExch(&row[c], 0u));
     } else {
-      for (uint32_t t = tid; t <= hm; t += nthr)
-        if (s_key[t] != NONE) apply(s_key[t], s_val[t]);
+      if (nsp) __threadfence();
+      for (uint32_t t = lane; t < nsp; t += 64u) {
+        const uint32_t subj = s_spl[t];
+        apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
+      }
     }
-    const uint32_t nsp = s_nspill < SPILL_CAP ? s_nspill : SPILL_CAP;
-    if (nsp) __threadfence();
-    for (uint32_t t = tid; t < nsp; t += nthr) {
-      const uint32_t subj = s_spl[t];
-      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
-    }
-    if (tid == 0) atomicAdd(&P.held[p], total);
-    nspills += tid == 0 ? nsp : 0u;
-    __syncthreads();  // the table is reused by the next receiver
+    if (lane == 0) atomicAdd(&P.held[p], total);
+    nspills += lane == 0 ? s_misc[0] : 0u;
+    wsync();  // the table is reused by the wave's next receiver
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   add_stat(P, ST_APPLY_WORDS, nwords);
@@ -2704,13 +2839,13 @@ __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
     uint32_t dst, i;
     if (!xrec_locate(P, P.ctl->xs_cnt, g, &dst, &i)) break;
     const uint32_t q = P.xs_pend[(size_t)dst * 2u * P.nloc + i];
-    uint32_t* out = P.xsend + (size_t)g * (N + 2u);
+    uint32_t* out = P.xsend + (size_t)g * (P.W + 2u);  // a row of W cells (N x K: columns)
     if (threadIdx.x == 0) {
       out[0] = q;
       out[1] = P.req_to[q];
     }
-    const uint32_t* row = P.view + lrow(P, q >> 1) * N;
-    for (uint32_t c = threadIdx.x; c < N; c += blockDim.x) out[2 + c] = row[c];
+    const uint32_t* row = P.view + lrow(P, q >> 1) * P.W;
+    for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) out[2 + c] = row[c];
   }
 }
 
@@ -2719,7 +2854,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
-    const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
+    const uint32_t* rec = P.xrecv + (size_t)g * (P.W + 2u);
     P.rs_ref[rec[0]] = g;
     atomicAdd(&P.recv_count[rec[1]], 1u);
   }
@@ -2729,7 +2864,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
-    const uint32_t* rec = P.xrecv + (size_t)g * (P.N + 2u);
+    const uint32_t* rec = P.xrecv + (size_t)g * (P.W + 2u);
     const uint32_t to = rec[1];
     P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = 4u * (rec[0] >> 1) + (rec[0] & 1u);
   }
@@ -2739,7 +2874,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
 __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.N + 2u)]] = g;
+  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.W + 2u)]] = g;
 }
 
 // Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
@@ -3200,7 +3335,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
       src = P.stage_sync + (size_t)slot * P.W;
       ack = P.stage_ack + (size_t)slot * P.W;
     } else {  // request from another shard: payload in the received record, ack into the same
-      const size_t g = (size_t)P.rs_ref[q] * (P.N + 2u);  // position of the send buffer
+      const size_t g = (size_t)P.rs_ref[q] * (P.W + 2u);  // position of the send buffer
       src = P.xrecv + g + 2;
       ack = P.xsend + g + 2;
       if (threadIdx.x == 0) {
@@ -3261,7 +3396,7 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
     } else {
       const uint32_t qq = 2 * i + kd[k], slot = P.req_stage[qq];
       attempt = (to[k] << 1) | kd[k];
-      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.N + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
+      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.W + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
     }
     merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4);
   }

@@ -174,7 +174,7 @@ class ShardedSwimCluster(SwimCluster):
         last = np.max([p[1] for p in parts], axis=0).astype(np.uint32)
         return pres, last
 
-    _SAME = ("period", "live_gossip_slots")
+    _SAME = ("period", "live_gossip_slots", "live_gossip_records")
 
     def stats(self) -> dict:
         parts = self._gather_objects(SwimCluster.stats(self))

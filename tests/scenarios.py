@@ -174,9 +174,17 @@ SCENARIOS = {
 }
 
 
+# Larger shapes, run only where their cost is the point (sharded rehearsals of BASELINE configs)
+SCENARIOS_EXTRA = {
+    # C4's schedule shape (BASELINE configs[3]: LAN defaults, 1 % loss, 0.1 % simultaneous crash)
+    # at 4,096 members
+    "lan4096_c4_shape": (ClusterConfig.defaultLanConfig(), 4096, 13, lambda c: _lan_loss(c, 4, 16, 1.0, t0=3)),
+}
+
+
 def scenario(name):
     """(config, n, seed, script, create kwargs) of scenario `name`."""
-    cfg, n, seed, script, *kw = SCENARIOS[name]
+    cfg, n, seed, script, *kw = SCENARIOS[name] if name in SCENARIOS else SCENARIOS_EXTRA[name]
     return cfg, n, seed, script, (kw[0] if kw else {})
 
 

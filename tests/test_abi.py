@@ -36,8 +36,38 @@ def test_oracle_mirrors_stateful_api():
 def test_struct_sizes_match_c_layout():
     assert ctypes.sizeof(nat.SwimEvent) == 24
     assert ctypes.sizeof(nat.SwimStats) == 8 * len(nat.STAT_FIELDS)
-    assert ctypes.sizeof(nat.SwimConfig) == 96
+    assert ctypes.sizeof(nat.SwimConfig) == 104
     assert ctypes.sizeof(nat.SwimXchg) == 16 + 2 * 8 * nat.MAX_WORLD + 8
+
+
+def test_struct_layout_matches_the_c_compiler(tmp_path):
+    """Every field offset of the ctypes mirror equals the C compiler's for include/swimhip.h."""
+    import shutil
+    import subprocess
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        import pytest
+
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{nat.HEADER_PATH}"', "int main(void) {"]
+    for cname, cls in (("swim_config", nat.SwimConfig), ("swim_stats", nat.SwimStats),
+                       ("swim_event", nat.SwimEvent), ("swim_xchg", nat.SwimXchg)):
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'  printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-o", str(exe), str(src)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                               text=True).stdout.split("\n") if line)
+    for cname, cls in (("swim_config", nat.SwimConfig), ("swim_stats", nat.SwimStats),
+                       ("swim_event", nat.SwimEvent), ("swim_xchg", nat.SwimXchg)):
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
 
 
 def test_create_without_gpu_fails_cleanly():

@@ -32,7 +32,7 @@ def test_kernel_bytes_covers_every_timed_class():
                         "suspicion_timeouts")}
     for name in SwimCluster.KERNEL_CLASSES:
         if name != "bookkeeping":
-            assert bench.kernel_bytes(name, d, 1) > 0, name
+            assert bench.kernel_bytes(name, d) > 0, name
 
 
 def test_pmc_traffic_reads_committed_summary():

@@ -18,6 +18,50 @@ def test_scenario_parity(name):
     scenarios.run_pair(name, SwimCluster, OracleCluster)
 
 
+# Gossip batches: lossless scenarios run batched by default; the same scenarios
+# with one ring slot per gossip must match the oracle too (the round-2 layout, kept for lossy links)
+LOSSLESS = ["c1_local32_crash", "local128_partition_heal", "test64_long_partition_rejoin", "local48_links",
+            "local32_leave2", "local24_inbound_blocks", "local40_restart_join"]
+
+
+@pytest.mark.parametrize("name", LOSSLESS)
+def test_scenario_parity_unbatched(name):
+    def make(cfg, n, seed, **kw):
+        return SwimCluster(cfg, n, seed, gossip_batching=False, **kw)
+
+    scenarios.run_pair(name, make, OracleCluster)
+
+
+def test_batches_share_slots_and_refuse_probabilistic_loss():
+    """Batching stores each (origin, phase) batch in one slot: the C3 storm at N = 1,024 then needs
+    several times fewer live slots than gossips, with every counter equal to the unbatched run's.
+    A probabilistic loss cannot start while a multi-gossip slot is live (loss draws are per
+    gossip): SWIM_EINVAL, the handle unchanged; once every batch is swept it is accepted."""
+    import bench
+    from swimhip import SwimError
+
+    cfg = bench.preset_config("lan")
+    n = 1024
+    a = SwimCluster(cfg, n, seed=1, gossip_capacity=1 << 17)
+    b = SwimCluster(cfg, n, seed=1, gossip_capacity=1 << 17, gossip_batching=False)
+    for c in (a, b):
+        c.step(3)
+        bench.inject_faults(c, "c3", 3, 1, n=n)
+        c.step(8)
+    sa, sb = a.stats(), b.stats()
+    assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+    assert a.digest() == b.digest()
+    assert sb["live_gossip_slots"] == sb["live_gossip_records"]  # one gossip per slot
+    assert 0 < sa["live_gossip_slots"] * 2 < sa["live_gossip_records"]
+    assert sa["apply_records"] > 0 and sb["apply_records"] == 0
+    with pytest.raises(SwimError) as ei:
+        a.set_loss(5.0)
+    assert ei.value.code == -22
+    b.set_loss(5.0)  # one gossip per slot: always allowed
+    a.set_loss(100.0)  # blockAllOutbound draws nothing: allowed
+    a.set_loss(0.0)
+
+
 # N x K tracked-subject mode vs the dense oracle: K columns cover every subject whose record ever
 # leaves the converged baseline in the scenario (crashes, false suspicions under loss, leaves)
 NXK = {
@@ -190,7 +234,7 @@ for _ in range(6):
     sx, sy = x.stats(), y.stats()
     assert {{k: sx[k] for k in scenarios.PARITY_KEYS}} == {{k: sy[k] for k in scenarios.PARITY_KEYS}}
 spills += x.stats()["apply_spills"]
-print("SPILLS", spills)
+print("SPILLS", spills, "RECORDS", x.stats()["apply_records"], "RADIX", x.stats()["gossips_created"])
 """
 
 
@@ -227,7 +271,8 @@ def test_apply_spill_path_parity():
     the table is at its cap) only run in storm rounds of the full C3 bench with the product's
     16,384-slot hash. A variant built with a 64-slot hash (__graft_entry__.build, -DSWIM_APPLY_HLOG=6)
     takes them in almost every round: it must still match the oracle bit for bit, and the spill
-    counter proves the path ran."""
+    counter proves the path ran. The same variant gives the batch-slot kernel (k_gossip_apply_b,
+    lossless C3 part) 64-slot wave tables and a 4-entry spill list, so its inbox-row scan runs too."""
     import os
     import subprocess
     import sys
@@ -241,7 +286,7 @@ def test_apply_spill_path_parity():
     out = subprocess.run([sys.executable, "-c", _SPILL_SCRIPT.format(paths=paths)], env=env, capture_output=True,
                          text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
-    spills = int(out.stdout.split("SPILLS")[-1])
+    spills = int(out.stdout.split("SPILLS")[-1].split()[0])
     assert spills > 0, "the spill path never ran"
 
 

@@ -105,6 +105,52 @@ def test_shards_match_unsharded(world, names):
     mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
 
 
+def _nxk_worker(rank, world, port, names, k):
+    import scenarios
+    from swimhip import SwimCluster
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        for name in names:
+            scenarios.run_pair(name, lambda *a, **kw: ShardedSwimCluster(*a, tracked_subjects=k, **kw),
+                               lambda *a, **kw: SwimCluster(*a, tracked_subjects=k, **kw))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,names,k", [(2, ["c1_local32_crash", "local128_partition_heal"], 128),
+                                           (2, ["lan256_loss5_crash3"], 256)])
+def test_nxk_shards_match_unsharded(world, names, k):
+    """N x K tracked-subject views sharded by observer rows: every shard's column requests are
+    all-gathered and allocated in subject order, so all shards agree on the columns (a SYNC row
+    between shards is a row of columns). Bit-exact with the unsharded N x K handle, which is
+    itself bit-exact with the dense oracle (test_gpu_parity.py::test_nxk_scenario_parity)."""
+    mp.spawn(_nxk_worker, args=(world, _free_port(), names, k), nprocs=world, join=True)
+
+
+def _c4_worker(rank, world, port):
+    import scenarios
+    from swimhip import SwimCluster
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        scenarios.run_pair("lan4096_c4_shape", lambda *a, **k: ShardedSwimCluster(*a, **k), SwimCluster,
+                           compare_every=4)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_c4_shape_world8_matches_unsharded():
+    """C4's schedule shape (1 % loss, 0.1 % crash, LAN) at 4,096 members over 8 observer-row shards
+    (8 ranks sharing cuda:0, gloo): the exchanges C4's 8-GPU run makes (gossip-id commits, sender
+    windows to remote receivers, SYNC rows) at world 8, bit-exact with the unsharded handle."""
+    mp.spawn(_c4_worker, args=(8, _free_port()), nprocs=8, join=True)
+
+
 def _overflow_worker(rank, world, port):
     from swimhip import ClusterConfig
 
