@@ -60,6 +60,15 @@ extern "C" {
 #define SWIM_EV_ADDED 1
 #define SWIM_EV_REMOVED 2
 #define SWIM_EV_UPDATED 3
+/* the other listen() streams of the reference, in the same ring (not MembershipEvents):
+ * GossipProtocol.listen() (GossipProtocolImpl.java:171-183, sink.next on a new gossip id): a member's
+ * first receipt of a user gossip of swim_spread; subject = the gossip's origin, record = its tag */
+#define SWIM_EV_GOSSIP 8
+/* FailureDetector.listen() (FailureDetectorImpl.java:365-368): one FailureDetectorEvent; subject =
+ * the probed member, record = its status (SWIM_ALIVE, SWIM_SUSPECT or SWIM_DEAD), reason = its index
+ * among the probe's events. Recorded only while swim_trace(SWIM_TRACE_FD) is on. */
+#define SWIM_EV_FD 9
+#define SWIM_TRACE_FD 1u
 
 /* update reasons (MembershipProtocolImpl.java:58-64) */
 #define SWIM_R_FAILURE_DETECTOR_EVENT 0
@@ -211,6 +220,14 @@ int swim_join(swim_handle* h, const uint32_t* ids, uint32_t n);
  * (MembershipProtocolImpl.java:499-505). Dense, unsharded handles. */
 int swim_restart(swim_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n);
 
+/* GossipProtocol.spread (GossipProtocol.java:12-29, GossipProtocolImpl.java:124-128): member
+ * `origin` spreads a user gossip carrying `tag` (the payload stand-in); it is created before the
+ * next period (infectionPeriod = that period's first round), travels like every gossip, and each
+ * member's first receipt is a SWIM_EV_GOSSIP event. Unsharded handles. */
+int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag);
+/* Optional trace streams into the event ring (mask of SWIM_TRACE_*; 0 = off, the default). */
+int swim_trace(swim_handle* h, uint32_t mask);
+
 /* Advance `periods` protocol periods (FD, G gossip rounds, suspicion
  * timeouts, SYNC/SYNC_ACK). Asynchronous to the host only inside the call. */
 int swim_step(swim_handle* h, uint32_t periods);
@@ -252,7 +269,7 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev);
 /* Begin a period (when none is in flight) or resume it after the described exchange. */
 int swim_shard_step(swim_handle* h, swim_xchg* x);
 
-/* MembershipEvents in canonical order (period, observer, phase, subject, type). */
+/* Events in canonical order (period, observer, phase, subject, type, reason, record). */
 int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);
 /* One observer's membershipTable as packed cells (n = n_members; the observer's shard). */
 int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);

@@ -258,6 +258,7 @@ struct oracle_handle {
   std::vector<swim_event> events;
   swim_stats st;
   std::vector<uint32_t> pres, last_removed;
+  uint32_t trace = 0;              // swim_trace mask (SWIM_TRACE_FD: FailureDetectorEvents into the ring)
   std::vector<uint64_t> dbg_send;  // debug: per sender, GossipRequests to alive peers before / by infectedFrom
   uint32_t dbg_watch = 0xFFFFFFFFu;
   // pending gossip-delivered records per receiver: subject -> lattice max
@@ -616,6 +617,8 @@ void do_ping(oracle_handle* h, uint32_t i) {
       for (uint32_t s = 0; s < sent; ++s) evs.push_back(ok ? acked : SWIM_SUSPECT);  // FDI:190-207
     }
   }
+  for (uint32_t k = 0; k < evs.size(); ++k)  // FailureDetector.listen() (FDI:365-368), when traced
+    if (h->trace & SWIM_TRACE_FD) emit_event(h, i, j, SWIM_EV_FD, k, 0, evs[k]);
   for (uint32_t ev : evs) {  // publishPingResult (FDI:365-368) -> MPI:376
     if (ev == SWIM_ALIVE)
       h->st.fd_alive_events++;
@@ -775,6 +778,10 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     gossip_put(h, pm, d.gid, r + 1);
     h->st.gossip_first_receipts++;
     const Gossip& g = h->registry[d.gid];
+    if (g.subject >= h->N) {  // a user gossip (oracle_spread): GossipProtocol.listen() gets it (GPI:176)
+      emit_event(h, d.to, g.subject - h->N, SWIM_EV_GOSSIP, SWIM_R_MEMBERSHIP_GOSSIP, phase, g.record);
+      continue;
+    }
     h->inbox[d.to].push_back({g.subject, g.record});  // sink.next -> onMembershipGossip, batched
   }
   // ... and addToInfected(from) for every message (GPI:181)
@@ -1154,6 +1161,20 @@ int oracle_restart(oracle_handle* h, const uint32_t* old_ids, const uint32_t* ne
   return SWIM_OK;
 }
 
+// GossipProtocolImpl.spread (GPI:124-128) of a user gossip: created before the next period like a
+// leave's gossip; its subject is N + origin (no member), its record the tag
+int oracle_spread(oracle_handle* h, uint32_t origin, uint32_t tag) {
+  if (!h || origin >= h->N || !h->m[origin].alive) return SWIM_EINVAL;
+  spread_gossip(h, origin, h->N + origin, tag, (int64_t)h->period * h->G);
+  return SWIM_OK;
+}
+
+int oracle_trace(oracle_handle* h, uint32_t mask) {
+  if (!h) return SWIM_EINVAL;
+  h->trace = mask;
+  return SWIM_OK;
+}
+
 int oracle_step(oracle_handle* h, uint32_t periods) {
   if (!h) return SWIM_EINVAL;
   for (uint32_t p = 0; p < periods; ++p) step_period(h);
@@ -1167,7 +1188,9 @@ int oracle_drain_events(oracle_handle* h, swim_event* buf, uint64_t cap, uint64_
     if (a.observer != b.observer) return a.observer < b.observer;
     if (a.phase != b.phase) return a.phase < b.phase;
     if (a.subject != b.subject) return a.subject < b.subject;
-    return a.type < b.type;
+    if (a.type != b.type) return a.type < b.type;
+    if (a.reason != b.reason) return a.reason < b.reason;
+    return a.record < b.record;
   });
   uint64_t n = std::min<uint64_t>(cap, h->events.size());
   if (n && buf) std::memcpy(buf, h->events.data(), n * sizeof(swim_event));

@@ -245,7 +245,8 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
     P.batched = 1u;
   }
   CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u, 0u};
-  C.npass = (32u + bitlen(h->N - 1u) + 7u) / 8u;  // key = subject << 32 | record
+  // key = subject << 32 | record (user gossips: subject N + origin) or origin << 32 | subject
+  C.npass = (32u + bitlen(2u * h->N - 1u) + 7u) / 8u;
   // launch the radix kernels only when the batch may need them: the sharded batch size is known
   // here; a local stage is bounded by the phase (`bound`: a gossip round stages at most one
   // refutation per member, MPI:549-569; k_commit fails loudly if a bound is ever exceeded)
@@ -1160,6 +1161,22 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
   return SWIM_OK;
 }
 
+int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag) {
+  if (!h || origin >= h->N) return SWIM_EINVAL;
+  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_spread: not supported on sharded handles");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_spread: a period is in flight");
+  hipLaunchKernelGGL(k_spread, dim3(1), dim3(64), 0, h->stream, h->base, origin, tag);
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
+int swim_trace(swim_handle* h, uint32_t mask) {
+  if (!h || (mask & ~SWIM_TRACE_FD)) return SWIM_EINVAL;
+  h->base.trace = mask;
+  return SWIM_OK;
+}
+
 int swim_step_async(swim_handle* h, uint32_t periods) {
   if (!h) return SWIM_EINVAL;
   if (h->world > 1) return fail(h, SWIM_EINVAL, "sharded handle: use swim_shard_step");
@@ -1198,7 +1215,9 @@ int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n
     if (a.observer != b.observer) return a.observer < b.observer;
     if (a.phase != b.phase) return a.phase < b.phase;
     if (a.subject != b.subject) return a.subject < b.subject;
-    return a.type < b.type;
+    if (a.type != b.type) return a.type < b.type;
+    if (a.reason != b.reason) return a.reason < b.reason;
+    return a.record < b.record;
   });
   const uint64_t n = std::min<uint64_t>(cap, ev.size());
   if (n && buf) std::memcpy(buf, ev.data(), n * sizeof(swim_event));

@@ -209,6 +209,7 @@ struct KP {
   uint32_t* wsum;     // [GC/32] gossips in a word's slots (counters weight a slot by its gossips)
   uint32_t batch_commit;  // this phase's commit groups gossips into batches by origin (loss_mode != 1)
   uint32_t batched;       // batching is on and has been used: counters weight slots, apply expands records
+  uint32_t trace;         // swim_trace mask: SWIM_TRACE_FD puts FailureDetectorEvents into the event ring
   uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
                       // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips

@@ -96,6 +96,17 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
   add_stat(P, ST_GOSSIPS_CREATED, created);
 }
 
+// swim_spread: a user gossip (GossipProtocolImpl.spread, :124-128) staged like a leave's gossip;
+// its subject is N + origin (no member: apply hands it to GossipProtocol.listen, not to membership)
+__global__ void k_spread(KP P, uint32_t origin, uint32_t tag) {  // one wave; lane 0 does the work
+  uint32_t created = 0;
+  if (threadIdx.x == 0 && P.alive[origin] && is_local(P, origin)) {
+    emit_gossip(P, origin, P.N + origin, tag, P.gseq[origin]++);
+    created = 1;
+  }
+  add_stat(P, ST_GOSSIPS_CREATED, created);
+}
+
 // converged start with spare slots: cell (row, col) = BASELINE for col < n0, absent otherwise
 __global__ void k_init_rows(uint32_t* view, size_t n, uint32_t W, uint32_t n0) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -327,7 +338,8 @@ __device__ __forceinline__ uint32_t commit_block(const KP& P, uint32_t g0, uint3
     if (i >= n) break;
     if (op[q]) ++ci;
     const unsigned long long prev = q ? kk[q - 1] : kp;
-    const bool run = P.batch_commit || i == 0u || (prev >> 32) != (kk[q] >> 32);  // a subject run starts
+    // a subject run starts (a user gossip, subject >= N, is a run of its own: each is delivered)
+    const bool run = P.batch_commit || i == 0u || (prev >> 32) != (kk[q] >> 32) || (uint32_t)(kk[q] >> 32) >= P.N;
     commit_one(P, g0, c0, i, ci - 1u, kk[q], val(i), op[q], i + 1u == n || op[q + 1], run);
   }
   return tot;
@@ -821,6 +833,7 @@ __global__ void __launch_bounds__(256) k_fd(KP P) {
     const uint32_t snap = P.cnt[i];
     for (uint32_t e = 0; e < pr.nA + pr.nB; ++e) {
       const uint32_t st = e < pr.nA ? (uint32_t)SWIM_SUSPECT : pr.stB;
+      if (P.trace & SWIM_TRACE_FD) push_event(P, i, j, SWIM_EV_FD, e, st);  // FailureDetector.listen()
       if (st == SWIM_ALIVE)
         ++aev;
       else if (st == SWIM_DEAD)
@@ -2172,6 +2185,10 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j) {
           if (j >= nl) break;
+          if (sr[j].x >= P.N) {  // a user gossip: GossipProtocol.listen() (GossipProtocolImpl.java:176)
+            push_event(P, p, sr[j].x - P.N, SWIM_EV_GOSSIP, SWIM_R_MEMBERSHIP_GOSSIP, sr[j].y);
+            continue;
+          }
           uint32_t h = (sr[j].x * 0x9E3779B1u) >> (32u - lg);
           bool placed = false;
           for (uint32_t q = 0; q < HPROBE; ++q) {
@@ -2544,6 +2561,10 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
     // lattice max per subject; a plain read first settles most repeats without atomics
     bool rowscan = false;  // the spill list overflowed: scan the whole inbox row at the end
     auto insert = [&](uint2 sr) {
+      if (sr.x >= P.N) {  // a user gossip: GossipProtocol.listen() (GossipProtocolImpl.java:176)
+        push_event(P, p, sr.x - P.N, SWIM_EV_GOSSIP, SWIM_R_MEMBERSHIP_GOSSIP, sr.y);
+        return;
+      }
       uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
       for (uint32_t q = 0; q < HPROBE; ++q) {
         uint32_t k = s_key[h];

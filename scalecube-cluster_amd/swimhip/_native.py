@@ -25,6 +25,8 @@ SWIM_EOVERFLOW = -75
 ABSENT, ALIVE, SUSPECT, DEAD = 0, 1, 2, 0xFFFFFFFF
 
 EV_ADDED, EV_REMOVED, EV_UPDATED = 1, 2, 3
+EV_GOSSIP, EV_FD = 8, 9  # GossipProtocol.listen() / FailureDetector.listen() streams (include/swimhip.h)
+TRACE_FD = 1
 R_FAILURE_DETECTOR_EVENT, R_MEMBERSHIP_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_SUSPICION_TIMEOUT = 0, 1, 2, 3, 4
 
 
@@ -160,6 +162,8 @@ def api_table(prefix: str):
         (prefix + "leave", _I, [_P, _pU32, _U32]),
         (prefix + "join", _I, [_P, _pU32, _U32]),
         (prefix + "restart", _I, [_P, _pU32, _pU32, _U32]),
+        (prefix + "spread", _I, [_P, _U32, _U32]),
+        (prefix + "trace", _I, [_P, _U32]),
         (prefix + "step", _I, [_P, _U32]),
         (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
         (prefix + "read_view", _I, [_P, _U32, _pU32, _U32]),

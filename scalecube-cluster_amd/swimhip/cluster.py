@@ -51,6 +51,12 @@ class MembershipEvent:
     def isUpdated(self):
         return self.type == nat.EV_UPDATED
 
+    def isGossip(self):  # GossipProtocol.listen(): first receipt of a user gossip (member = origin)
+        return self.type == nat.EV_GOSSIP
+
+    def isFailureDetector(self):  # FailureDetectorEvent: member = probed member, record = status
+        return self.type == nat.EV_FD
+
     def key(self):
         return (self.period, self.observer, self.phase, self.member, self.type, self.reason, self.record)
 
@@ -165,6 +171,15 @@ class SwimCluster:
         drops that gossip."""
         ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
         self._call("leave", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+
+    def spread(self, origin: int, tag: int):
+        """GossipProtocol.spread (GossipProtocolImpl.java:124-128) of a user gossip by member
+        `origin`; every member's first receipt shows up as an EV_GOSSIP event (GossipProtocol.listen)."""
+        self._call("spread", self._h, int(origin), int(tag) & 0xFFFFFFFF)
+
+    def trace(self, fd: bool = True):
+        """FailureDetector.listen() (FailureDetectorImpl.java:365-368) into the event ring as EV_FD."""
+        self._call("trace", self._h, nat.TRACE_FD if fd else 0)
 
     def join(self, ids):
         """ClusterImpl.start() of new members in spare slots (ids >= n_initial), each at an address

@@ -99,6 +99,144 @@ def fd_trusted_despite_bad_network(make):
             assert_suspected(c, m)
 
 
+# -- FailureDetectorTest on the FailureDetectorEvent stream (swim_trace, EV_FD) ------------
+# The reference asserts the next FailureDetectorEvent each detector publishes about each member
+# (listenNextEventFor / assertStatus, FailureDetectorTest.java:444-494). FailureDetectorImpl runs
+# alone there; here membership runs on top, with a suspicion timeout and a SYNC interval far past
+# every test window, so no member is ever removed and every FD keeps probing every member, as in
+# the FD-only test.
+def fd_events_config(n, fd=None):
+    cfg = fd_test_config(n) if fd is None else ClusterConfig.defaultLocalConfig().failureDetector(
+        lambda o: fd).membership(lambda o: o.seedMembers(list(range(n))))
+    return cfg.membership(lambda o: o.suspicionMult(1000).syncInterval(10 ** 7))
+
+
+def next_fd_events(c, members, max_periods=50):
+    """listenNextEventFor(fd, members) of every member: the first FailureDetectorEvent each one
+    publishes about each other member from now on (awaitEvents waits up to 10 s: max_periods)."""
+    c.events()
+    want = {(o, s) for o in members for s in members if o != s}
+    first = {}
+    for _ in range(max_periods):
+        c.step(1)
+        for e in c.events():
+            if e.isFailureDetector() and (e.observer, e.member) in want and (e.observer, e.member) not in first:
+                first[(e.observer, e.member)] = e.record
+        if len(first) == len(want):
+            break
+    assert len(first) == len(want), f"no FD event yet for {sorted(want - set(first))}"
+    return first
+
+
+def assert_fd_status(first, obs, status, *expected):
+    """assertStatus (:465-487): the members obs's next events give `status` are exactly `expected`."""
+    got = sorted(s for (o, s), st in first.items() if o == obs and st == status)
+    assert got == sorted(expected), f"member {obs}: {status} events about {got}, expected {sorted(expected)}"
+
+
+ALIVE_ST, SUSPECT_ST = 1, 2
+
+
+def fd_events_trusted(make):
+    """testTrusted (:50-77): clean network, every next event is ALIVE."""
+    c = make(fd_events_config(3), 3, 61)
+    c.trace(True)
+    first = next_fd_events(c, (A, B, C))
+    for m in (A, B, C):
+        assert_fd_status(first, m, ALIVE_ST, *[x for x in (A, B, C) if x != m])
+
+
+def fd_events_suspected(make):
+    """testSuspected (:79-114): every member blocks all its outbound traffic: every event SUSPECT."""
+    c = make(fd_events_config(3), 3, 62)
+    c.trace(True)
+    for m in (A, B, C):
+        block_outbound(c, m, (A, B, C))
+    first = next_fd_events(c, (A, B, C))
+    for m in (A, B, C):
+        assert_fd_status(first, m, SUSPECT_ST, *[x for x in (A, B, C) if x != m])
+
+
+def fd_events_trusted_despite_bad_network(make):
+    """testTrustedDespiteBadNetwork (:116-146): a -> b blocked; the ping-req through c keeps every
+    event ALIVE."""
+    c = make(fd_events_config(3), 3, 63)
+    c.trace(True)
+    block_outbound(c, A, (B,))
+    first = next_fd_events(c, (A, B, C))
+    for m in (A, B, C):
+        assert_fd_status(first, m, ALIVE_ST, *[x for x in (A, B, C) if x != m])
+
+
+def fd_events_trusted_despite_different_ping_timings(make):
+    """testTrustedDespiteDifferentPingTimings (:148-176): b and c run FailureDetectorConfig
+    defaults (ping 1,000 / timeout 500). The simulator steps every member with one config, so the
+    whole cluster runs the defaults: clean network, every next event ALIVE."""
+    c = make(fd_events_config(3, FailureDetectorConfig.defaultConfig()), 3, 64)
+    c.trace(True)
+    first = next_fd_events(c, (A, B, C))
+    for m in (A, B, C):
+        assert_fd_status(first, m, ALIVE_ST, *[x for x in (A, B, C) if x != m])
+
+
+def fd_events_suspected_member_with_bad_network(make):
+    """testSuspectedMemberWithBadNetworkGetsPartitioned (:178-236): a blocks its outbound traffic
+    to everyone: a suspects b, c, d; each of them suspects a only. After unblocking and 4 s, every
+    next event is ALIVE."""
+    n = 4
+    c = make(fd_events_config(n), n, 65)
+    c.trace(True)
+    block_outbound(c, A, (A, B, C, D))
+    first = next_fd_events(c, (A, B, C, D))
+    assert_fd_status(first, A, SUSPECT_ST, B, C, D)
+    for m in (B, C, D):
+        assert_fd_status(first, m, SUSPECT_ST, A)
+    unblock_all_outbound(c, A)
+    c.step(seconds(4))
+    first = next_fd_events(c, (A, B, C, D))
+    for m in (A, B, C, D):
+        assert_fd_status(first, m, ALIVE_ST, *[x for x in (A, B, C, D) if x != m])
+
+
+def fd_events_suspected_member_with_normal_network(make):
+    """testSuspectedMemberWithNormalNetworkGetsPartitioned (:238-299): a, b, c block their traffic
+    to d: they suspect d, d suspects all three (its acks come back through them). After
+    unblocking and 4 s, every next event is ALIVE."""
+    n = 4
+    c = make(fd_events_config(n), n, 66)
+    c.trace(True)
+    for m in (A, B, C):
+        block_outbound(c, m, (D,))
+    first = next_fd_events(c, (A, B, C, D))
+    for m in (A, B, C):
+        assert_fd_status(first, m, SUSPECT_ST, D)
+    assert_fd_status(first, D, SUSPECT_ST, A, B, C)
+    for m in (A, B, C):
+        unblock_all_outbound(c, m)
+    c.step(seconds(4))
+    first = next_fd_events(c, (A, B, C, D))
+    for m in (A, B, C, D):
+        assert_fd_status(first, m, ALIVE_ST, *[x for x in (A, B, C, D) if x != m])
+
+
+def fd_events_status_change_after_network_recovery(make):
+    """testMemberStatusChangeAfterNetworkRecovery (:301-341): a and b block each other: both
+    suspect; unblocked, within 2 s both are ALIVE again."""
+    c = make(fd_events_config(2), 2, 67)
+    c.trace(True)
+    block_outbound(c, A, (B,))
+    block_outbound(c, B, (A,))
+    first = next_fd_events(c, (A, B))
+    assert_fd_status(first, A, SUSPECT_ST, B)
+    assert_fd_status(first, B, SUSPECT_ST, A)
+    unblock_all_outbound(c, A)
+    unblock_all_outbound(c, B)
+    c.step(seconds(2))
+    first = next_fd_events(c, (A, B))
+    assert_fd_status(first, A, ALIVE_ST, B)
+    assert_fd_status(first, B, ALIVE_ST, A)
+
+
 # -- MembershipProtocolTest ---------------------------------------------------------------
 def mp_initial_phase_ok(make):
     """testInitialPhaseOk (:68-91)."""
@@ -392,6 +530,58 @@ def gossip_dissemination_bound(make):
         assert all(c.view(o)[n - 1] == 0 for o in range(n - 1)), (n, loss)
 
 
+# -- GossipProtocolTest (:48-64 grid, asserts :154, :155-161, :173) ------------------------
+# (N, loss %) of the reference's experiments; its mean delays (2 ms, and 100 ms in two rows) are
+# below one gossip interval (200 ms): until the delay model exists every row
+# runs with deliveries inside the round, i.e. at the 2 ms setting.
+GOSSIP_GRID = [(2, 0), (2, 0), (3, 0), (5, 0), (10, 0), (10, 10), (10, 25), (10, 25), (10, 50), (50, 0), (50, 10),
+               (50, 10)]
+
+
+def gossip_test_config(n):
+    """GossipProtocolTest.initGossipProtocol (:258-263): GossipConfig defaults (fanout 3, interval
+    200 ms, repeat mult 3). The test runs GossipProtocolImpl alone on a fixed member list; here
+    membership runs too, with no removal and no SYNC inside the window (the member list stays
+    fixed, as there)."""
+    return ClusterConfig.defaultLanConfig().membership(lambda o: o.suspicionMult(1000).syncInterval(10 ** 7))
+
+
+def gossip_protocol_grid(make):
+    """testGossipProtocol (:110-208): member 0 spreads one gossip; every other member receives it
+    (:154) within gossipTimeoutToSweep (:155-161), and no member has it delivered twice (:173),
+    over the whole gossip lifetime plus three intervals (awaitFullCompletion, :163-169)."""
+    for idx, (n, loss) in enumerate(GOSSIP_GRID):
+        cfg = gossip_test_config(n)
+        g = cfg.gossipConfig()
+        interval = g.gossipInterval()
+        rounds_per_period = cfg.failureDetectorConfig().pingInterval() // interval
+        c = make(cfg, n, 300 + idx)
+        c.set_loss(loss)
+        c.step(1)
+        c.events()
+        tag = 0x5EED0000 + idx
+        p0 = c.stats()["period"]
+        c.spread(0, tag)  # created for round p0 * G (the next period's first round)
+        timeout_ms = cluster_math.gossipTimeoutToSweep(g.gossipRepeatMult(), n, interval)
+        # the latch waits 2 x gossipTimeout (:152); then the rest of the lifetime + 3 intervals
+        total_rounds = 2 * timeout_ms // interval + 3
+        first, double = {}, []
+        for _ in range((total_rounds + rounds_per_period - 1) // rounds_per_period):
+            c.step(1)
+            for e in c.events():
+                if e.isGossip() and e.record == tag and e.member == 0:
+                    r = e.period * rounds_per_period + e.phase - 1  # the round it arrived in
+                    if e.observer in first:
+                        double.append(e.observer)
+                    else:
+                        first[e.observer] = r
+        assert set(first) == set(range(1, n)), (n, loss, "Not all members received gossip")
+        # dissemination time: spread to the end of the round the last member got it in
+        dissem_ms = (max(first.values()) + 1 - p0 * rounds_per_period) * interval if first else 0
+        assert dissem_ms < timeout_ms, (n, loss, f"Too long dissemination time {dissem_ms}ms (timeout {timeout_ms}ms)")
+        assert not double, (n, loss, "Delivered gossip twice to same member", double)
+
+
 def mp_restart_stopped_members(make):
     """testRestartStoppedMembers (:374-451): c and d stop; a and b suspect, then remove them; new
     members start on new addresses (spare ids 4 and 5) with the four old addresses as seeds and
@@ -450,6 +640,10 @@ def mp_restart_on_same_addresses(make):
 
 ALL = [
     fd_trusted, fd_suspected, fd_trusted_despite_bad_network,
+    fd_events_trusted, fd_events_suspected, fd_events_trusted_despite_bad_network,
+    fd_events_trusted_despite_different_ping_timings, fd_events_suspected_member_with_bad_network,
+    fd_events_suspected_member_with_normal_network, fd_events_status_change_after_network_recovery,
+    gossip_protocol_grid,
     mp_initial_phase_ok, mp_partition_no_outbound_then_recover, mp_member_lost_network_then_recover,
     mp_partition_twice_then_recover, mp_network_lost_on_all_nodes_then_recover, mp_long_partition_then_removed,
     mp_partition_no_inbound_then_removed, mp_partition_no_inbound_then_recover, mp_between_two_members_no_inbound,
