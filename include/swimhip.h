@@ -170,6 +170,8 @@ typedef struct swim_stats {
   uint64_t apply_spills;      /* subjects k_gossip_apply merged through the global inbox (LDS hash full); 0 in the oracle */
   uint64_t apply_records;     /* gossip records of batch slots expanded by k_gossip_apply; 0 in the oracle */
   uint64_t live_gossip_records; /* gossips held in the live ring slots (live_gossip_slots counts batches) */
+  uint64_t events_updated;    /* MembershipEvent UPDATED: an accepted ALIVE record whose fetched
+                                 metadata differs from the stored one (MembershipProtocolImpl.java:589-610) */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -203,6 +205,14 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
  * keeps running until its own sweep drops that gossip (spread() completes at sweep,
  * GossipProtocolImpl.java:299-302), then stops at the end of that gossip round. Unsharded handles. */
 int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n);
+
+/* Cluster.updateMetadata (ClusterImpl.java:364-367): each member's metadata changes (a new version;
+ * MetadataStoreImpl.updateMetadata) and MembershipProtocolImpl.updateIncarnation (:184-196) makes its
+ * own record ALIVE with incarnation + 1 and spreads it. Observers that accept the new record fetch the
+ * metadata (MetadataStoreImpl.fetchMetadata :151-193) and, for a member they already had, emit UPDATED
+ * when it differs from the one they stored (onAliveMemberDetected :589-610). Takes effect before the
+ * next period. Unsharded handles. */
+int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n);
 
 /* Join = a new member's ClusterImpl.start() (ClusterImpl.java:170-227): spare slot `ids[k]` (never
  * started) starts before the next period at an address of its own with a table holding only itself

@@ -203,6 +203,8 @@ struct Batch {
 
 struct Member {
   std::vector<uint32_t> table;          // MPI:87 membershipTable (+ MPI:88 members: cell != 0)
+  std::vector<uint32_t> meta;           // MetadataStoreImpl.membersMetadata: the version of each member's
+                                        // metadata this member fetched last (MetadataStoreImpl.java:112-135)
   uint32_t others = 0;                  // members.size() - 1 == pingMembers == remoteMembers
   int32_t delta = 0;                    // deferred member-count change of the current phase
   std::map<uint32_t, uint64_t> timers;  // MPI:101 suspicionTimeoutTasks: subject -> fire period
@@ -258,6 +260,7 @@ struct oracle_handle {
   std::vector<swim_event> events;
   swim_stats st;
   std::vector<uint32_t> pres, last_removed;
+  std::vector<uint32_t> meta_cur;  // each member's own metadata version (MetadataStoreImpl.updateMetadata, :107-110)
   uint32_t trace = 0;              // swim_trace mask (SWIM_TRACE_FD: FailureDetectorEvents into the ring)
   std::vector<uint64_t> dbg_send;  // debug: per sender, GossipRequests to alive peers before / by infectedFrom
   uint32_t dbg_watch = 0xFFFFFFFFu;
@@ -329,6 +332,7 @@ void emit_event(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t type, ui
                 uint32_t record) {
   if (type == SWIM_EV_ADDED) h->st.events_added++;
   if (type == SWIM_EV_REMOVED) h->st.events_removed++;
+  if (type == SWIM_EV_UPDATED) h->st.events_updated++;
   if (h->cfg.event_capacity == 0) return;
   swim_event e;
   std::memset(&e, 0, sizeof e);
@@ -503,12 +507,17 @@ void update_membership(oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t r
   if (!fetch_ok(h, obs, subj, attempt, tick)) return;  // MPI:540 failed fetch silently skipped
   me.timers.erase(subj);                               // MPI:534
   if (spread) spread_gossip(h, obs, subj, r1, create_round);  // MPI:535
+  // the fetched metadata (the subject's current version) replaces the stored one (MPI:537)
+  const uint32_t m1 = h->meta_cur[subj], m0 = me.meta[subj];
+  me.meta[subj] = m1;
   cell = r1;                                                  // MPI:604
   h->st.records_accepted++;
-  if (r0 == SWIM_ABSENT) {  // MPI:597-598 ADDED (UPDATED needs metadata versions: not modelled)
+  if (r0 == SWIM_ABSENT) {  // MPI:597-598 ADDED
     me.delta += 1;
     if (me.alive && subj != obs) h->pres[subj]++;
     emit_event(h, obs, subj, SWIM_EV_ADDED, reason, phase, r1);
+  } else if (m1 != m0) {  // MPI:599-600 UPDATED: metadata differs from the stored one
+    emit_event(h, obs, subj, SWIM_EV_UPDATED, reason, phase, r1);
   }
 }
 
@@ -1022,6 +1031,7 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
       std::fill(h->m[i].table.begin(), h->m[i].table.begin() + n0, SWIM_PACK(0, SWIM_ALIVE));
       h->m[i].others = n0 - 1;
       h->m[i].alive = i < n0;
+      h->m[i].meta.assign(h->N, 0);  // the converged start shares every member's initial metadata
       h->m[i].gossips.held.assign(h->rc / 64, 0);
       h->m[i].gossips.win.assign(h->rc / 64, 0);
       h->m[i].gossips.inf.assign(h->rc, 0);
@@ -1030,6 +1040,7 @@ int oracle_create(const swim_config* cfg, oracle_handle** out) {
     h->pres.assign(h->N, 0);
     std::fill(h->pres.begin(), h->pres.begin() + n0, n0 - 1);
     h->last_removed.assign(h->N, 0);
+    h->meta_cur.assign(h->N, 0);
     h->dbg_send.assign(2ull * h->N, 0);
     if (const char* w = std::getenv("SWIMHIP_DEBUG_WATCH")) h->dbg_watch = (uint32_t)std::strtoul(w, nullptr, 10);
     h->addr.resize(h->N);
@@ -1118,12 +1129,32 @@ int oracle_leave(oracle_handle* h, const uint32_t* ids, uint32_t n) {
   return SWIM_OK;
 }
 
+// Cluster.updateMetadata (ClusterImpl.java:364-367): MetadataStoreImpl.updateMetadata (a new local
+// version), then MembershipProtocolImpl.updateIncarnation (MPI:184-196): the own record becomes ALIVE
+// with incarnation + 1 and is spread (spreadMembershipGossip: always). Before the next period.
+int oracle_update_metadata(oracle_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k)
+    if (ids[k] >= h->N) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t i = ids[k];
+    Member& me = h->m[i];
+    if (!me.alive || me.leaving) continue;
+    h->meta_cur[i]++;
+    const uint32_t r = SWIM_PACK(inc_of(me.table[i]) + 1u, SWIM_ALIVE);
+    me.table[i] = r;
+    spread_gossip(h, i, i, r, (int64_t)h->period * h->G);
+  }
+  return SWIM_OK;
+}
+
 // A new member starts in spare slot x at address a (ClusterImpl.start, ClusterImpl.java:170-227):
 // its table holds only itself ALIVE inc 0 (MPI:138-142), every protocol cursor starts afresh, and
 // this period's SYNC phase makes its initial SYNC to the seeds (MPI:222-257).
 void start_member(oracle_handle* h, uint32_t x, uint32_t a) {
   Member& me = h->m[x];
   std::fill(me.table.begin(), me.table.end(), SWIM_ABSENT);
+  std::fill(me.meta.begin(), me.meta.end(), 0u);
   me.table[x] = SWIM_PACK(0, SWIM_ALIVE);
   me.others = 0;
   me.delta = 0;

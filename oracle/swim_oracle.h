@@ -35,6 +35,7 @@ int oracle_block_link(oracle_handle* h, uint32_t src, uint32_t dst, int blocked)
 int oracle_block_inbound(oracle_handle* h, uint32_t dst, uint32_t src, int blocked);
 int oracle_crash(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_leave(oracle_handle* h, const uint32_t* ids, uint32_t n);
+int oracle_update_metadata(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_join(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_restart(oracle_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n);
 int oracle_spread(oracle_handle* h, uint32_t origin, uint32_t tag);

@@ -843,6 +843,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.events, std::max<uint32_t>(1, h->ecap));
   ALLOC(P.pres, N);
   ALLOC(P.last_removed, N);
+  ALLOC(P.meta_cur, N);
+  P.meta_view = nullptr;  // allocated by the first swim_update_metadata
   ALLOC(P.req_to, 2ull * N);
   ALLOC(P.req_stage, 2ull * N);
   ALLOC(P.stage_req, h->scap);
@@ -935,6 +937,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.nb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.meta_cur, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
@@ -1156,6 +1159,32 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
     hipLaunchKernelGGL(k_stop_addr, dim3(1), dim3(64), 0, h->stream, h->base, c);
   }
   HIPC(h, hipMemcpyAsync(h->base.alive, alive.data(), h->N, hipMemcpyHostToDevice, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
+int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n) {
+  if (!h || (n && !ids)) return SWIM_EINVAL;
+  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_update_metadata: not supported on sharded handles");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_update_metadata: a period is in flight");
+  for (uint32_t k = 0; k < n; ++k)
+    if (ids[k] >= h->N) return SWIM_EINVAL;
+  if (!h->base.meta_view) {  // first metadata change: every stored version is the initial one
+    uint32_t* mv = nullptr;
+    const size_t cells = (size_t)h->base.nloc * h->base.W;
+    int rc = dalloc(h, &mv, cells);
+    if (rc) return rc;
+    HIPC(h, hipMemsetAsync(mv, 0, cells * 4, h->stream));
+    h->base.meta_view = mv;
+  }
+  for (uint32_t k = 0; k < n; ++k) {
+    if (h->base.nxk) {  // the member's own record leaves the baseline: give it a column
+      hipLaunchKernelGGL(k_track_one, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+      track_commit(h, h->base);
+    }
+    hipLaunchKernelGGL(k_update_meta, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+  }
   HIPC(h, hipStreamSynchronize(h->stream));
   HIPC(h, hipGetLastError());
   return SWIM_OK;
@@ -1384,6 +1413,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->fd_dead_events = stats[ST_FD_DEAD_EV];
   out->apply_spills = stats[ST_APPLY_SPILL];
   out->apply_records = stats[ST_APPLY_RECS];
+  out->events_updated = stats[ST_UPDATED];
   {  // gossips in the live slots: the record ring from the oldest live slot's first record
     uint32_t c_lo = ctl.ccount;
     if (ctl.gcount != ctl.glo && ctl.gcount - ctl.glo <= h->GC) {

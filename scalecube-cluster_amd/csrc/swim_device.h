@@ -58,6 +58,7 @@ enum StatIdx : int {
   ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
   ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
   ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply expanded into its LDS table
+  ST_UPDATED,      // MembershipEvent UPDATED (MembershipProtocolImpl.java:599-600)
   ST_COUNT
 };
 
@@ -210,6 +211,12 @@ struct KP {
   uint32_t batch_commit;  // this phase's commit groups gossips into batches by origin (loss_mode != 1)
   uint32_t batched;       // batching is on and has been used: counters weight slots, apply expands records
   uint32_t trace;         // swim_trace mask: SWIM_TRACE_FD puts FailureDetectorEvents into the event ring
+  // member metadata (Cluster.updateMetadata, ClusterImpl.java:364-367): each member's current
+  // version, and per (observer, cell) the version the observer fetched last (MetadataStoreImpl
+  // membersMetadata). meta_view is allocated by the first swim_update_metadata: until then every
+  // version is the initial one and no ALIVE record can carry different metadata.
+  uint32_t* meta_cur;   // [N]
+  uint32_t* meta_view;  // [nloc][W] or nullptr
   uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
                       // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
@@ -429,7 +436,7 @@ __device__ __forceinline__ void push_event(const KP& P, uint32_t obs, uint32_t s
 }
 
 struct Tally {
-  uint32_t accepted = 0, refut = 0, added = 0, removed = 0;
+  uint32_t accepted = 0, refut = 0, added = 0, removed = 0, updated = 0;
 };
 
 // GossipProtocolImpl.spread -> createAndPutGossip (GossipProtocolImpl.java:124-128,163-169),
@@ -507,11 +514,22 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
   *dlp = 0u;
   *cellp = r1;
   T.accepted++;
+  // the fetched metadata (the subject's current version) replaces the stored one (MPI:537)
+  bool updated = false;
+  if (P.meta_view) {
+    uint32_t* mp = P.meta_view + lrow(P, obs) * P.W + col;
+    const uint32_t m1 = P.meta_cur[subj];
+    updated = r0 != SWIM_ABSENT && *mp != m1;
+    *mp = m1;
+  }
   if (r0 == SWIM_ABSENT) {
     atomicAdd(&P.cnt_delta[obs], 1);
     atomicAdd(&P.pres[subj], 1u);
     T.added++;
     push_event(P, obs, subj, SWIM_EV_ADDED, reason, r1);
+  } else if (updated) {  // MPI:599-600: a member it had, with metadata that differs
+    T.updated++;
+    push_event(P, obs, subj, SWIM_EV_UPDATED, reason, r1);
   }
   return spread ? r1 : 0u;
 }
@@ -551,6 +569,7 @@ __device__ __forceinline__ void flush_tally(const KP& P, const Tally& T) {
   add_stat(P, ST_REFUTATIONS, T.refut);
   add_stat(P, ST_ADDED, T.added);
   add_stat(P, ST_REMOVED, T.removed);
+  add_stat(P, ST_UPDATED, T.updated);
 }
 
 }  // namespace swim

@@ -107,6 +107,27 @@ __global__ void k_spread(KP P, uint32_t origin, uint32_t tag) {  // one wave; la
   add_stat(P, ST_GOSSIPS_CREATED, created);
 }
 
+// swim_update_metadata: MetadataStoreImpl.updateMetadata (a new version of the member's metadata)
+// and MembershipProtocolImpl.updateIncarnation (MPI:184-196): the own record becomes ALIVE with
+// incarnation + 1 and is staged as a gossip (spreadMembershipGossip: always spread)
+__global__ void k_update_meta(KP P, uint32_t i) {  // one wave; lane 0 does the work
+  uint32_t created = 0;
+  if (threadIdx.x == 0 && P.alive[i] && !P.leaving[i]) {
+    P.meta_cur[i] += 1u;
+    const uint32_t col = col_of(P, i);  // N x K: k_track_one asked for a column
+    if (col == NONE) {
+      atomicOr(&P.ctl->overflow, OV_TRACK);
+    } else if (is_local(P, i)) {
+      uint32_t* cellp = P.view + lrow(P, i) * P.W + col;
+      const uint32_t r = SWIM_PACK(rec_inc(*cellp) + 1u, SWIM_ALIVE);
+      *cellp = r;
+      emit_gossip(P, i, i, r, P.gseq[i]++);
+      created = 1;
+    }
+  }
+  add_stat(P, ST_GOSSIPS_CREATED, created);
+}
+
 // converged start with spare slots: cell (row, col) = BASELINE for col < n0, absent otherwise
 __global__ void k_init_rows(uint32_t* view, size_t n, uint32_t W, uint32_t n0) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -131,6 +152,7 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
   for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
     P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
     P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
+    if (P.meta_view) P.meta_view[lrow(P, x) * P.W + c] = 0u;
   }
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;

@@ -115,6 +115,7 @@ STAT_FIELDS = [
     "apply_spills",
     "apply_records",
     "live_gossip_records",
+    "events_updated",
 ]
 
 
@@ -162,6 +163,7 @@ def api_table(prefix: str):
         (prefix + "leave", _I, [_P, _pU32, _U32]),
         (prefix + "join", _I, [_P, _pU32, _U32]),
         (prefix + "restart", _I, [_P, _pU32, _pU32, _U32]),
+        (prefix + "update_metadata", _I, [_P, _pU32, _U32]),
         (prefix + "spread", _I, [_P, _U32, _U32]),
         (prefix + "trace", _I, [_P, _U32]),
         (prefix + "step", _I, [_P, _U32]),

@@ -172,6 +172,13 @@ class SwimCluster:
         ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
         self._call("leave", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
 
+    def update_metadata(self, ids):
+        """Cluster.updateMetadata (ClusterImpl.java:364-367) of each member: a new metadata version
+        and updateIncarnation (MembershipProtocolImpl.java:184-196): its own record ALIVE with
+        incarnation + 1, spread; members that had it emit UPDATED once they fetch the new metadata."""
+        ids = np.ascontiguousarray(np.asarray(list(ids), dtype=np.uint32))
+        self._call("update_metadata", self._h, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids))
+
     def spread(self, origin: int, tag: int):
         """GossipProtocol.spread (GossipProtocolImpl.java:124-128) of a user gossip by member
         `origin`; every member's first receipt shows up as an EV_GOSSIP event (GossipProtocol.listen)."""

@@ -14,7 +14,7 @@ PARITY_KEYS = [
     "period", "fd_probes", "fd_direct_ok", "fd_ping_req", "fd_suspect_events", "fd_alive_events",
     "gossips_created", "gossip_first_receipts", "gossip_sends", "syncs_sent", "syncs_delivered",
     "sync_acks_delivered", "records_accepted", "events_added", "events_removed", "suspicion_timeouts",
-    "refutations", "not_converged", "infected_suppressed", "fd_dead_events",
+    "refutations", "not_converged", "infected_suppressed", "fd_dead_events", "events_updated",
 ]
 
 
@@ -143,6 +143,25 @@ def _churn(c, crash, restart_new, join_new, loss, before=3, mid=4, after=25):
         yield
 
 
+def _metadata(c, loss):
+    # Cluster.updateMetadata (ClusterImpl.java:364-367) -> updateIncarnation (MembershipProtocolImpl.
+    # java:184-196): the updated members' ALIVE records with incarnation + 1 spread; every member
+    # that had them fetches the new metadata and emits UPDATED (:589-610). A second update of one
+    # member, a crash in between, and (with loss) fetches that fail and are silently skipped (:540).
+    c.set_loss(loss)
+    c.step(3)
+    yield
+    c.update_metadata([3, 10, 20])
+    for _ in range(3):
+        c.step(1)
+        yield
+    c.update_metadata([10])
+    c.crash([5])
+    for _ in range(20):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -167,6 +186,8 @@ SCENARIOS = {
     "local40_restart_join": (
         ClusterConfig.defaultLocalConfig().membership(lambda o: o.seedMembers([0, 1, 2]).syncInterval(3000)),
         40, 11, lambda c: _churn(c, [3, 7, 20], [32, 33], [34, 35], 0.0), {"n_initial": 32}),
+    "local64_update_metadata": (ClusterConfig.defaultLocalConfig(), 64, 14, lambda c: _metadata(c, 0.0)),
+    "lan128_update_metadata_loss10": (ClusterConfig.defaultLanConfig(), 128, 15, lambda c: _metadata(c, 10.0)),
     "lan288_restart_join_loss5": (
         ClusterConfig.defaultLanConfig().membership(lambda o: o.seedMembers([0, 1, 2, 3])),
         288, 12, lambda c: _churn(c, [5, 40, 41, 100, 200, 255], [256, 257, 258, 259], [260, 261, 262], 5.0),
