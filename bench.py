@@ -58,9 +58,8 @@ WORKLOADS = {
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
                     "crashes (concurrent churn), suspicion-timeout sweep",
                n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 17, tracked=256),
-    # The SYNC re-spread storm of 256 simultaneous crashes at 2^20 members (~1.2e6 live gossips, each
-    # held by every member: DESIGN.md §6) exceeds any per-member holdings that fit one GPU, so the
-    # full-size N x K geometry is also measured with the churn it can hold exactly:
+    # round 2's stand-in for C5 (before gossip batches, DESIGN.md §3.12, its 256-crash storm did not
+    # fit one GPU): the full-size N x K geometry with the churn per-gossip holdings could hold
     "c5g": dict(desc="C5 geometry at 1,048,576 members: N x K tracked-subject views (K = 256), LAN defaults, 8 "
                      "simultaneous crashes, suspicion-timeout sweep",
                 n=1 << 20, preset="lan", loss=0.0, crash_n=8, part=0, gcap=1 << 17, tracked=256),
@@ -71,6 +70,11 @@ WORKLOADS = {
     "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
                     "0.1% simultaneous crash",
                n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 19, scap=4096),
+    # C4's schedule on ONE GPU in N x K mode (the dense 262,144^2 view needs 8 GPUs): measures the
+    # storm C4's 1 % loss and 0.1 % crash create, to size C4's ring (1 % loss: one gossip per slot)
+    "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
+                       "0.1% simultaneous crash",
+                  n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 18, tracked=1024),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }

@@ -64,6 +64,7 @@ struct swim_handle {
   uint32_t n_out_pairs = 0, n_in_pairs = 0, nneed = 0;
   uint32_t out_pairs[SWIM_MAX_WORLD] = {0};
   unsigned long long* d_digest = nullptr;
+  uint32_t* d_scan = nullptr;  // k_scan_tiles sums and their exclusive scan
   std::vector<void*> allocs;
   std::string err;
   // timing
@@ -535,7 +536,12 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
           if (n_rec) hipLaunchKernelGGL(k_sync_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 7, "k_scan", [&] { hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, P); });
+        timed(h, 7, "k_scan", [&] {
+          const uint32_t nt = blocks_for(N, SCAN_TILE);
+          hipLaunchKernelGGL(k_scan_tiles, dim3(nt), dim3(1024), 0, s, P, h->d_scan);
+          hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(CS_THREADS), 0, s, h->d_scan, h->d_scan + nt, nt);
+          hipLaunchKernelGGL(k_scan_apply, dim3(nt), dim3(1024), 0, s, P, h->d_scan + nt, nt);
+        });
         timed(h, 7, "k_sync_scatter", [&] {
           hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(2ull * nloc, 256)), dim3(256), 0, s, P);
         });
@@ -879,6 +885,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.ctl, 1);
   ALLOC(P.stat_shards, (size_t)STAT_SHARDS * STAT_STRIDE);
   ALLOC(h->d_digest, 2);
+  ALLOC(h->d_scan, 2ull * ((N + SCAN_TILE - 1) / SCAN_TILE));
 #undef ALLOC
   P.group = group;
   if (rc != SWIM_OK) {

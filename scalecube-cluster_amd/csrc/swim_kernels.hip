@@ -2979,12 +2979,16 @@ __device__ __forceinline__ uint32_t sweep_cell(const KP& P, uint32_t j, uint32_t
     return v;
   }
   uint32_t* cellp = P.view + (size_t)li * P.W + j;
-  const uint32_t r0 = *cellp;
+  const uint32_t subj = subj_of(P, j);
+  const bool general = subj == i || (P.rerouted && P.addr[subj] == P.addr[i]);  // (never in practice)
+  // A deadline implies a record: every path that clears a cell clears its deadline too (DEAD
+  // accepted, crash, join, leave stop), so without an event to fill (ecap = 0, the bench) the
+  // strided view read is skipped and the cell just written.
+  const uint32_t r0 = (general || P.ecap) ? *cellp : SWIM_SUSPECT;
   if (r0 != 0u) {
     ++*fired;
-    const uint32_t subj = subj_of(P, j);
-    if (subj == i || (P.rerouted && P.addr[subj] == P.addr[i])) {  // the general path (never taken
-      apply_record(P, i, subj, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);  // in practice)
+    if (general) {
+      apply_record(P, i, subj, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
     } else {
       // updateMembership(DEAD) -> onDeadMemberDetected (MPI:571-587) as in apply_record, with the
       // subject's presence count and last-removal period left to the caller: every cell of a
@@ -3211,31 +3215,42 @@ __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
   }
 }
 
-// exclusive scan of recv_count -> recv_off (single workgroup of 1024)
-__global__ void __launch_bounds__(1024) k_scan(KP P) {
+// exclusive scan of recv_count -> recv_off over the chip: per-tile sums (SCAN_TILE counts per
+// workgroup), their scan (k_excl_scan, one workgroup over the tiles), then each tile's own scan
+// from its base. (A single 1,024-thread workgroup walking all N counts took 1.8 ms per period at
+// N = 2^20.)
+constexpr uint32_t SCAN_TILE = 4096;
+__global__ void __launch_bounds__(1024) k_scan_tiles(KP P, uint32_t* tsum) {
   SWIM_GUARD(P);
-  __shared__ uint32_t s_part[1024];
-  const uint32_t N = P.N;
-  const uint32_t per = (N + 1023u) / 1024u;
-  const uint32_t b = threadIdx.x * per;
+  __shared__ uint32_t s_lds[16];
+  const uint32_t b = blockIdx.x * SCAN_TILE + 4u * threadIdx.x;
   uint32_t sum = 0;
-  for (uint32_t k = 0; k < per; ++k)
-    if (b + k < N) sum += P.recv_count[b + k];
-  s_part[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024u; o <<= 1) {
-    const uint32_t y = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0u;
-    __syncthreads();
-    s_part[threadIdx.x] += y;
-    __syncthreads();
+  if (b + 3u < P.N) {
+    const uint4 v = *reinterpret_cast<const uint4*>(P.recv_count + b);
+    sum = v.x + v.y + v.z + v.w;
+  } else {
+    for (uint32_t k = 0; k < 4u; ++k)
+      if (b + k < P.N) sum += P.recv_count[b + k];
   }
-  uint32_t run = s_part[threadIdx.x] - sum;
-  for (uint32_t k = 0; k < per; ++k)
-    if (b + k < N) {
+  uint32_t tot;
+  block_excl_scan1024(sum, &tot, s_lds);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_apply(KP P, const uint32_t* tbase, uint32_t ntiles) {
+  SWIM_GUARD(P);
+  __shared__ uint32_t s_lds[16];
+  const uint32_t b = blockIdx.x * SCAN_TILE + 4u * threadIdx.x;
+  uint32_t v[4];
+  for (uint32_t k = 0; k < 4u; ++k) v[k] = b + k < P.N ? P.recv_count[b + k] : 0u;
+  uint32_t tot;
+  uint32_t run = tbase[blockIdx.x] + block_excl_scan1024(v[0] + v[1] + v[2] + v[3], &tot, s_lds);
+  for (uint32_t k = 0; k < 4u; ++k)
+    if (b + k < P.N) {
       P.recv_off[b + k] = run;
-      run += P.recv_count[b + k];
+      run += v[k];
     }
-  if (threadIdx.x == 1023u) P.recv_off[N] = s_part[1023];
+  if (blockIdx.x == ntiles - 1u && threadIdx.x == 0) P.recv_off[P.N] = tbase[blockIdx.x] + tot;
 }
 
 __global__ void k_sync_scatter(KP P) {
