@@ -40,19 +40,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 WORKLOADS = {
     "c3": dict(desc="C3: 65,536 members, dense N x N views, LAN defaults, 10% simultaneous crash + 2-way "
                     "partition (16-member group) for 40 periods healed via SYNC",
-               n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16, gcap=1 << 20, scap=8192),
+               n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16, gcap=1 << 17, scap=8192),
     # SURVEY §8(d) C3 variant: the partition outlasts the 85-period suspicion timeout, so both
     # sides remove each other; the cut group rejoins through the seed addresses (ids 0..15) after
     # the heal (MembershipProtocolTest.testLongNetworkPartitionNoOutboundThenRemoved, :844-918)
     "c3long": dict(desc="C3 variant: 65,536 members, LAN defaults, seeds 0..15, 10% simultaneous crash + a "
                         "16-member group partitioned for 120 periods (past the suspicion timeout), rejoining "
                         "through the seeds",
-                   n=65536, preset="lan", loss=0.0, crash=0.10, part=120, part_group=16, gcap=1 << 20,
+                   n=65536, preset="lan", loss=0.0, crash=0.10, part=120, part_group=16, gcap=1 << 18,
                    scap=8192, seeds=16),
     "c3s": dict(desc="C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash",
                 n=65536, preset="lan", loss=0.0, crash=0.001, part=0, gcap=1 << 16),
     "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",
-                    n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 20, scap=8192),
+                    n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
@@ -224,13 +224,15 @@ def _oracle_run(args):
         c.set_loss(w["loss"])
     c.step(warmup)
     inject_faults(c, workload, warmup, seed, n=n)
+    r0 = c.stats()["gossip_first_receipts"]
     done, t0 = 0, time.perf_counter()
     while done < periods and (budget_s is None or time.perf_counter() - t0 < budget_s):
         c.step(1)
         done += 1
     dt = time.perf_counter() - t0
+    receipts = c.stats()["gossip_first_receipts"] - r0
     c.close()
-    return n, done, dt
+    return n, done, dt, receipts
 
 
 def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
@@ -242,7 +244,7 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
     aggregate; the single-thread rate is reported beside it."""
     import multiprocessing as mp
 
-    n, done, dt = _oracle_run((workload, warmup, seed, max_periods, budget_s))
+    n, done, dt, rcpt = _oracle_run((workload, warmup, seed, max_periods, budget_s))
     single = n * done / dt
     cores = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16
     t0 = time.perf_counter()
@@ -253,7 +255,9 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
     agg = sum(r[0] * r[1] for r in res) / max(r[2] for r in res)
     w = WORKLOADS[workload]
     return {"value": agg, "unit": "member-periods/s", "cores": cores, "kind": "port",
-            "single_thread": {"value": single, "cores": 1, "periods": done, "seconds": round(dt, 2)},
+            "single_thread": {"value": single, "cores": 1, "periods": done, "seconds": round(dt, 2),
+                              "gossip_first_receipts_per_s": rcpt / dt},
+            "gossip_first_receipts_per_s": sum(r[3] for r in res) / max(r[2] for r in res),
             "sample": f"oracle (C++ restatement of the reference's per-member logic) on the same schedule at {n} of "
                       f"{w['n']} members: {warmup} untimed periods, the faults, then the first {done} timed periods; "
                       f"single thread {dt:.1f} s, then {cores} replicas (seeds {seed}..{seed + cores - 1}) on "
@@ -397,6 +401,11 @@ def main():
                    "crashed": len(crashed), "loss_pct": w["loss"], "partition_periods": w["part"],
                    "gossip_ring_slots": w["gcap"], "tracked_subjects": w.get("tracked")},
         "periods_to_dead": periods_to_dead,
+        # work-normalised rates: the storm's work per member-period grows with N, so member-periods/s
+        # alone does not compare runs of different sizes
+        "rates": {"gossip_first_receipts_per_s": d["gossip_first_receipts"] / elapsed,
+                  "gossips_created_per_s": d["gossips_created"] / elapsed,
+                  "gossip_requests_per_s": d["gossip_sends"] / elapsed},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": rl["frac"], "traffic": pmc_traffic(dom, args.workload, world, args.steps, args.warmup),
                      "bytes_per_launch": rl["bytes_per_launch"], "avg_launch_ms": rl["avg_launch_ms"],
