@@ -167,7 +167,7 @@ def preset_config(preset):
     return {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
 
 
-def make_cluster(workload, device, seed, event_capacity=0, sharded=False):
+def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batching=True):
     """One cluster of the workload: on this GPU alone, or (sharded) this rank's observer rows of
     a cluster spread over the torch.distributed world."""
     from swimhip import ShardedSwimCluster, SwimCluster
@@ -178,7 +178,9 @@ def make_cluster(workload, device, seed, event_capacity=0, sharded=False):
     cfg = preset_config(w["preset"])
     if w.get("seeds"):  # the first `seeds` member ids are the seed addresses
         cfg = cfg.membership(lambda o: o.seedMembers(list(range(w["seeds"]))))
-    c = cls(cfg, w["n"], seed=seed, gossip_capacity=w["gcap"], device=device,
+    # one slot per gossip without batches: the ring of round 2's C3 runs
+    gcap = w["gcap"] if batching else max(w["gcap"], w.get("gcap_unbatched", 1 << 20))
+    c = cls(cfg, w["n"], seed=seed, gossip_capacity=gcap, device=device, gossip_batching=batching,
             event_capacity=event_capacity, sync_capacity=w.get("scap", 0), **kw)
     if w["loss"]:
         c.set_loss(w["loss"])
@@ -274,6 +276,7 @@ def main():
     ap.add_argument("--converge", type=int, default=120,
                     help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unbatched", action="store_true", help="one ring slot per gossip (A/B of DESIGN.md §3.12)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for --gpus > 1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
@@ -300,7 +303,7 @@ def main():
     n = w["n"]
     pc = preset_config(w["preset"])
     G = pc.failureDetectorConfig().pingInterval() // pc.gossipConfig().gossipInterval()  # rounds per period
-    c = make_cluster(args.workload, local, args.seed, sharded=world > 1)
+    c = make_cluster(args.workload, local, args.seed, sharded=world > 1, batching=not args.unbatched)
     log(f"created {args.workload}: N={n}")
     c.step(args.warmup)
     log(f"warmup {args.warmup} periods done")
@@ -399,7 +402,8 @@ def main():
         "config": {"workload": w["desc"], "members": n, "members_per_gpu": n // world,
                    "parallelism": f"observer-row shards x{world}" if world > 1 else "1 GPU",
                    "crashed": len(crashed), "loss_pct": w["loss"], "partition_periods": w["part"],
-                   "gossip_ring_slots": w["gcap"], "tracked_subjects": w.get("tracked")},
+                   "gossip_ring_slots": w["gcap"] if not args.unbatched else max(w["gcap"], w.get("gcap_unbatched", 1 << 20)),
+                   "gossip_batching": not args.unbatched, "tracked_subjects": w.get("tracked")},
         "periods_to_dead": periods_to_dead,
         # work-normalised rates: the storm's work per member-period grows with N, so member-periods/s
         # alone does not compare runs of different sizes
@@ -421,7 +425,7 @@ def main():
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
                                    "infected_suppressed", "infected_pruned_pairs", "infected_records",
-                                   "apply_words", "apply_runs", "apply_subjects", "apply_records")},
+                                   "apply_words", "apply_runs", "apply_subjects", "apply_records", "apply_spills")},
         "gossip_slots": {"live_at_end": s1["live_gossip_slots"], "gossips_live_at_end": s1["live_gossip_records"]},
     }
     c.close()

@@ -21,6 +21,7 @@ using namespace swim;
 namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
+constexpr uint32_t DICT_GRID = 128;  // workgroups of the record-dictionary kernels (grid-stride)
 
 uint32_t pow2ceil(uint64_t v) {
   uint64_t p = 1;
@@ -56,6 +57,7 @@ struct swim_handle {
   uint32_t cs_maxt = 1;
   // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
   uint32_t apply_blocks = 1, apply_blocks_b = 1;
+  bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
   unsigned long long* ck[2] = {nullptr, nullptr};
@@ -272,6 +274,13 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
     }
     // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights)
     if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P);
+    // the record dictionary of the batched apply: every commit while batching is
+    // enabled, so records committed before the first batch have their entries too
+    if (h->dict_on) {
+      hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, DICT_SIDS / 256)), dim3(256), 0, s, P);
+    }
   });
   return SWIM_OK;
 }
@@ -708,7 +717,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU
     h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
     // the batch-slot variant: one receiver per wave, AW_WAVES waves per workgroup, each with its
-    // own table; as many workgroups per CU as the 160 KiB of LDS (and 2,048 threads) allow
+    // own entry bitmap; as many workgroups per CU as the 160 KiB of LDS (and 2,048 threads) allow
     h->apply_lds_b = 4ull * AW_WAVES * AW_WORDS;
     const uint32_t per_cu_b = std::max<uint32_t>(
         1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
@@ -802,6 +811,15 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_cref, h->GC);
   ALLOC(P.c_sr, h->CC);
   ALLOC(P.c_hash, h->CC);
+  h->dict_on = c.gossip_batching == 0;
+  if (h->dict_on) {
+    ALLOC(P.c_id, h->CC);
+    ALLOC(P.sid_of, N);
+    ALLOC(P.d_subj, DICT_SIDS);
+    ALLOC(P.d_rec, DICT_IDS);
+    ALLOC(P.d_last, DICT_IDS);
+    ALLOC(P.d_free, DICT_SIDS);
+  }
   ALLOC(P.wsum, h->GC / 32);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
@@ -946,6 +964,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.meta_cur, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
+  if (h->dict_on) {
+    (void)hipMemsetAsync(P.sid_of, 0xFF, (size_t)N * 4, s);
+    (void)hipMemsetAsync(P.d_subj, 0xFF, (size_t)DICT_SIDS * 4, s);
+    (void)hipMemsetAsync(P.d_rec, 0, (size_t)DICT_IDS * 4, s);
+    (void)hipMemsetAsync(P.d_last, 0, (size_t)DICT_IDS * 4, s);
+  }
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_cref, 0, (size_t)h->GC * 8, s);

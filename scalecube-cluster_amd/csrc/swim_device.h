@@ -57,7 +57,7 @@ enum StatIdx : int {
   ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
   ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
   ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
-  ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply expanded into its LDS table
+  ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply_b expanded into its entry bitmap
   ST_UPDATED,      // MembershipEvent UPDATED (MembershipProtocolImpl.java:599-600)
   ST_COUNT
 };
@@ -118,6 +118,10 @@ struct Ctl {
   // the ring id count before the last commit, and the batches the last chip-wide commit made
   uint32_t ccount, g_prev, rs_ncls;
   uint32_t ntrack;       // N x K: subjects listed in track_list for the coming allocation
+  // record dictionary: the record count before the last commit, blocks ever
+  // handed out (high-water mark), free blocks on the stack, blocks the last claim took off it, and
+  // the unwrapped end of the newest record that got no dictionary entry
+  uint32_t c_prev, d_hw, d_nfree, d_taken, d_none_last;
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -217,6 +221,15 @@ struct KP {
   // version is the initial one and no ALIVE record can carry different metadata.
   uint32_t* meta_cur;   // [N]
   uint32_t* meta_view;  // [nloc][W] or nullptr
+  // Record dictionary: every distinct (subject, record) of the live record ring
+  // is an entry of its subject's block of DICT_WAYS entries; c_id names each ring record's entry,
+  // so a receiver ORs one bit per received record into an LDS bitmap and merges per block.
+  uint32_t* sid_of;   // [N] subject -> its block, NONE
+  uint32_t* d_subj;   // [DICT_SIDS] block -> subject, NONE while free
+  uint32_t* d_rec;    // [DICT_IDS] packed record of each entry, 0 = empty (no record packs to 0)
+  uint32_t* d_last;   // [DICT_IDS] unwrapped index + 1 of the newest ring record naming the entry
+  uint32_t* d_free;   // [DICT_SIDS] stack of free blocks
+  uint32_t* c_id;     // [CC] entry of each record-ring record; ID_USER, or ID_NONE (slow path)
   uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
                       // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
@@ -314,6 +327,27 @@ __device__ __forceinline__ uint32_t cell_get(const KP& P, uint32_t obs, uint32_t
 }
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// record dictionary geometry; tests build a variant with a tiny one
+#ifndef SWIM_DICT_SIDS
+#define SWIM_DICT_SIDS 8192
+#endif
+constexpr uint32_t DICT_SIDS = SWIM_DICT_SIDS;   // subject blocks
+constexpr uint32_t DICT_WAYS = 8;                // distinct live records per subject
+constexpr uint32_t DICT_IDS = DICT_SIDS * DICT_WAYS;
+constexpr uint32_t DICT_WORDS = DICT_IDS / 32u;  // a receiver's entry bitmap
+constexpr uint32_t ID_USER = 0xFFFFFFFEu;        // c_id of a user gossip (subject >= N)
+constexpr uint32_t ID_NONE = NONE;               // c_id of a record that found no entry
+constexpr uint32_t DICT_LOCK = 0xFFFFFFFEu;      // sid_of while k_dict_claim allocates the block
+static_assert(DICT_SIDS >= 4 && (DICT_SIDS & (DICT_SIDS - 1)) == 0 && DICT_SIDS <= (1u << 16),
+              "SWIM_DICT_SIDS: a power of two in 4 .. 65536");
+
+// the unwrapped index of the live record ring's first record: the oldest possibly-live slot's
+// first one (the ring's end when no slot is live)
+__device__ __forceinline__ uint32_t live_rec_lo(const KP& P) {
+  const uint32_t glo = P.ctl->glo, g0 = P.ctl->gcount;
+  return (g0 != glo && g0 - glo <= P.GC) ? P.g_cref[glo & P.gmask].x : P.ctl->ccount;
+}
 
 // the member whose transport receives a message sent to member x (TransportImpl sends to
 // member.address()): x itself while alive, or after a restart on x's address the new member

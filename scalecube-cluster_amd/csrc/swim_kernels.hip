@@ -421,6 +421,7 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
   if (t == 0) {
     P.ctl->g_prev = g0;
     P.ctl->gcount = g0 + nslots;
+    P.ctl->c_prev = c0;
     P.ctl->ccount = c0 + n;
     if (stg) P.ctl->stg_count = 0u;
   }
@@ -577,6 +578,7 @@ __global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
   const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
   P.ctl->g_prev = P.ctl->gcount;
   P.ctl->gcount += C.stat[C.maxt + nt - 1u] + C.stat[nt - 1u];
+  P.ctl->c_prev = P.ctl->ccount;
   P.ctl->ccount += n;
   if (stg) P.ctl->stg_count = 0u;
 }
@@ -605,6 +607,90 @@ __global__ void k_commit_wsum(KP P) {
       sum += cref[2u * s + 1u] - cref[2u * s];
     }
     P.wsum[w & ((P.GC >> 5) - 1u)] = sum;
+  }
+}
+
+// ---- record dictionary, after every commit: claim, entries, free ----
+// A block for each subject of the commit's records that has none: the CAS winner pops a free
+// block (or takes a new one); when none is left the subject keeps NONE and its records take the
+// apply kernel's slow path. No thread waits on another.
+__global__ void k_dict_claim(KP P) {
+  const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0, nfree = P.ctl->d_nfree;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t subj = P.c_sr[(c0 + i) & P.cmask].x;
+    if (subj >= P.N || P.sid_of[subj] != NONE) continue;
+    if (atomicCAS(&P.sid_of[subj], NONE, DICT_LOCK) != NONE) continue;
+    const uint32_t k = atomicAdd(&P.ctl->d_taken, 1u);
+    uint32_t sid = NONE;
+    if (k < nfree) {
+      sid = P.d_free[nfree - 1u - k];
+    } else {
+      const uint32_t hw = atomicAdd(&P.ctl->d_hw, 1u);
+      if (hw < DICT_SIDS) sid = hw;
+    }
+    if (sid != NONE) P.d_subj[sid] = subj;
+    P.sid_of[subj] = sid;
+  }
+}
+
+// Each record's entry in its subject's block: an entry holding the same record, else the first
+// empty one (claimed by CAS); a full block or no block: ID_NONE, remembered in d_none_last.
+__global__ void k_dict_entries(KP P) {
+  const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the blocks k_dict_claim popped leave the stack
+    const uint32_t t = P.ctl->d_taken, f = P.ctl->d_nfree;
+    P.ctl->d_nfree = f - min(t, f);
+    P.ctl->d_taken = 0u;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t x = c0 + i;
+    const uint2 sr = P.c_sr[x & P.cmask];
+    uint32_t id = ID_NONE;
+    if (sr.x >= P.N) {
+      id = ID_USER;
+    } else {
+      const uint32_t sid = P.sid_of[sr.x];
+      if (sid < DICT_SIDS) {
+        for (uint32_t k = 0; k < DICT_WAYS; ++k) {
+          uint32_t* e = &P.d_rec[sid * DICT_WAYS + k];
+          uint32_t v = *e;
+          if (v == 0u) v = atomicCAS(e, 0u, sr.y);
+          if (v == 0u || v == sr.y) {
+            id = sid * DICT_WAYS + k;
+            break;
+          }
+        }
+      }
+    }
+    P.c_id[x & P.cmask] = id;
+    if (id < DICT_IDS)
+      atomicMax(&P.d_last[id], x + 1u);
+    else if (id == ID_NONE)
+      atomicMax(&P.ctl->d_none_last, x + 1u);
+  }
+}
+
+// Entries no live record names are emptied; a block left empty goes back on the stack (its
+// subject gets a block again with its next record).
+__global__ void k_dict_free(KP P) {
+  const uint32_t hw = min(P.ctl->d_hw, DICT_SIDS), c_lo = live_rec_lo(P);
+  for (uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x; sid < hw; sid += gridDim.x * blockDim.x) {
+    const uint32_t subj = P.d_subj[sid];
+    if (subj == NONE) continue;
+    bool live = false;
+    for (uint32_t k = 0; k < DICT_WAYS; ++k) {
+      const uint32_t id = sid * DICT_WAYS + k;
+      if (P.d_rec[id] == 0u) continue;
+      if ((int32_t)(P.d_last[id] - c_lo) > 0)
+        live = true;
+      else
+        P.d_rec[id] = 0u;
+    }
+    if (!live) {
+      P.d_subj[sid] = NONE;
+      P.sid_of[subj] = NONE;
+      P.d_free[atomicAdd(&P.ctl->d_nfree, 1u)] = sid;
+    }
   }
 }
 
@@ -2418,49 +2504,45 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
   }
 }
 
-// k_gossip_apply when the ring holds batch slots (P.batched): a received slot stands for all
-// the gossips of its batch, so its record range is expanded into an LDS table. One WAVE per
-// receiver (its own table of up to 2^SWIM_APPLY_WLOG slots; several receivers in flight per CU,
-// no workgroup barriers): in a storm a receiver gets ~10^4 records of ~10^3 distinct subjects per
-// round, and a whole workgroup per receiver spent its time in barrier-separated phases (measured:
-// 570 ms per 100 C3 rounds with per-wave expansion inside a 1,024-thread receiver, 670 ms with a
-// workgroup-wide record list). Two passes per receiver: (1) holdings, infection
-// rounds and age bounds of every receipt word, and the record count of the received run tops
-// (sizes the table); (2) the records, flattened across the 64 lanes (wave_owner) four per lane at
-// a time, lattice-max per subject. Subjects that find no slot go to the global inbox row; when
-// more spill than the wave's list holds, the row is scanned at the end. Then updateMembership per
-// subject whose merged record overrides the cell (MembershipRecord.isOverrides, the only ones
-// updateMembership does anything for, MPI:489-496), cells loaded eight at a time.
-#ifndef SWIM_APPLY_WLOG
-#define SWIM_APPLY_WLOG 11
-#endif
-constexpr uint32_t AW_LOG = SWIM_APPLY_WLOG;
-constexpr uint32_t AW_SLOTS = 1u << AW_LOG;  // per-wave table slots (keys + values)
+// k_gossip_apply when the ring holds batch slots (P.batched): a received slot stands for all the
+// gossips of its batch. One WAVE per receiver, AW_WAVES receivers per workgroup, no workgroup
+// barriers. The records of every received run top are ORed into the wave's LDS bitmap over the
+// record dictionary (one bit per entry); then per block (subject) with set bits
+// the lattice max of its set entries is merged: updateMembership when it overrides the cell
+// (MembershipRecord.isOverrides, the only records updateMembership acts on, MPI:489-496). A storm
+// receiver gets ~10^4..10^5 records of ~10^3..10^4 subjects per round, mostly the same few records
+// per subject again: an LDS hash of (subject, max) per receiver spent its time probing and
+// spilling there (4.4 s per 100 C3 rounds); a bit per record costs one LDS OR.
+// Records without an entry (dictionary out of blocks or ways) take the global inbox (lattice max
+// per cell; spilled subjects listed in LDS, the whole inbox row scanned when the list overflows).
+// While any such record is live, the bitmap's maxima go through the inbox as well, so a subject
+// is merged exactly once per round.
 #ifndef SWIM_APPLY_WSPILL
 #define SWIM_APPLY_WSPILL 128
 #endif
 constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
-constexpr uint32_t AW_WAVES = 4;             // waves per workgroup
-constexpr uint32_t AW_WORDS = 2u * AW_SLOTS + AW_SPILL + 4u;  // LDS words per wave
-static_assert(AW_LOG >= 6 && AW_LOG <= 13, "SWIM_APPLY_WLOG out of range");
+constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per workgroup
+constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
 __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  uint32_t* s_key = s_dyn + wv * AW_WORDS;
-  uint32_t* s_val = s_key + AW_SLOTS;
-  uint32_t* s_spl = s_val + AW_SLOTS;
+  uint32_t* s_bm = s_dyn + wv * AW_WORDS;  // entry bitmap: all-zero between receivers
+  uint32_t* s_spl = s_bm + DICT_WORDS;
   uint32_t* s_misc = s_spl + AW_SPILL;  // [0] spilled subjects
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
+  const uint32_t bw = (min(P.ctl->d_hw, DICT_SIDS) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
+  const bool via_inbox = (int32_t)(P.ctl->d_none_last - live_rec_lo(P)) > 0;  // a live record has no entry
   Tally T;
   uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrecs = 0, nrcpt = 0;
   auto wsync = [] {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   };
+  for (uint32_t t = lane; t < bw; t += 64u) s_bm[t] = 0u;
   for (uint32_t li = blockIdx.x * AW_WAVES + wv; li < n_list; li += gridDim.x * AW_WAVES) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
@@ -2468,190 +2550,128 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
     const bool summ = nsw <= NSUM;
     const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
+    uint32_t* inrow = P.inbox + lrow(P, p) * P.W;
     if (lane == 0) s_misc[0] = 0u;
-    // the list positions with receipts, compacted from the summary into the table area (free
-    // until the table is sized), as long as they fit it
-    uint32_t n_comp = 0;
-    bool compact = summ;
-    if (summ) {
-      for (uint32_t c0 = 0; c0 < nsw && compact; c0 += 64u) {
-        const uint32_t t = c0 + lane;
-        uint32_t bits = t < nsw ? sumr[t] : 0u;
-        uint32_t tot;
-        uint32_t o = n_comp + wave_excl_scan((uint32_t)__popc(bits), &tot);
-        if (n_comp + tot > 2u * AW_SLOTS) {
-          compact = false;  // uniform
-          break;
-        }
-        while (bits) {
-          s_key[o++] = 32u * t + (uint32_t)__builtin_ctz(bits);
-          bits &= bits - 1u;
-        }
-        n_comp += tot;
-      }
-      wsync();
-    }
-    const uint32_t n_it = !summ ? n_act : (compact ? n_comp : nsw * 32u);
-    auto item = [&](uint32_t u, const uint32_t* list) -> uint32_t {
-      if (u >= n_it) return NONE;
-      if (!summ) return u;
-      if (compact) return list[u];
-      return ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
-    };
-    // pass 1: receive the words; count the records their run tops carry
-    uint32_t ent = 0, rc = 0;
-    for (uint32_t it0 = 0; it0 < n_it; it0 += 256u) {
-      uint32_t kv[4], ev[4], bv[4], wsv[4], pv[4], rv[4];
-      uint4 v0[4], v1[4];
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) kv[j] = item(it0 + 64u * j + lane, s_key);
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) ev[j] = kv[j] != NONE ? P.act[kv[j]] : 0u;
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j)
-        bv[j] = (kv[j] != NONE && ((ev[j] >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        wsv[j] = (w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u);
-        pv[j] = rv[j] = 0u;
-        if (bv[j]) {
-          pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
-          rv[j] = P.runw[wsv[j]];
-          const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
-          if ((bv[j] & 0xFFFFu) && (pv[j] & 0xFFFFu)) v0[j] = dp[0];
-          if ((bv[j] >> 16) && (pv[j] >> 16)) v1[j] = dp[1];
-        }
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        uint32_t rm = 0u;
-        if (bv[j]) {
-          receive_word(P, p, wsv[j], bv[j], pv[j], v0[j], v1[j]);
-          ++nwords;
-          rm = run_tops(bv[j], rv[j]);
-          rc += (uint32_t)(__popc(bv[j]) - __popc(rm));  // slots inside runs: one gossip each
-          nruns += (uint32_t)__popc(rm);
-        }
-        uint32_t tot;
-        const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
-        for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
-          const uint32_t q = q0 + lane;
-          const uint32_t o = wave_owner(off, q);
-          const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(wsv[j], (int)o, 64), oo = __shfl(off, (int)o, 64);
-          if (q < tot) {
-            const uint2 cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
-            ent += cr.y - cr.x;
-          }
-        }
-      }
-    }
-    const uint32_t E = wave_sum(ent), R = wave_sum(rc + ent);
-    if (lane == 0) {
-      nrcpt += R;
-      nrecs += E;
-    }
-    uint32_t lg = 6;  // >= 2 slots per record, 64 .. AW_SLOTS
-    while (lg < AW_LOG && (1u << lg) < 2u * E) ++lg;
-    const uint32_t hm = (1u << lg) - 1u;
-    // the compacted items move behind the table's keys when they fit there (otherwise pass 2
-    // tests the summary bits again); through registers, so overlapping ranges are safe
-    const bool keep = compact && n_comp <= AW_SLOTS - (1u << lg) && n_comp <= 256u;
-    uint32_t* items2 = s_key + AW_SLOTS - n_comp;
-    {
-      uint32_t tmp[4];
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) tmp[j] = (keep && 64u * j + lane < n_comp) ? s_key[64u * j + lane] : 0u;
-      wsync();
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j)
-        if (keep && 64u * j + lane < n_comp) items2[64u * j + lane] = tmp[j];
-      wsync();
-    }
-    for (uint32_t t = lane; t <= hm; t += 64u) {
-      s_key[t] = NONE;
-      s_val[t] = 0u;
-    }
     wsync();
-    const bool compact2 = keep;
-    const uint32_t n_it2 = !summ ? n_act : (compact2 ? n_comp : nsw * 32u);
-    auto item2 = [&](uint32_t u) -> uint32_t {
-      if (u >= n_it2) return NONE;
-      if (!summ) return u;
-      if (compact2) return items2[u];
-      return ((sumr[u >> 5] >> (u & 31u)) & 1u) ? u : NONE;
-    };
-    // lattice max per subject; a plain read first settles most repeats without atomics
     bool rowscan = false;  // the spill list overflowed: scan the whole inbox row at the end
-    auto insert = [&](uint2 sr) {
-      if (sr.x >= P.N) {  // a user gossip: GossipProtocol.listen() (GossipProtocolImpl.java:176)
-        push_event(P, p, sr.x - P.N, SWIM_EV_GOSSIP, SWIM_R_MEMBERSHIP_GOSSIP, sr.y);
+    uint32_t ent = 0, rc = 0;
+    // lattice max into the receiver's inbox cell; the subject's first writer lists it
+    auto spill = [&](uint32_t subj, uint32_t rec) {
+      const uint32_t c = col_of(P, subj);
+      if (c == NONE) {  // N x K: no column for a subject with a live gossip
+        atomicOr(&P.ctl->overflow, OV_TRACK);
         return;
       }
-      uint32_t h = (sr.x * 0x9E3779B1u) >> (32u - lg);
-      for (uint32_t q = 0; q < HPROBE; ++q) {
-        uint32_t k = s_key[h];
-        if (k == NONE) {
-          k = atomicCAS(&s_key[h], NONE, sr.x);
-          if (k == NONE) {
-            atomicMax(&s_val[h], sr.y);
-            return;
-          }
-        }
-        if (k == sr.x) {
-          if (s_val[h] < sr.y) atomicMax(&s_val[h], sr.y);
-          return;
-        }
-        h = (h + 1u) & hm;
-      }
-      // slots only ever fill up, so this subject spills for the whole round
-      if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr.x)], sr.y) == 0u) {
+      if (atomicMax(&inrow[c], rec) == 0u) {
         const uint32_t o = atomicAdd(&s_misc[0], 1u);
         if (o < AW_SPILL)
-          s_spl[o] = sr.x;
+          s_spl[o] = subj;
         else
           rowscan = true;
       }
     };
-    // pass 2: the records of every received run top into the table; receipts cleared
-    for (uint32_t it0 = 0; it0 < n_it2; it0 += 256u) {
-      uint32_t kv[4], bv[4], wsv[4], rv[4];
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) kv[j] = item2(it0 + 64u * j + lane);
-#pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t e = kv[j] != NONE ? P.act[kv[j]] : 0u;
-        bv[j] = (kv[j] != NONE && ((e >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
-        wsv[j] = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
-        rv[j] = bv[j] ? P.runw[wsv[j]] : 0u;
-        if (bv[j]) nbr[kv[j]] = 0u;  // nb is all-zero between rounds
+    // record-ring record x of a received run top
+    auto record = [&](uint32_t x, uint32_t id) {
+      if (id < DICT_IDS) {
+        atomicOr(&s_bm[id >> 5], 1u << (id & 31u));
+        return;
       }
+      const uint2 sr = P.c_sr[x & P.cmask];
+      if (sr.x >= P.N)  // a user gossip: GossipProtocol.listen() (GossipProtocolImpl.java:176)
+        push_event(P, p, sr.x - P.N, SWIM_EV_GOSSIP, SWIM_R_MEMBERSHIP_GOSSIP, sr.y);
+      else
+        spill(sr.x, sr.y);
+    };
+    // one receipt word per lane (kv = its active-list position, or NONE): holdings, infection
+    // rounds and age bounds, then the records of its run tops, flattened across the wave
+    auto word = [&](uint32_t kv) {
+      const uint32_t e = kv != NONE ? P.act[kv] : 0u;
+      const uint32_t bits = (kv != NONE && ((e >> 26) & 3u) != WC_NONE) ? nbr[kv] : 0u;
+      const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+      uint32_t rm = 0u;
+      if (bits) {
+        const uint32_t prior = P.hb[lrow(P, p) * W32 + ws];
+        const uint32_t rs = P.runw[ws];
+        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+        const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)ws * 32u);
+        if ((bits & 0xFFFFu) && (prior & 0xFFFFu)) v0 = dp[0];
+        if ((bits >> 16) && (prior >> 16)) v1 = dp[1];
+        receive_word(P, p, ws, bits, prior, v0, v1);
+        nbr[kv] = 0u;  // nb is all-zero between rounds
+        ++nwords;
+        rm = run_tops(bits, rs);
+        rc += (uint32_t)(__popc(bits) - __popc(rm));  // slots inside runs: one gossip each
+        nruns += (uint32_t)__popc(rm);
+      }
+      uint32_t tot;
+      const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
+      for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
+        const uint32_t q = q0 + lane;
+        const uint32_t o = wave_owner(off, q);
+        const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(ws, (int)o, 64), oo = __shfl(off, (int)o, 64);
+        uint2 cr = make_uint2(0u, 0u);
+        if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
+        const uint32_t len = cr.y - cr.x;
+        ent += len;
+        // long ranges (batches): the whole wave walks each, four coalesced records per lane in flight
+        unsigned long long big = __ballot(len >= 64u);
+        while (big) {
+          const int L = __builtin_ctzll(big);
+          big &= big - 1ull;
+          const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
+          for (uint32_t x0 = b0; x0 != b1; x0 += min(256u, b1 - x0)) {
+            uint32_t id[4];
 #pragma unroll
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t rm = bv[j] ? run_tops(bv[j], rv[j]) : 0u;
+            for (uint32_t u = 0; u < 4u; ++u) {
+              const uint32_t x = x0 + 64u * u + lane;
+              id[u] = (x - b0) < (b1 - b0) ? P.c_id[x & P.cmask] : DICT_IDS;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; ++u) {
+              const uint32_t x = x0 + 64u * u + lane;
+              if ((x - b0) < (b1 - b0)) record(x, id[u]);
+            }
+          }
+        }
+        // short ranges (single gossips, small batches): flattened across the lanes
+        uint32_t etot;
+        const uint32_t eoff = wave_excl_scan(len < 64u ? len : 0u, &etot);
+        for (uint32_t e0 = 0; e0 < etot; e0 += 256u) {
+          uint32_t xs[4], id[4];
+#pragma unroll
+          for (uint32_t u = 0; u < 4u; ++u) {
+            const uint32_t ee = e0 + 64u * u + lane;
+            const uint32_t eo = wave_owner(eoff, ee);
+            const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
+            xs[u] = bx + ee - bo;
+            id[u] = ee < etot ? P.c_id[xs[u] & P.cmask] : DICT_IDS;
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < 4u; ++u)
+            if (e0 + 64u * u + lane < etot) record(xs[u], id[u]);
+        }
+      }
+    };
+    if (!summ) {
+      for (uint32_t it0 = 0; it0 < n_act; it0 += 64u) word(it0 + lane < n_act ? it0 + lane : NONE);
+    } else {  // the summary's set bits, flattened across the wave
+      for (uint32_t c0 = 0; c0 < nsw; c0 += 64u) {
+        const uint32_t sb = c0 + lane < nsw ? sumr[c0 + lane] : 0u;
         uint32_t tot;
-        const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
+        const uint32_t off = wave_excl_scan((uint32_t)__popc(sb), &tot);
         for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
           const uint32_t q = q0 + lane;
           const uint32_t o = wave_owner(off, q);
-          const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(wsv[j], (int)o, 64), oo = __shfl(off, (int)o, 64);
-          uint2 cr = make_uint2(0u, 0u);
-          if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
-          uint32_t etot;
-          const uint32_t eoff = wave_excl_scan(cr.y - cr.x, &etot);
-          for (uint32_t e0 = 0; e0 < etot; e0 += 256u) {  // four records per lane in flight
-            uint2 sr[4];
-#pragma unroll
-            for (uint32_t u = 0; u < 4u; ++u) {
-              const uint32_t e = e0 + 64u * u + lane;
-              const uint32_t eo = wave_owner(eoff, e);
-              const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
-              if (e < etot) sr[u] = P.c_sr[(bx + e - bo) & P.cmask];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 4u; ++u)
-              if (e0 + 64u * u + lane < etot) insert(sr[u]);
-          }
+          const uint32_t bo = __shfl(sb, (int)o, 64), oo = __shfl(off, (int)o, 64);
+          word(q < tot ? 32u * (c0 + o) + kth_set_bit(bo, q - oo) : NONE);
         }
+      }
+    }
+    {
+      const uint32_t E = wave_sum(ent), R = wave_sum(rc) + E;
+      if (lane == 0) {
+        nrcpt += R;
+        nrecs += E;
       }
     }
     wsync();
@@ -2664,44 +2684,58 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
         ++created;
       }
     };
-    // updateMembership for the subjects whose merged record overrides the cell; cells of eight
-    // table slots per lane loaded together
-    for (uint32_t t0 = 0; t0 <= hm; t0 += 512u) {
-      uint32_t ks[8], vs[8], cs[8];
+    // per block with set entries: the max of its set entries' records, merged once (bitmap words
+    // cleared on the way; four words per lane loaded together)
+    for (uint32_t t0 = 0; t0 < bw; t0 += 256u) {
+      uint32_t wd[4];
 #pragma unroll
-      for (uint32_t u = 0; u < 8u; ++u) {
+      for (uint32_t u = 0; u < 4u; ++u) {
         const uint32_t t = t0 + 64u * u + lane;
-        ks[u] = t <= hm ? s_key[t] : NONE;
-        vs[u] = ks[u] != NONE ? s_val[t] : 0u;
+        wd[u] = t < bw ? s_bm[t] : 0u;
+        if (wd[u]) s_bm[t] = 0u;
       }
 #pragma unroll
-      for (uint32_t u = 0; u < 8u; ++u) cs[u] = ks[u] != NONE ? cell_get(P, p, ks[u]) : 0u;
-#pragma unroll
-      for (uint32_t u = 0; u < 8u; ++u)
-        if (ks[u] != NONE) {
-          if (is_overrides(vs[u], cs[u]) || (P.nxk && P.colmap[ks[u]] == NONE))  // (the latter: OV_TRACK)
-            apply(ks[u], vs[u]);
-          else
-            ++nsubj;
+      for (uint32_t u = 0; u < 4u; ++u) {
+        while (wd[u]) {
+          const uint32_t sh = (uint32_t)__builtin_ctz(wd[u]) & ~(DICT_WAYS - 1u);  // the block's first bit
+          uint32_t m = (wd[u] >> sh) & ((1u << DICT_WAYS) - 1u);
+          wd[u] &= ~(((1u << DICT_WAYS) - 1u) << sh);
+          const uint32_t base = 32u * (t0 + 64u * u + lane) + sh;  // entry id of the block's way 0
+          uint32_t best = 0u;
+          while (m) {
+            best = max(best, P.d_rec[base + (uint32_t)__builtin_ctz(m)]);
+            m &= m - 1u;
+          }
+          const uint32_t subj = P.d_subj[base / DICT_WAYS];
+          if (via_inbox) {
+            spill(subj, best);
+          } else {
+            const uint32_t c = cell_get(P, p, subj);
+            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
+              apply(subj, best);
+            else
+              ++nsubj;
+          }
         }
+      }
     }
+    wsync();
     const uint32_t nsp = min(s_misc[0], AW_SPILL);
     if (__any(rowscan)) {  // every spilled subject: the inbox row's nonzero cells
       __threadfence();
-      uint32_t* row = P.inbox + lrow(P, p) * P.W;
       const uint32_t nc = ncells(P);
       for (uint32_t c = lane; c < nc; c += 64u)
-        if (row[c]) apply(subj_of(P, c), atomicExch(&row[c], 0u));
+        if (inrow[c]) apply(subj_of(P, c), atomicExch(&inrow[c], 0u));
     } else {
       if (nsp) __threadfence();
       for (uint32_t t = lane; t < nsp; t += 64u) {
         const uint32_t subj = s_spl[t];
-        apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
+        apply(subj, atomicExch(&inrow[col_of(P, subj)], 0u));
       }
     }
     if (lane == 0) atomicAdd(&P.held[p], total);
     nspills += lane == 0 ? s_misc[0] : 0u;
-    wsync();  // the table is reused by the wave's next receiver
+    wsync();  // the spill counter is reset for the wave's next receiver
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   add_stat(P, ST_APPLY_WORDS, nwords);

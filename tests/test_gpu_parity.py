@@ -272,7 +272,9 @@ def test_apply_spill_path_parity():
     16,384-slot hash. A variant built with a 64-slot hash (__graft_entry__.build, -DSWIM_APPLY_HLOG=6)
     takes them in almost every round: it must still match the oracle bit for bit, and the spill
     counter proves the path ran. The same variant gives the batch-slot kernel (k_gossip_apply_b,
-    lossless C3 part) 64-slot wave tables and a 4-entry spill list, so its inbox-row scan runs too."""
+    lossless C3 part) a 4-subject record dictionary (-DSWIM_DICT_SIDS=4) and a 4-entry spill list:
+    most records find no entry, so the bitmap maxima go through the inbox with them (the
+    exactly-once merge of DESIGN.md §3.15) and the inbox-row scan runs too."""
     import os
     import subprocess
     import sys
