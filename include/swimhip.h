@@ -187,6 +187,14 @@ int swim_destroy(swim_handle* h);
  * is still live returns SWIM_EINVAL (set the loss before the gossips are created, or create the
  * handle with gossip_batching = 1). */
 int swim_set_loss(swim_handle* h, uint32_t loss_bp);
+/* Mean message delay in ms on every link (NetworkEmulator.setDefaultOutboundSettings(loss, meanDelay)
+ * :81-84, tryDelayOutbound :189-201, evaluateDelay :358-368; 0 = none; <= 60,000). Each message draws
+ * an exponential delay: a GossipRequest is handled delay / gossipInterval rounds after it was sent,
+ * and a ping, ping-req relay or metadata round trip counts only if it returns within its timeout
+ * (DESIGN.md §3.15). Draws per message, so, like a probabilistic loss, it needs one gossip per ring
+ * slot (SWIM_EINVAL while batch slots are live). Switching back to 0 is refused while delayed messages
+ * are in flight. Unsharded handles, up to 65,536 members. */
+int swim_set_delay(swim_handle* h, uint32_t mean_ms);
 /* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
  * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */
 int swim_set_partition(swim_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1);

@@ -21,6 +21,7 @@
 #include "swim_oracle.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -165,6 +166,7 @@ struct Gossip {  // Gossip.java:7-49 + GossipRequest payload (MembershipRecord)
   uint32_t origin, seq, subject, record, hash;
   int64_t create;
   int32_t holders;  // members whose gossips map currently holds it
+  int32_t inflight; // delayed GossipRequests of it still travelling (keep its id live)
 };
 
 // GossipProtocolImpl.gossips (GPI:49): gossipId -> GossipState (infectionPeriod,
@@ -242,6 +244,19 @@ struct oracle_handle {
   uint64_t seed;
   uint64_t period = 0;
   uint32_t loss_bp = 0;
+  // NetworkEmulator.OutboundSettings.meanDelay (NE:309-368) of every link, in ms (0 = none), and
+  // its exponential draw as a threshold table: dthr[k] = the smallest 32-bit uniform whose delay
+  // -ln(1 - u/2^32) * mean (NE:358-368) is >= k ms, for every k a 32-bit draw can reach
+  uint32_t delay_mean = 0;
+  std::vector<uint32_t> dthr;
+  uint32_t dmax_rounds = 0;  // the longest gossip delay a draw can give, in rounds
+  // GossipRequests delayed past their round: delivered at the start of round
+  // `arrive`'s onGossipReq step to process `to`, if it still runs
+  struct Flight {
+    int64_t arrive;
+    uint32_t to, from, gid;
+  };
+  std::vector<Flight> flights;
   std::vector<uint8_t> group;
   uint64_t part_t0 = 0, part_t1 = 0;
   std::vector<uint8_t> link;    // outbound block src->dst (send error), lazily allocated
@@ -321,6 +336,21 @@ bool link_ok(const oracle_handle* h, uint32_t src, uint32_t dst) {
 // Is message src->dst delivered to dst's protocol handlers?
 bool delivered(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
   return out_ok(h, kind, src, dst, c, tick) && in_ok(h, dst, src);
+}
+
+// NetworkEmulator.tryDelayOutbound / evaluateDelay (NE:189-201,358-368) of message src->dst: its
+// delay in whole ms, from the second word of the message's draw (the first is its loss draw, so one
+// Philox block decides both): (long)(-ln(1 - x) * meanDelay) with x = u / 2^32, read from the
+// threshold table (exact integer compares, no floating point per message).
+uint32_t delay_of_draw(const oracle_handle* h, uint32_t u) {
+  if (h->delay_mean == 0) return 0;
+  return (uint32_t)(std::upper_bound(h->dthr.begin(), h->dthr.end(), u) - h->dthr.begin()) - 1u;
+}
+uint32_t msg_delay(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
+  if (h->delay_mean == 0) return 0;
+  const uint32_t rs = route(h, src), rd = route(h, dst);
+  if (rs == NONE || rd == NONE) return 0;  // not sent at all (out_ok fails)
+  return delay_of_draw(h, draw4(h->seed, kind, rs, rd, c, tick).v[1]);
 }
 
 void perm_keys(const oracle_handle* h, uint32_t kind, uint32_t member, uint32_t epoch, uint32_t* k) {
@@ -446,7 +476,7 @@ void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t
   Member& o = h->m[origin];
   uint32_t seq = o.gossip_seq++;
   const uint32_t gid = (uint32_t)h->registry.size();
-  h->registry.push_back(Gossip{origin, seq, subject, record, ghash(origin, seq), create_round, 0});
+  h->registry.push_back(Gossip{origin, seq, subject, record, ghash(origin, seq), create_round, 0, 0});
   gossip_reserve(h, gid + 1);
   gossip_put(h, o, gid, create_round);
   h->st.gossips_created++;
@@ -456,9 +486,12 @@ void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t
 // liveness round trip: GET_METADATA_REQ obs->subj and GET_METADATA_RESP subj->obs delivered
 // and the subject serving: the process at its address must be the subject itself (onMetadataRequest
 // answers only requests for its own id, :216-223; otherwise the fetch times out).
+// With message delays the round trip must come back within metadataTimeout (:170).
 bool fetch_ok(const oracle_handle* h, uint32_t obs, uint32_t subj, uint32_t attempt, uint32_t tick) {
   return route(h, subj) == subj && delivered(h, K_MREQ, obs, subj, attempt, tick) &&
-         delivered(h, K_MRESP, subj, obs, attempt, tick);
+         delivered(h, K_MRESP, subj, obs, attempt, tick) &&
+         msg_delay(h, K_MREQ, obs, subj, attempt, tick) + msg_delay(h, K_MRESP, subj, obs, attempt, tick) <
+             (uint32_t)h->cfg.metadata_timeout_ms;
 }
 
 // MembershipProtocolImpl.updateMembership (MPI:481-547) with its callees onSelfMemberDetected
@@ -591,7 +624,11 @@ void do_ping(oracle_handle* h, uint32_t i) {
   // onPing (FDI:226-252) at the process on j's address answers DEST_GONE unless it is j itself;
   // computeMemberStatus (FDI:370-391) turns that ack into DEAD
   const uint32_t acked = route(h, j) == j ? SWIM_ALIVE : SWIM_DEAD;
-  if (delivered(h, K_PING, i, j, 0, tick) && delivered(h, K_ACK, j, i, 0, tick)) {  // FDI:143-150
+  // round trip of the direct ping (its delays, NE:189-201); the ack counts if it is back within
+  // pingTimeout (FDI:145 .timeout), otherwise it arrives late (handled with the ping-req below)
+  const uint32_t t_direct = msg_delay(h, K_PING, i, j, 0, tick) + msg_delay(h, K_ACK, j, i, 0, tick);
+  const bool ping_in = delivered(h, K_PING, i, j, 0, tick);
+  if (ping_in && delivered(h, K_ACK, j, i, 0, tick) && (!h->delay_mean || t_direct < (uint32_t)h->cfg.ping_timeout_ms)) {  // FDI:143-150
     h->st.fd_direct_ok++;
     evs.push_back(acked);
   } else {
@@ -602,7 +639,12 @@ void do_ping(oracle_handle* h, uint32_t i) {
     } else {
       h->st.fd_ping_req++;
       uint32_t unsent = 0, sent = 0;
-      uint32_t first = 0xFFFFFFFFu;  // proxy whose forwarded ack reaches i's transport first
+      // the ack that reaches i's transport first, and when (ms from the direct ping's send). The
+      // PING_REQs go out when the direct ping times out (FDI:152-168) and wait time_left (FDI:183).
+      // The direct ping's own ack, when late, shares their correlation id (FDI:174-178) and is
+      // taken the same way if it comes back before they time out.
+      uint32_t first = 0xFFFFFFFFu, t_first = 0xFFFFFFFFu;
+      const uint32_t pto = (uint32_t)h->cfg.ping_timeout_ms, pint = (uint32_t)h->cfg.ping_interval_ms;
       for (uint32_t p : proxies) {
         if (!out_ok(h, K_PING_REQ, i, p, j, tick)) {  // tryFailOutbound: immediate error -> SUSPECT
           ++unsent;
@@ -612,15 +654,27 @@ void do_ping(oracle_handle* h, uint32_t i) {
         // onPingReq (FDI:255-277) -> transit PING -> onPing at j -> ACK to the proxy ->
         // onTransitPingAck (FDI:283-305) forwards it to i. Each hop is a send that the next
         // receiver's inbound filter may drop; the last hop reaches i's TransportImpl.
-        if (first == 0xFFFFFFFFu && in_ok(h, p, i) && delivered(h, K_PROXY_PING, p, j, i, tick) &&
-            delivered(h, K_PROXY_ACK, j, p, i, tick) && out_ok(h, K_FWD_ACK, p, i, j, tick))
-          first = p;
+        if (in_ok(h, p, i) && delivered(h, K_PROXY_PING, p, j, i, tick) && delivered(h, K_PROXY_ACK, j, p, i, tick) &&
+            out_ok(h, K_FWD_ACK, p, i, j, tick)) {
+          const uint32_t hops = msg_delay(h, K_PING_REQ, i, p, j, tick) + msg_delay(h, K_PROXY_PING, p, j, i, tick) +
+                                msg_delay(h, K_PROXY_ACK, j, p, i, tick) + msg_delay(h, K_FWD_ACK, p, i, j, tick);
+          if (hops < (uint32_t)time_left && pto + hops < t_first) {  // earliest; ties: selection order
+            first = p;
+            t_first = pto + hops;
+          }
+        }
+      }
+      // the late direct ack (sender j) wins ties: it is compared first
+      if (h->delay_mean && sent && ping_in && out_ok(h, K_ACK, j, i, 0, tick) && t_direct >= pto && t_direct < pint &&
+          t_direct <= t_first) {
+        first = j;
+        t_first = t_direct;
       }
       // TransportImpl.requestResponse matches responses by correlation id only (:236-238) and
-      // every PING_REQ of this probe carries the same cid (FDI:174-178), so the first forwarded
-      // ack (canonically: the first proxy in selection order whose relay got through) is taken
-      // by every pending subscription; NET:64-68 then checks i's inbound filter against that
-      // ack's sender (the proxy): blocked -> Mono.never() -> every subscription times out.
+      // every PING_REQ of this probe carries the same cid (FDI:174-178), so the first ack to
+      // arrive (without delays: the first proxy in selection order whose relay got through) is
+      // taken by every pending subscription; NET:64-68 then checks i's inbound filter against
+      // that ack's sender: blocked -> Mono.never() -> every subscription times out.
       const bool ok = first != 0xFFFFFFFFu && in_ok(h, i, first);
       for (uint32_t u = 0; u < unsent; ++u) evs.push_back(SWIM_SUSPECT);
       for (uint32_t s = 0; s < sent; ++s) evs.push_back(ok ? acked : SWIM_SUSPECT);  // FDI:190-207
@@ -680,7 +734,8 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   const uint32_t phase = 1 + q;
   const uint32_t tick = tick_of(h, phase);
   const int32_t rm = h->cfg.gossip_repeat_mult;
-  while (h->gbase < h->registry.size() && h->registry[h->gbase].holders == 0) h->gbase++;
+  while (h->gbase < h->registry.size() && h->registry[h->gbase].holders == 0 && h->registry[h->gbase].inflight == 0)
+    h->gbase++;
   const uint32_t gend = (uint32_t)h->registry.size();
   const uint32_t wlo = h->gbase >> 6, whi = (gend + 63) >> 6, nw = whi - wlo;
   const uint32_t thr = (uint32_t)(((uint64_t)h->loss_bp << 32) / 10000u);
@@ -689,6 +744,13 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     if (h->loss_bp == 0) return true;
     if (h->loss_bp >= 10000) return false;
     return draw(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk) >= thr;
+  };
+  // NetworkEmulator.evaluateDelay of the same message in whole gossip rounds:
+  // sent in round t, it is handled by onGossipReq in round t + delay / gossipInterval
+  const uint32_t gint = (uint32_t)h->cfg.gossip_interval_ms;
+  auto delay_rounds = [&](uint32_t src, uint32_t dst, uint32_t gid, uint32_t tk) -> uint32_t {
+    if (h->delay_mean == 0) return 0;
+    return delay_of_draw(h, draw4(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk).v[1]) / gint;
   };
   // GPI:144-146 "gossips.isEmpty()" on the start-of-round state of every member
   std::vector<uint8_t> nonempty(h->N, 0);
@@ -743,8 +805,11 @@ void gossip_round(oracle_handle* h, uint32_t q) {
             if (w < wlo || w >= whi) continue;
             for (uint64_t c = bt.bits[j] & W[w - wlo] & ~S[w - wlo]; c; c &= c - 1) {
               const uint32_t g = (w << 6) + (uint32_t)__builtin_ctzll(c);
-              // the batch counts for the current GossipState only (created in round inf - 1)
-              if (bt.t < me.gossips.inf[g & (h->rc - 1)] - 1 || !not_lost(p, s, g, bt.tick)) continue;
+              // the batch counts for the current GossipState only (created in round inf - 1); a
+              // delayed message counts from the round it arrived in (before this round's sends)
+              if (!not_lost(p, s, g, bt.tick)) continue;
+              const int64_t arrive = bt.t + delay_rounds(p, s, g, bt.tick);
+              if (arrive < me.gossips.inf[g & (h->rc - 1)] - 1 || arrive >= r) continue;
               S[w - wlo] |= 1ull << (g & 63);
               ++nsupp;
             }
@@ -771,14 +836,38 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       for (uint32_t k = k0; k < k1; ++k) {
         const uint64_t eff = W[k] & ~S[k];
         st.b.bits.push_back(eff);
-        // first receipts: messages p lacks the gossip of, each with its own loss draw
-        for (uint64_t cand = eff & ~held_word(h, pm, wlo + k); cand; cand &= cand - 1) {
+        // first receipts: messages p lacks the gossip of, each with its own loss draw; with
+        // delays every message that is not lost and arrives in a later round travels (p may have
+        // swept the gossip by then, and the message adds s to p's infectedFrom when it arrives)
+        const uint64_t held = held_word(h, pm, wlo + k);
+        for (uint64_t cand = h->delay_mean ? eff : eff & ~held; cand; cand &= cand - 1) {
           const uint32_t g = ((wlo + k) << 6) + (uint32_t)__builtin_ctzll(cand);
-          if (not_lost(s, rp, g, tick)) deliveries.push_back({rp, g});
+          if (!not_lost(s, rp, g, tick)) continue;
+          const uint32_t dr = delay_rounds(s, rp, g, tick);
+          if (dr) {
+            h->flights.push_back({r + (int64_t)dr, rp, s, g});
+            h->registry[g].inflight++;
+          } else if (!((held >> (g & 63)) & 1u)) {
+            deliveries.push_back({rp, g});
+          }
         }
       }
       sent.push_back(std::move(st));
     }
+  }
+  // delayed messages arriving this round, at a receiver still running
+  if (!h->flights.empty()) {
+    size_t o = 0;
+    for (size_t k = 0; k < h->flights.size(); ++k) {
+      const auto& fl = h->flights[k];
+      if (fl.arrive != r) {
+        h->flights[o++] = fl;
+        continue;
+      }
+      h->registry[fl.gid].inflight--;
+      if (h->m[fl.to].alive) deliveries.push_back({fl.to, fl.gid});
+    }
+    h->flights.resize(o);
   }
   // onGossipReq (GPI:171-183): a new id starts a GossipState with infectionPeriod = r + 1
   for (const Delivery& d : deliveries) {
@@ -796,7 +885,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   // ... and addToInfected(from) for every message (GPI:181)
   for (Sent& st : sent) h->m[st.to].recv[st.from].push_back(std::move(st.b));
   if (q + 1 == h->G) {  // batches that can no longer suppress a send
-    const int64_t keep = r + 1 - h->hzn;
+    const int64_t keep = r + 1 - h->hzn - (int64_t)h->dmax_rounds;  // a delayed message arrives late
     for (auto& mm : h->m)
       for (auto it = mm.recv.begin(); it != mm.recv.end();) {
         auto& v = it->second;
@@ -1067,6 +1156,23 @@ int oracle_destroy(oracle_handle* h) {
 int oracle_set_loss(oracle_handle* h, uint32_t loss_bp) {
   if (!h || loss_bp > 10000) return SWIM_EINVAL;
   h->loss_bp = loss_bp;
+  return SWIM_OK;
+}
+
+// NetworkEmulator.setDefaultOutboundSettings(loss, meanDelay) (NE:81-84) of every member: the mean
+// delay part. The threshold table: dthr[k] = ceil(2^32 * (1 - exp(-k / mean))).
+int oracle_set_delay(oracle_handle* h, uint32_t mean_ms) {
+  if (!h || mean_ms > 60000) return SWIM_EINVAL;
+  h->delay_mean = mean_ms;
+  h->dthr.clear();
+  h->dmax_rounds = 0;
+  if (!mean_ms) return SWIM_OK;
+  for (uint32_t k = 0;; ++k) {
+    const double t = std::ceil(std::ldexp(-std::expm1(-(double)k / (double)mean_ms), 32));
+    if (t > 4294967295.0) break;
+    h->dthr.push_back((uint32_t)t);
+  }
+  h->dmax_rounds = (uint32_t)(h->dthr.size() - 1) / (uint32_t)h->cfg.gossip_interval_ms;
   return SWIM_OK;
 }
 

@@ -30,6 +30,7 @@ typedef struct oracle_handle oracle_handle;
 int oracle_create(const swim_config* cfg, oracle_handle** out);
 int oracle_destroy(oracle_handle* h);
 int oracle_set_loss(oracle_handle* h, uint32_t loss_bp);
+int oracle_set_delay(oracle_handle* h, uint32_t mean_ms);
 int oracle_set_partition(oracle_handle* h, const uint8_t* group, uint32_t n, uint64_t t0, uint64_t t1);
 int oracle_block_link(oracle_handle* h, uint32_t src, uint32_t dst, int blocked);
 int oracle_block_inbound(oracle_handle* h, uint32_t dst, uint32_t src, int blocked);

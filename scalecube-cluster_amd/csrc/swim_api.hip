@@ -60,6 +60,7 @@ struct swim_handle {
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
+  uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
@@ -403,6 +404,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 8, "k_gossip_select", [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
+        if (P.delay_on)
+          timed(h, 10, "k_gossip_pairdelay", [&] { hipLaunchKernelGGL(k_gossip_pairdelay, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
         if (W > 1) {  // (1) registrations with receivers on other shards
           Ctl c;
@@ -756,6 +759,17 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.stg_cap = h->CC;
   P.loss_mode = 0;
   P.loss_thr = 0;
+  // message delays: off until swim_set_delay
+  P.delay_on = 0;
+  P.dthr = nullptr;
+  P.dthr_n = 0;
+  P.dq = nullptr;
+  P.dq_head = nullptr;
+  P.dqcap = 0;
+  P.gint = (uint32_t)c.gossip_interval_ms;
+  P.pto = (uint32_t)std::max(0, c.ping_timeout_ms);
+  P.pint = (uint32_t)std::max(0, c.ping_interval_ms);
+  P.mto = (uint32_t)std::max(0, c.metadata_timeout_ms);
   P.link = nullptr;
   P.inlink = nullptr;
   P.rerouted = 0;
@@ -898,6 +912,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.rec_body, P.bcap);
   ALLOC(P.sp_list, P.spcap);
   ALLOC(P.sp_recs, (size_t)P.spcap * MAXREC);
+  ALLOC(P.sp_dq, P.spcap);
   ALLOC(P.pw, P.pwcap);
   ALLOC(P.rp_list, P.spcap);
   ALLOC(P.ctl, 1);
@@ -1045,7 +1060,81 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
     P.loss_mode = 1;
     P.loss_thr = (uint32_t)(((uint64_t)loss_bp << 32) / 10000u);
   }
-  P.batch_commit = (h->cfg.gossip_batching == 0 && P.loss_mode != 1u) ? 1u : 0u;
+  P.batch_commit = (h->cfg.gossip_batching == 0 && P.loss_mode != 1u && !P.delay_on) ? 1u : 0u;
+  return SWIM_OK;
+}
+
+// NetworkEmulator.setDefaultOutboundSettings(loss, meanDelay) of every member, the delay part
+// (NetworkEmulator.java:81-84,189-201,358-368). Each message draws an exponential
+// delay of mean `mean_ms`: GossipRequests are handled delay / gossipInterval rounds later (a
+// per-receiver ring of messages in flight), ping / ping-req / metadata round trips must come back
+// within their timeouts. Delays draw per message, i.e. per gossip: like a probabilistic loss they
+// need one gossip per ring slot. Unsharded handles; rings sized for test-scale clusters.
+int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
+  if (!h || mean_ms > 60000) return SWIM_EINVAL;
+  KP& P = h->base;
+  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_set_delay: not supported on sharded handles");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_set_delay: a period is in flight");
+  if (mean_ms == 0) {
+    if (P.delay_on) {  // messages in flight keep travelling only while delays are on
+      uint32_t* d = reinterpret_cast<uint32_t*>(h->d_digest);
+      HIPC(h, hipMemsetAsync(d, 0, 4, h->stream));
+      hipLaunchKernelGGL(k_dq_pending, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, h->stream, P, d);
+      uint32_t pending = 0;
+      HIPC(h, hipMemcpyAsync(&pending, d, 4, hipMemcpyDeviceToHost, h->stream));
+      HIPC(h, hipStreamSynchronize(h->stream));
+      if (pending) return fail(h, SWIM_EINVAL, "swim_set_delay(0): delayed messages are still in flight");
+    }
+    P.delay_on = 0;
+    P.batch_commit = (h->cfg.gossip_batching == 0 && P.loss_mode != 1u) ? 1u : 0u;
+    return SWIM_OK;
+  }
+  if (P.batched) {  // the same refusal as a probabilistic loss
+    uint32_t* d = reinterpret_cast<uint32_t*>(h->d_digest);
+    HIPC(h, hipMemsetAsync(d, 0, 4, h->stream));
+    hipLaunchKernelGGL(k_multi_live, dim3(256), dim3(256), 0, h->stream, P, d);
+    uint32_t multi = 0;
+    HIPC(h, hipMemcpyAsync(&multi, d, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    if (multi)
+      return fail(h, SWIM_EINVAL,
+                  "swim_set_delay: delays draw per gossip, but live ring slots hold batches of several gossips "
+                  "(DESIGN.md 3.12): set the delay before they are created, or create with gossip_batching = 1");
+  }
+  // dthr[k] = ceil(2^32 (1 - exp(-k / mean))) for every k a 32-bit draw can reach (the oracle
+  // computes the same table with the same expression)
+  std::vector<uint32_t> thr;
+  for (uint32_t k = 0;; ++k) {
+    const double t = std::ceil(std::ldexp(-std::expm1(-(double)k / (double)mean_ms), 32));
+    if (t > 4294967295.0) break;
+    thr.push_back((uint32_t)t);
+  }
+  if (thr.size() > h->dthr_cap) {  // (a smaller earlier table stays allocated until swim_destroy)
+    uint32_t* dt = nullptr;
+    int rc = dalloc(h, &dt, thr.size());
+    if (rc) return rc;
+    P.dthr = dt;
+    h->dthr_cap = (uint32_t)thr.size();
+  }
+  HIPC(h, hipMemcpyAsync(const_cast<uint32_t*>(P.dthr), thr.data(), thr.size() * 4, hipMemcpyHostToDevice, h->stream));
+  P.dthr_n = (uint32_t)thr.size();
+  if (!P.dq) {  // per receiver: messages in flight plus the arrived ones still inside the horizon
+    const uint32_t cap = 4096;
+    if ((uint64_t)P.nloc * cap > (1ull << 28))
+      return fail(h, SWIM_EINVAL, "swim_set_delay: the delayed-message rings are sized for clusters up to 65,536 members");
+    uint4* dq = nullptr;
+    uint32_t* head = nullptr;
+    int rc = dalloc(h, &dq, (size_t)P.nloc * cap);
+    if (!rc) rc = dalloc(h, &head, h->N);
+    if (rc) return rc;
+    HIPC(h, hipMemsetAsync(head, 0, (size_t)h->N * 4, h->stream));
+    P.dq = dq;
+    P.dq_head = head;
+    P.dqcap = cap;
+  }
+  HIPC(h, hipStreamSynchronize(h->stream));
+  P.delay_on = 1;
+  P.batch_commit = 0;  // one gossip per slot while delays are on
   return SWIM_OK;
 }
 

@@ -81,6 +81,8 @@ enum IfromOverflow : uint32_t {
   IF_PAIRS = 4u,       // pruned pairs of a round over spcap / pwcap
   IF_RECORDS = 8u,     // delivery records or their bodies over rcap / bcap within the horizon
   IF_INHIST = 16u,     // a member's in-history ring (IHCAP) wrapped inside the horizon
+  IF_DELAYQ = 32u,     // a receiver's delayed-message ring (dqcap) wrapped over a message still in flight
+                       // or inside the horizon
 };
 
 constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
@@ -295,6 +297,16 @@ struct KP {
   uint32_t* pw;        // [PWCAP] per pruned pair, its window over this round's active list
   uint4* rp_list;      // [SPCAP] this round's recorded deliveries: {in_list entry, receiver, record, sender}
   uint32_t spcap, pwcap;
+  uint32_t* sp_dq;     // [SPCAP] the pair's sender also delivered delayed messages (k_gossip_pairdelay)
+  // message delays (NetworkEmulator meanDelay); delay_on = 0: every message is
+  // handled in the phase it was sent in, as before
+  uint32_t delay_on;
+  const uint32_t* dthr;  // [dthr_n] dthr[k]: the smallest 32-bit draw whose delay is >= k ms
+  uint32_t dthr_n;
+  uint32_t gint, pto, pint, mto;  // gossip interval, ping timeout, ping interval, metadata timeout (ms)
+  uint4* dq;             // [nloc][dqcap] per receiver: delayed GossipRequests {sender, slot, arrival round, flags}
+  uint32_t* dq_head;     // [N] entries ever appended
+  uint32_t dqcap;        // power of two
   Ctl* ctl;
   unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
@@ -363,6 +375,8 @@ constexpr uint32_t SPAIR = 0x40000000u;  // in_list entry: a pruned pair (window
 constexpr uint32_t IHCAP = 512;  // in-history entries per member (~f per round over the horizon: ~2 f hzn,
                                  // with the in-degree tail of 10^6 members)
 constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
+constexpr uint32_t DQ_ARRIVED = 1u;      // delayed-message entry flag: handled by its receiver
+constexpr uint32_t DQ_PAIR = 0x10000u;   // k_gossip_select: the chosen peer delivered delayed messages
 constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
 
 __device__ __forceinline__ void ifrom_overflow(const KP& P, uint32_t why) {
@@ -443,6 +457,30 @@ __device__ __forceinline__ bool delivered(const KP& P, uint32_t kind, uint32_t s
   return out_ok(P, kind, src, dst, c, tick) && in_ok(P, dst, src);
 }
 
+// NetworkEmulator.evaluateDelay (NetworkEmulator.java:358-368) of a message whose draw's second
+// word is u: (long)(-ln(1 - u/2^32) * meanDelay) ms, as the largest k with dthr[k] <= u (the host
+// computes the table once; integer compares only, so the oracle and the device agree exactly).
+__device__ __forceinline__ uint32_t delay_of_draw(const KP& P, uint32_t u) {
+  uint32_t lo = 0, hi = P.dthr_n;  // dthr[0] = 0 <= u
+  while (hi - lo > 1u) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P.dthr[mid] <= u)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+// the delay of message src -> dst (tryDelayOutbound, NetworkEmulator.java:189-201): the same draw as
+// its loss (keyed by the two processes), second word
+__device__ __forceinline__ uint32_t msg_delay(const KP& P, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c,
+                                              uint32_t tick) {
+  if (!P.delay_on) return 0u;
+  const uint32_t rs = route(P, src), rd = route(P, dst);
+  if (rs == NONE || rd == NONE) return 0u;
+  return delay_of_draw(P, draw4(P.seed, kind, rs, rd, c, tick).y);
+}
+
 __device__ __forceinline__ uint32_t susp_periods(const KP& P, uint32_t others) { return P.mult * bitlen(others + 1u); }
 __device__ __forceinline__ uint32_t spread_rounds(const KP& P, uint32_t others) { return P.rm * bitlen(others + 1u); }
 __device__ __forceinline__ uint32_t sweep_rounds(const KP& P, uint32_t others) {
@@ -490,7 +528,11 @@ __device__ __forceinline__ void emit_gossip(const KP& P, uint32_t origin, uint32
 // process at the subject's address answers only requests for its own id (:216-223).
 __device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t subj, uint32_t attempt) {
   if (P.rerouted && route(P, subj) != subj) return false;
-  return delivered(P, K_MREQ, obs, subj, attempt, P.tick) && delivered(P, K_MRESP, subj, obs, attempt, P.tick);
+  if (!delivered(P, K_MREQ, obs, subj, attempt, P.tick) || !delivered(P, K_MRESP, subj, obs, attempt, P.tick))
+    return false;
+  // with message delays the round trip must come back within metadataTimeout (:170)
+  return !P.delay_on ||
+         msg_delay(P, K_MREQ, obs, subj, attempt, P.tick) + msg_delay(P, K_MRESP, subj, obs, attempt, P.tick) < P.mto;
 }
 
 // MembershipProtocolImpl.updateMembership (MembershipProtocolImpl.java:481-547) and callees

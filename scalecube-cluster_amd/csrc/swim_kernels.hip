@@ -752,7 +752,11 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
   // onPing at the process on j's address answers DEST_GONE unless it is j itself (FDI:226-252),
   // which computeMemberStatus turns into DEAD (FDI:370-391)
   const uint32_t acked = (P.rerouted && route(P, j) != j) ? SWIM_DEAD : SWIM_ALIVE;
-  if (delivered(P, K_PING, i, j, 0, P.tick) && delivered(P, K_ACK, j, i, 0, P.tick)) {
+  // the direct round trip counts if it is back within pingTimeout (FDI:145 .timeout); a later ack
+  // competes with the ping-req relays below
+  const bool ping_in = delivered(P, K_PING, i, j, 0, P.tick);
+  const uint32_t t_direct = P.delay_on ? msg_delay(P, K_PING, i, j, 0, P.tick) + msg_delay(P, K_ACK, j, i, 0, P.tick) : 0u;
+  if (ping_in && delivered(P, K_ACK, j, i, 0, P.tick) && (!P.delay_on || t_direct < P.pto)) {
     pr.direct = 1;
     pr.nB = 1;
     pr.stB = acked;
@@ -773,7 +777,10 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
     return pr;
   }
   pr.preq = 1;
-  uint32_t first = NONE;  // the proxy whose forwarded ack reaches i's transport first
+  // the ack that reaches i's transport first (ms after the direct ping was sent): a proxy's
+  // forwarded ack (PING_REQs leave at the direct timeout and wait pingInterval - pingTimeout,
+  // FDI:152-183), or the direct ping's own late ack, which carries the same correlation id
+  uint32_t first = NONE, t_first = NONE;
   for (uint32_t q = 0; q < np; ++q) {
     const uint32_t p = proxies[q];
     if (!out_ok(P, K_PING_REQ, i, p, j, P.tick)) {
@@ -781,10 +788,20 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
       continue;
     }
     ++pr.nB;
-    if (first == NONE && in_ok(P, p, i) && delivered(P, K_PROXY_PING, p, j, i, P.tick) &&
-        delivered(P, K_PROXY_ACK, j, p, i, P.tick) && out_ok(P, K_FWD_ACK, p, i, j, P.tick))
-      first = p;
+    if ((first == NONE || P.delay_on) && in_ok(P, p, i) && delivered(P, K_PROXY_PING, p, j, i, P.tick) &&
+        delivered(P, K_PROXY_ACK, j, p, i, P.tick) && out_ok(P, K_FWD_ACK, p, i, j, P.tick)) {
+      const uint32_t hops = P.delay_on ? msg_delay(P, K_PING_REQ, i, p, j, P.tick) + msg_delay(P, K_PROXY_PING, p, j, i, P.tick) +
+                                             msg_delay(P, K_PROXY_ACK, j, p, i, P.tick) + msg_delay(P, K_FWD_ACK, p, i, j, P.tick)
+                                       : 0u;
+      if (hops < P.pint - P.pto && P.pto + hops < t_first) {  // earliest; ties: selection order
+        first = p;
+        t_first = P.pto + hops;
+      }
+    }
   }
+  if (P.delay_on && pr.nB && ping_in && t_direct >= P.pto && t_direct < P.pint && t_direct <= t_first &&
+      out_ok(P, K_ACK, j, i, 0, P.tick))
+    first = j;  // the late direct ack wins ties
   // cid-only matching (TransportImpl.java:236-238): that ack completes every pending
   // subscription, then i's inbound filter on its sender decides (NetworkEmulatorTransport.java:64-68)
   pr.stB = (first != NONE && in_ok(P, i, first)) ? acked : SWIM_SUSPECT;
@@ -1644,15 +1661,27 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       }
       if (!__any(young)) break;
     }
+    if (P.delay_on) {  // delayed messages from a chosen peer that arrived within the horizon (§3.15)
+      const uint32_t dh = P.dq_head[m], nv = dh < P.dqcap ? dh : P.dqcap;
+      const uint4* dq = P.dq + lrow(P, m) * P.dqcap;
+      for (uint32_t j = lane; j < nv; j += 64u) {
+        const uint4 e = dq[j];
+        if ((e.w & DQ_ARRIVED) && e.z < r && e.z + P.hzn >= r)
+          for (uint32_t q = 0; q < np; ++q)
+            if (s_peers[w][q] == e.x) atomicOr(&s_nrec[w][q], DQ_PAIR);
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (lane < np && s_nrec[w][lane]) {  // this pair's window gets pruned (k_gossip_pairprune)
-      const uint32_t nr = s_nrec[w][lane] < MAXREC ? s_nrec[w][lane] : MAXREC;
+    if (lane < np && s_nrec[w][lane]) {  // this pair's window gets pruned (k_gossip_pairprune / _pairdelay)
+      const uint32_t nrc = s_nrec[w][lane] & (DQ_PAIR - 1u);
+      const uint32_t nr = nrc < MAXREC ? nrc : MAXREC;
       const uint32_t sp = atomicAdd(&P.ctl->sp_cnt, 1u);
       const uint32_t n4 = (n_act + 3u) & ~3u;  // act-indexed window, padded to quads for k_gossip_pull
       const uint32_t off = atomicAdd(&P.ctl->pw_used, n4);
       if (sp < P.spcap && off + n4 <= P.pwcap && off + n4 >= off) {
         P.sp_list[sp] = make_uint4(m, s_peers[w][lane], nr, off);
+        P.sp_dq[sp] = (s_nrec[w][lane] & DQ_PAIR) ? 1u : 0u;
         for (uint32_t c = 0; c < nr; ++c) P.sp_recs[(size_t)sp * MAXREC + c] = s_rec[w][lane][c];
         entry = SPAIR | sp;
       } else {
@@ -1767,6 +1796,53 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   add_stat(P, ST_IF_PAIRS, (blockIdx.x == 0 && threadIdx.x == 0) ? n : 0u);
 }
 
+// Pruned pairs whose peer also delivered delayed messages to the sender: every
+// such message that arrived within the horizon, during the sender's current GossipState of its
+// gossip, takes that gossip out of the pair's window (GossipProtocolImpl.java:181,245-250). One
+// wave per pair scans the sender's delayed-message ring.
+__global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
+  SWIM_GUARD(P);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
+  const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, r = P.round;
+  const uint32_t W32 = P.GC >> 5;
+  uint32_t removed_alive = 0;
+  for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+    if (!P.sp_dq[i]) continue;  // (uniform per wave)
+    const uint4 sp = P.sp_list[i];  // {sender, peer, records, window offset}
+    const uint32_t dh = P.dq_head[sp.x], nv = dh < P.dqcap ? dh : P.dqcap;
+    const uint4* dq = P.dq + lrow(P, sp.x) * P.dqcap;
+    uint32_t removed = 0;
+    for (uint32_t j = lane; j < nv; j += 64u) {
+      const uint4 e = dq[j];  // {peer that sent it, ring slot, arrival round, flags}
+      if (e.x != sp.y || !(e.w & DQ_ARRIVED) || e.z >= r || e.z + P.hzn < r) continue;
+      const uint32_t ws = (e.y >> 5) & (W32 - 1u);
+      const uint2 ap = P.actpos[ws];  // listed this round, as this very word?
+      if (ap.x != r || ap.y >= n_act) continue;
+      const uint32_t ea = P.act[ap.y];
+      if (((w_beg + (ea & ACT_OFF_MASK)) & (W32 - 1u)) != ws || ((ea >> 26) & 3u) == WC_NONE) continue;
+      const uint32_t supp = (1u << (e.y & 31u)) & state_since(P, sp.x, ws, e.z);
+      if (supp) removed += slot_gossips(P, ws, atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
+    }
+    if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
+      removed_alive += removed;
+      if (removed) atomicAdd(&P.dbg_send[2 * sp.x + 1], (unsigned long long)removed);
+    }
+  }
+  add_stat(P, ST_GOSSIP_SUPP, removed_alive);
+}
+
+// delayed messages still in flight (swim_set_delay(0) is refused while any is)
+__global__ void k_dq_pending(KP P, uint32_t* out) {
+  const uint32_t p = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.row0 + P.nloc) return;
+  const uint32_t dh = P.dq_head[p], nv = dh < P.dqcap ? dh : P.dqcap;
+  const uint4* dq = P.dq + lrow(P, p) * P.dqcap;
+  bool any = false;
+  for (uint32_t j = 0; j < nv && !any; ++j) any = dq[j].z >= P.round && !(dq[j].w & DQ_ARRIVED);
+  if (any && P.alive[p]) atomicOr(out, 1u);
+}
+
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
 // position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull).
 // (Drawing lazily at pruning time instead was measured slower: a record is pruned against
@@ -1782,14 +1858,17 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
     v = P.pw[P.sp_list[sreg & ~SPAIR].w + k];
   else
     v = own_window(P, sreg, k, w_beg, lo, hi);
-  if (v && P.loss_mode == 1u) {
+  if (v && (P.loss_mode == 1u || P.delay_on)) {  // this round's deliveries only: not lost, not delayed
     const uint32_t W32 = P.GC >> 5, wi = w_beg + (ea & ACT_OFF_MASK);
     uint32_t need = v;
     v = 0u;
     while (need) {
       const uint32_t b = (uint32_t)__builtin_ctz(need);
       need &= need - 1u;
-      if (draw1(P.seed, K_GOSSIP, sid, p, P.g_hash[(wi & (W32 - 1u)) * 32u + b], P.tick) >= P.loss_thr) v |= 1u << b;
+      const u32x4 d = draw4(P.seed, K_GOSSIP, sid, p, P.g_hash[(wi & (W32 - 1u)) * 32u + b], P.tick);
+      if (P.loss_mode == 1u && d.x < P.loss_thr) continue;
+      if (P.delay_on && delay_of_draw(P, d.y) >= P.gint) continue;
+      v |= 1u << b;
     }
   }
   return v;
@@ -1916,6 +1995,19 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
 // NetworkEmulator.evaluateLoss draws one value per (sender, receiver, gossip) message and is drawn
 // only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
 // receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
+// a delayed GossipRequest sender -> p of ring slot `slot`, handled in round `arrive` (DESIGN.md
+// §3.15): into p's ring (written by p's own pull wave only). The slot's word stays live and listed
+// until then: its wlast (the newest infection round any holder may have) is raised to `arrive`,
+// which only widens the word's age classes (MIXED instead of ALL / NONE: still exact).
+__device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender, uint32_t slot, uint32_t arrive) {
+  const uint32_t pos = atomicAdd(&P.dq_head[p], 1u);
+  uint4* e = P.dq + lrow(P, p) * P.dqcap + (pos & (P.dqcap - 1u));
+  if (pos >= P.dqcap && (*e).z + P.hzn >= P.round) ifrom_overflow(P, IF_DELAYQ);  // in flight / in the horizon
+  *e = make_uint4(sender, slot, arrive, 0u);
+  const uint32_t ws = slot >> 5;
+  if (P.wlast[ws] < arrive) atomicMax(&P.wlast[ws], arrive);
+}
+
 #ifndef SWIM_PULL_WAVES
 #define SWIM_PULL_WAVES 1
 #endif
@@ -1935,10 +2027,12 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   uint32_t* sum = s_sum[threadIdx.x >> 6];
   const uint32_t nsw = (n_act + 31u) >> 5;
-  if (deg && P.alive[p] && n_act) {  // a stopped transport loses every message
+  if ((deg || P.delay_on) && P.alive[p] && n_act) {  // a stopped transport loses every message
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
-    const uint32_t* lackr = (nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
+    // (with delays every message needs its draw, held gossip or not: no skipping)
+    const uint32_t* lackr =
+        (!P.delay_on && nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
     if (nsw <= NSUM)
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
@@ -2021,7 +2115,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
           prev[i] = 0u;
           if (wcv[i] == WC_NONE) continue;
           ++words;
-          if ((hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
+          if (!P.delay_on && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
           todo |= 1u << i;
           anyall |= wcv[i] == WC_ALL ? 1u : 0u;
           anymix |= wcv[i] == WC_MIXED ? 1u : 0u;
@@ -2076,7 +2170,20 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
               ++probes;
               if (!((reach >> (q0 + j)) & 1ull)) continue;
               uint32_t cand = win & ~hw[i] & ~u[i] & ~prev[i];
-              if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+              if (P.delay_on) {  // evaluateLoss + evaluateDelay per message, held gossip or not (§3.15)
+                cand = 0u;
+                for (uint32_t need = win; need; need &= need - 1u) {
+                  const uint32_t b = (uint32_t)__builtin_ctz(need);
+                  const u32x4 d = draw4(P.seed, K_GOSSIP, mv[j], p, P.g_hash[wsv[i] * 32u + b], P.tick);
+                  if (P.loss_mode == 1u && d.x < P.loss_thr) continue;
+                  const uint32_t dr = delay_of_draw(P, d.y) / P.gint;
+                  if (dr == 0u)
+                    cand |= 1u << b;
+                  else
+                    dq_push(P, p, mv[j], wsv[i] * 32u + b, P.round + dr);
+                }
+                cand &= ~hw[i] & ~u[i] & ~prev[i];
+              } else if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
                 uint32_t need = cand;
                 cand = 0u;
                 while (need) {
@@ -2101,6 +2208,28 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
             }
 
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
+    }
+    if (P.delay_on) {  // delayed messages arriving this round (after the senders' plain nb stores)
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint32_t dh = P.dq_head[p], nv = dh < P.dqcap ? dh : P.dqcap;
+      uint4* dq = P.dq + lrow(P, p) * P.dqcap;
+      for (uint32_t j = lane; j < nv; j += 64u) {
+        const uint4 e = dq[j];
+        if (e.z != P.round || (e.w & DQ_ARRIVED)) continue;
+        dq[j].w = e.w | DQ_ARRIVED;  // counts for infectedFrom from now on (k_gossip_select)
+        const uint32_t ws = (e.y >> 5) & (W32 - 1u), bit = 1u << (e.y & 31u);
+        if (hbr[ws] & bit) continue;  // held (after this round's sweep): no new GossipState
+        const uint2 ap = P.actpos[ws];
+        if (ap.x != P.round || ap.y >= n_act) {  // the slot's word is kept listed until then (wlast)
+          atomicOr(&P.ctl->overflow, OV_BUG);
+          continue;
+        }
+        const uint32_t old = atomicOr(&nbr[ap.y], bit);
+        if (!(old & bit)) {
+          ++receipts;
+          if (nsw <= NSUM) atomicOr(&sum[ap.y >> 5], 1u << (ap.y & 31u));
+        }
+      }
     }
     const uint32_t total = wave_sum(receipts);
     if (lane == 0 && total) {

@@ -156,6 +156,7 @@ def api_table(prefix: str):
         (prefix + "create", _I, [ctypes.POINTER(SwimConfig), ctypes.POINTER(_P)]),
         (prefix + "destroy", _I, [_P]),
         (prefix + "set_loss", _I, [_P, _U32]),
+        (prefix + "set_delay", _I, [_P, _U32]),
         (prefix + "set_partition", _I, [_P, _pU8, _U32, _U64, _U64]),
         (prefix + "block_link", _I, [_P, _U32, _U32, _I]),
         (prefix + "block_inbound", _I, [_P, _U32, _U32, _I]),

@@ -136,6 +136,13 @@ class SwimCluster:
         """setDefaultOutboundSettings(lossPercent, 0) on every member (NetworkEmulator.java:81-84)."""
         self._call("set_loss", self._h, int(round(percent * 100)))
 
+    def set_delay(self, mean_ms: int):
+        """setDefaultOutboundSettings(lossPercent, meanDelay) on every member, the delay part
+        (NetworkEmulator.java:81-84,189-201,358-368): each message is delayed by an exponential draw
+        of mean `mean_ms`. GossipRequests then arrive rounds later, ping / ping-req
+        / metadata round trips must come back within their timeouts. Unsharded handles."""
+        self._call("set_delay", self._h, int(mean_ms))
+
     def partition(self, groups, t0: int, t1: int):
         g = np.ascontiguousarray(np.asarray(groups, dtype=np.uint8))
         assert g.shape == (self.n,)

@@ -531,11 +531,10 @@ def gossip_dissemination_bound(make):
 
 
 # -- GossipProtocolTest (:48-64 grid, asserts :154, :155-161, :173) ------------------------
-# (N, loss %) of the reference's experiments; its mean delays (2 ms, and 100 ms in two rows) are
-# below one gossip interval (200 ms): until the delay model exists every row
-# runs with deliveries inside the round, i.e. at the 2 ms setting.
-GOSSIP_GRID = [(2, 0), (2, 0), (3, 0), (5, 0), (10, 0), (10, 10), (10, 25), (10, 25), (10, 50), (50, 0), (50, 10),
-               (50, 10)]
+# (N, loss %, mean delay ms) of the reference's experiments, delays included: a
+# GossipRequest is handled delay // gossipInterval rounds after it was sent
+GOSSIP_GRID = [(2, 0, 2), (2, 0, 2), (3, 0, 2), (5, 0, 2), (10, 0, 2), (10, 10, 2), (10, 25, 2), (10, 25, 100),
+               (10, 50, 2), (50, 0, 2), (50, 10, 2), (50, 10, 100)]
 
 
 def gossip_test_config(n):
@@ -550,13 +549,14 @@ def gossip_protocol_grid(make):
     """testGossipProtocol (:110-208): member 0 spreads one gossip; every other member receives it
     (:154) within gossipTimeoutToSweep (:155-161), and no member has it delivered twice (:173),
     over the whole gossip lifetime plus three intervals (awaitFullCompletion, :163-169)."""
-    for idx, (n, loss) in enumerate(GOSSIP_GRID):
+    for idx, (n, loss, delay) in enumerate(GOSSIP_GRID):
         cfg = gossip_test_config(n)
         g = cfg.gossipConfig()
         interval = g.gossipInterval()
         rounds_per_period = cfg.failureDetectorConfig().pingInterval() // interval
         c = make(cfg, n, 300 + idx)
         c.set_loss(loss)
+        c.set_delay(delay)
         c.step(1)
         c.events()
         tag = 0x5EED0000 + idx

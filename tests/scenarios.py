@@ -162,6 +162,23 @@ def _metadata(c, loss):
         yield
 
 
+def _delay(c, mean_ms, loss, n_crash, before, periods, part=0):
+    # NetworkEmulator mean delays (NetworkEmulator.java:189-201,358-368):
+    # GossipRequests arrive rounds late (and may find their gossip swept), pings / ping-req relays /
+    # metadata fetches time out when the round trip is too slow; with loss, a crash and optionally
+    # an even/odd partition that heals
+    c.set_loss(loss)
+    c.set_delay(mean_ms)
+    c.step(before)
+    yield
+    c.crash(crash_ids(c.n, n_crash, c.seed))
+    if part:
+        c.partition((np.arange(c.n) % 2).astype(np.uint8), before + 2, before + 2 + part)
+    for _ in range(periods):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -192,6 +209,14 @@ SCENARIOS = {
         ClusterConfig.defaultLanConfig().membership(lambda o: o.seedMembers([0, 1, 2, 3])),
         288, 12, lambda c: _churn(c, [5, 40, 41, 100, 200, 255], [256, 257, 258, 259], [260, 261, 262], 5.0),
         {"n_initial": 256}),
+    # message delays: local (gossip 100 ms: P(delay >= 1 round) = e^-1 at 100 ms mean), LAN (200 ms
+    # rounds, 500 ms ping timeout), and the MembershipProtocolTest config (20 ms rounds, 100 ms ping
+    # timeout: delays of up to ~30 rounds, most ping round trips time out) with a partition
+    "local64_delay100_loss10": (ClusterConfig.defaultLocalConfig(), 64, 16, lambda c: _delay(c, 100, 10.0, 2, 3, 25)),
+    "lan256_delay200_crash3": (ClusterConfig.defaultLanConfig(), 256, 17, lambda c: _delay(c, 200, 0.0, 3, 3, 30)),
+    "test48_delay30_partition": (
+        test_membership_config().membership(lambda o: o.seedMembers(0, 1)),
+        48, 18, lambda c: _delay(c, 30, 5.0, 1, 4, 30, part=8)),
 }
 
 

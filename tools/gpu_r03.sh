@@ -7,7 +7,7 @@ OUT=gpurun_out/${1:-r03}
 shift
 TESTS=${*:-tests/test_gpu_parity.py}
 mkdir -p "$OUT"
-timeout -k 10 ${PYTEST_LIMIT:-600} python -u -m pytest $TESTS -m gpu -x -q -p no:cacheprovider --timeout 400 \
+timeout -k 10 ${PYTEST_LIMIT:-600} python -u -m pytest $TESTS -m gpu ${PYTEST_X--x} -q -p no:cacheprovider --timeout 400 \
   --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest.log" 2>&1 || { echo "pytest rc=$?"; exit 1; }
 echo "pytest ok"
 [ -n "$NO_BENCH" ] && exit 0
