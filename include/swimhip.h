@@ -102,7 +102,10 @@ typedef struct swim_config {
   int32_t ping_req_members;
   int32_t gossip_fanout;
   int32_t gossip_interval_ms;
-  int32_t gossip_repeat_mult;
+  int32_t gossip_repeat_mult; /* infection rounds are kept mod 2^8: swim_create rejects
+                               gossip_repeat_mult * bit_length(n_members) > 83 (sweep + infectedFrom
+                               horizon past 255 rounds), e.g. 4 at 2^20 members or 5 at 65,536; the
+                               reference's presets (3, local 2) pass at every size up to 2^27 */
   int32_t sync_interval_ms;
   int32_t sync_timeout_ms;
   int32_t suspicion_mult;
@@ -172,6 +175,8 @@ typedef struct swim_stats {
   uint64_t live_gossip_records; /* gossips held in the live ring slots (live_gossip_slots counts batches) */
   uint64_t events_updated;    /* MembershipEvent UPDATED: an accepted ALIVE record whose fetched
                                  metadata differs from the stored one (MembershipProtocolImpl.java:589-610) */
+  uint64_t apply_pairs;       /* receiver pairs k_gossip_apply processed two to a workgroup; 0 in the oracle */
+  uint64_t commit_radix;      /* commit phases sorted by the chip-wide radix sort; 0 in the oracle      */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -191,7 +196,7 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp);
  * :81-84, tryDelayOutbound :189-201, evaluateDelay :358-368; 0 = none; <= 60,000). Each message draws
  * an exponential delay: a GossipRequest is handled delay / gossipInterval rounds after it was sent,
  * and a ping, ping-req relay or metadata round trip counts only if it returns within its timeout
- * (DESIGN.md §3.15). Draws per message, so, like a probabilistic loss, it needs one gossip per ring
+ * (DESIGN.md §3.16). Draws per message, so, like a probabilistic loss, it needs one gossip per ring
  * slot (SWIM_EINVAL while batch slots are live). Switching back to 0 is refused while delayed messages
  * are in flight. Unsharded handles, up to 65,536 members. */
 int swim_set_delay(swim_handle* h, uint32_t mean_ms);

@@ -250,7 +250,7 @@ struct oracle_handle {
   uint32_t delay_mean = 0;
   std::vector<uint32_t> dthr;
   uint32_t dmax_rounds = 0;  // the longest gossip delay a draw can give, in rounds
-  // GossipRequests delayed past their round (DESIGN.md §3.15): delivered at the start of round
+  // GossipRequests delayed past their round (DESIGN.md §3.16): delivered at the start of round
   // `arrive`'s onGossipReq step to process `to`, if it still runs
   struct Flight {
     int64_t arrive;
@@ -745,7 +745,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
     if (h->loss_bp >= 10000) return false;
     return draw(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk) >= thr;
   };
-  // NetworkEmulator.evaluateDelay of the same message in whole gossip rounds (DESIGN.md §3.15):
+  // NetworkEmulator.evaluateDelay of the same message in whole gossip rounds (DESIGN.md §3.16):
   // sent in round t, it is handled by onGossipReq in round t + delay / gossipInterval
   const uint32_t gint = (uint32_t)h->cfg.gossip_interval_ms;
   auto delay_rounds = [&](uint32_t src, uint32_t dst, uint32_t gid, uint32_t tk) -> uint32_t {
@@ -1160,7 +1160,7 @@ int oracle_set_loss(oracle_handle* h, uint32_t loss_bp) {
 }
 
 // NetworkEmulator.setDefaultOutboundSettings(loss, meanDelay) (NE:81-84) of every member: the mean
-// delay part (DESIGN.md §3.15). The threshold table: dthr[k] = ceil(2^32 * (1 - exp(-k / mean))).
+// delay part (DESIGN.md §3.16). The threshold table: dthr[k] = ceil(2^32 * (1 - exp(-k / mean))).
 int oracle_set_delay(oracle_handle* h, uint32_t mean_ms) {
   if (!h || mean_ms > 60000) return SWIM_EINVAL;
   h->delay_mean = mean_ms;

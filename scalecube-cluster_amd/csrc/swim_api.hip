@@ -759,7 +759,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.stg_cap = h->CC;
   P.loss_mode = 0;
   P.loss_thr = 0;
-  // message delays: off until swim_set_delay (DESIGN.md §3.15)
+  // message delays: off until swim_set_delay (DESIGN.md §3.16)
   P.delay_on = 0;
   P.dthr = nullptr;
   P.dthr_n = 0;
@@ -1065,7 +1065,7 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
 }
 
 // NetworkEmulator.setDefaultOutboundSettings(loss, meanDelay) of every member, the delay part
-// (NetworkEmulator.java:81-84,189-201,358-368; DESIGN.md §3.15). Each message draws an exponential
+// (NetworkEmulator.java:81-84,189-201,358-368; DESIGN.md §3.16). Each message draws an exponential
 // delay of mean `mean_ms`: GossipRequests are handled delay / gossipInterval rounds later (a
 // per-receiver ring of messages in flight), ping / ping-req / metadata round trips must come back
 // within their timeouts. Delays draw per message, i.e. per gossip: like a probabilistic loss they
@@ -1534,6 +1534,8 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->apply_spills = stats[ST_APPLY_SPILL];
   out->apply_records = stats[ST_APPLY_RECS];
   out->events_updated = stats[ST_UPDATED];
+  out->apply_pairs = stats[ST_APPLY_PAIRS];
+  out->commit_radix = stats[ST_COMMIT_RADIX];
   {  // gossips in the live slots: the record ring from the oldest live slot's first record
     uint32_t c_lo = ctl.ccount;
     if (ctl.gcount != ctl.glo && ctl.gcount - ctl.glo <= h->GC) {

@@ -59,6 +59,8 @@ enum StatIdx : int {
   ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
   ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply_b expanded into its entry bitmap
   ST_UPDATED,      // MembershipEvent UPDATED (MembershipProtocolImpl.java:599-600)
+  ST_APPLY_PAIRS,  // receiver pairs k_gossip_apply processed in two half-workgroups (SWIM_APPLY_PAIR)
+  ST_COMMIT_RADIX, // commit phases sorted by the chip-wide radix sort (more than CS_SMALL gossips)
   ST_COUNT
 };
 
@@ -298,7 +300,7 @@ struct KP {
   uint4* rp_list;      // [SPCAP] this round's recorded deliveries: {in_list entry, receiver, record, sender}
   uint32_t spcap, pwcap;
   uint32_t* sp_dq;     // [SPCAP] the pair's sender also delivered delayed messages (k_gossip_pairdelay)
-  // message delays (NetworkEmulator meanDelay, DESIGN.md §3.15); delay_on = 0: every message is
+  // message delays (NetworkEmulator meanDelay, DESIGN.md §3.16); delay_on = 0: every message is
   // handled in the phase it was sent in, as before
   uint32_t delay_on;
   const uint32_t* dthr;  // [dthr_n] dthr[k]: the smallest 32-bit draw whose delay is >= k ms

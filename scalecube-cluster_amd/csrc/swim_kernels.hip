@@ -581,6 +581,7 @@ __global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
   P.ctl->c_prev = P.ctl->ccount;
   P.ctl->ccount += n;
   if (stg) P.ctl->stg_count = 0u;
+  atomicAdd(&P.stat_shards[ST_COMMIT_RADIX], 1ull);  // (one thread: shard 0)
 }
 
 // Does a possibly-live ring slot hold a batch of several gossips? (swim_set_loss)
@@ -753,7 +754,7 @@ __device__ __forceinline__ Probe fd_probe(const KP& P, uint32_t i, bool commit) 
   // which computeMemberStatus turns into DEAD (FDI:370-391)
   const uint32_t acked = (P.rerouted && route(P, j) != j) ? SWIM_DEAD : SWIM_ALIVE;
   // the direct round trip counts if it is back within pingTimeout (FDI:145 .timeout); a later ack
-  // competes with the ping-req relays below (DESIGN.md §3.15)
+  // competes with the ping-req relays below (DESIGN.md §3.16)
   const bool ping_in = delivered(P, K_PING, i, j, 0, P.tick);
   const uint32_t t_direct = P.delay_on ? msg_delay(P, K_PING, i, j, 0, P.tick) + msg_delay(P, K_ACK, j, i, 0, P.tick) : 0u;
   if (ping_in && delivered(P, K_ACK, j, i, 0, P.tick) && (!P.delay_on || t_direct < P.pto)) {
@@ -1661,7 +1662,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       }
       if (!__any(young)) break;
     }
-    if (P.delay_on) {  // delayed messages from a chosen peer that arrived within the horizon (§3.15)
+    if (P.delay_on) {  // delayed messages from a chosen peer that arrived within the horizon (§3.16)
       const uint32_t dh = P.dq_head[m], nv = dh < P.dqcap ? dh : P.dqcap;
       const uint4* dq = P.dq + lrow(P, m) * P.dqcap;
       for (uint32_t j = lane; j < nv; j += 64u) {
@@ -1796,7 +1797,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   add_stat(P, ST_IF_PAIRS, (blockIdx.x == 0 && threadIdx.x == 0) ? n : 0u);
 }
 
-// Pruned pairs whose peer also delivered delayed messages to the sender (DESIGN.md §3.15): every
+// Pruned pairs whose peer also delivered delayed messages to the sender (DESIGN.md §3.16): every
 // such message that arrived within the horizon, during the sender's current GossipState of its
 // gossip, takes that gossip out of the pair's window (GossipProtocolImpl.java:181,245-250). One
 // wave per pair scans the sender's delayed-message ring.
@@ -1996,7 +1997,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
 // only for gossips p still lacks. Receipts are OR-ed into nb (zero outside a round's receivers);
 // receivers with any join alist. Senders come in chunks of <= 64 (in_list, then in_ov).
 // a delayed GossipRequest sender -> p of ring slot `slot`, handled in round `arrive` (DESIGN.md
-// §3.15): into p's ring (written by p's own pull wave only). The slot's word stays live and listed
+// §3.16): into p's ring (written by p's own pull wave only). The slot's word stays live and listed
 // until then: its wlast (the newest infection round any holder may have) is raised to `arrive`,
 // which only widens the word's age classes (MIXED instead of ALL / NONE: still exact).
 __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender, uint32_t slot, uint32_t arrive) {
@@ -2170,7 +2171,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
               ++probes;
               if (!((reach >> (q0 + j)) & 1ull)) continue;
               uint32_t cand = win & ~hw[i] & ~u[i] & ~prev[i];
-              if (P.delay_on) {  // evaluateLoss + evaluateDelay per message, held gossip or not (§3.15)
+              if (P.delay_on) {  // evaluateLoss + evaluateDelay per message, held gossip or not (§3.16)
                 cand = 0u;
                 for (uint32_t need = win; need; need &= need - 1u) {
                   const uint32_t b = (uint32_t)__builtin_ctz(need);
@@ -2342,6 +2343,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     const bool pair = SWIM_APPLY_PAIR && hcap_log >= 7u && li2 < n_list && 8u * P.alist[2 * li + 1] <= hcap &&
                       8u * P.alist[2 * li2 + 1] <= hcap && (n_act + 31u) / 32u <= NSUM;  // uniform
     const uint32_t half = pair ? (threadIdx.x >> 9) : 0u;
+    add_stat(P, ST_APPLY_PAIRS, (pair && threadIdx.x == 0u) ? 1u : 0u);
     const uint32_t tid = pair ? (threadIdx.x & 511u) : threadIdx.x, nthr = pair ? 512u : blockDim.x;
     const uint32_t mli = half ? li2 : li;
     li += pair ? 2u * gridDim.x : gridDim.x;

@@ -116,6 +116,8 @@ STAT_FIELDS = [
     "apply_records",
     "live_gossip_records",
     "events_updated",
+    "apply_pairs",
+    "commit_radix",
 ]
 
 

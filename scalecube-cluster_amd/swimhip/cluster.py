@@ -139,7 +139,7 @@ class SwimCluster:
     def set_delay(self, mean_ms: int):
         """setDefaultOutboundSettings(lossPercent, meanDelay) on every member, the delay part
         (NetworkEmulator.java:81-84,189-201,358-368): each message is delayed by an exponential draw
-        of mean `mean_ms` (DESIGN.md §3.15). GossipRequests then arrive rounds later, ping / ping-req
+        of mean `mean_ms` (DESIGN.md §3.16). GossipRequests then arrive rounds later, ping / ping-req
         / metadata round trips must come back within their timeouts. Unsharded handles."""
         self._call("set_delay", self._h, int(mean_ms))
 

@@ -531,7 +531,7 @@ def gossip_dissemination_bound(make):
 
 
 # -- GossipProtocolTest (:48-64 grid, asserts :154, :155-161, :173) ------------------------
-# (N, loss %, mean delay ms) of the reference's experiments, delays included (DESIGN.md §3.15): a
+# (N, loss %, mean delay ms) of the reference's experiments, delays included (DESIGN.md §3.16): a
 # GossipRequest is handled delay // gossipInterval rounds after it was sent
 GOSSIP_GRID = [(2, 0, 2), (2, 0, 2), (3, 0, 2), (5, 0, 2), (10, 0, 2), (10, 10, 2), (10, 25, 2), (10, 25, 100),
                (10, 50, 2), (50, 0, 2), (50, 10, 2), (50, 10, 100)]

@@ -163,7 +163,7 @@ def _metadata(c, loss):
 
 
 def _delay(c, mean_ms, loss, n_crash, before, periods, part=0):
-    # NetworkEmulator mean delays (NetworkEmulator.java:189-201,358-368; DESIGN.md §3.15):
+    # NetworkEmulator mean delays (NetworkEmulator.java:189-201,358-368; DESIGN.md §3.16):
     # GossipRequests arrive rounds late (and may find their gossip swept), pings / ping-req relays /
     # metadata fetches time out when the round trip is too slow; with loss, a crash and optionally
     # an even/odd partition that heals

@@ -234,7 +234,9 @@ for _ in range(6):
     sx, sy = x.stats(), y.stats()
     assert {{k: sx[k] for k in scenarios.PARITY_KEYS}} == {{k: sy[k] for k in scenarios.PARITY_KEYS}}
 spills += x.stats()["apply_spills"]
-print("SPILLS", spills, "RECORDS", x.stats()["apply_records"], "RADIX", x.stats()["gossips_created"])
+pairs = a.stats()["apply_pairs"] + x.stats()["apply_pairs"]
+radix = a.stats()["commit_radix"] + x.stats()["commit_radix"]
+print("SPILLS", spills, "PAIRS", pairs, "RADIX", radix, "RECORDS", x.stats()["apply_records"])
 """
 
 
@@ -262,34 +264,26 @@ def test_commit_radix_path_parity():
     (-DSWIM_CS_SMALL=32) runs the churn scenario and the C3 storm at N = 1,024 through it: bit-exact
     with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable)."""
     out = _run_variant("libswimhip_cs32.so", _SPILL_SCRIPT)
-    assert "SPILLS" in out
+    radix = int(out.split("RADIX")[-1].split()[0])
+    assert radix > 0, "the chip-wide radix sort never ran"
 
 
 def test_apply_spill_path_parity():
     """k_gossip_apply's overflow paths (a subject that finds no LDS hash slot within HPROBE probes
     goes through the global inbox and the LDS spill list; the summary walk without compaction when
     the table is at its cap) only run in storm rounds of the full C3 bench with the product's
-    16,384-slot hash. A variant built with a 64-slot hash (__graft_entry__.build, -DSWIM_APPLY_HLOG=6)
-    takes them in almost every round: it must still match the oracle bit for bit, and the spill
-    counter proves the path ran. The same variant gives the batch-slot kernel (k_gossip_apply_b,
-    lossless C3 part) a 4-subject record dictionary (-DSWIM_DICT_SIDS=4) and a 4-entry spill list:
-    most records find no entry, so the bitmap maxima go through the inbox with them (the
-    exactly-once merge of DESIGN.md §3.15) and the inbox-row scan runs too."""
-    import os
-    import subprocess
-    import sys
-
-    here = os.path.dirname(os.path.abspath(__file__))
-    repo = os.path.dirname(here)
-    lib = os.path.join(repo, "variants", "libswimhip_hlog6.so")
-    assert os.path.exists(lib), "variant not built: run __graft_entry__.build()"
-    paths = [here, repo, os.path.join(repo, "oracle"), os.path.join(repo, "scalecube-cluster_amd")]
-    env = dict(os.environ, SWIMHIP_LIB=lib)
-    out = subprocess.run([sys.executable, "-c", _SPILL_SCRIPT.format(paths=paths)], env=env, capture_output=True,
-                         text=True, timeout=600)
-    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
-    spills = int(out.stdout.split("SPILLS")[-1].split()[0])
+    16,384-slot hash. A variant built with a 128-slot hash (__graft_entry__.build, -DSWIM_APPLY_HLOG=7)
+    takes them in almost every round, and still pairs small receivers (two 64-slot half tables, each
+    with half the spill list): it must match the oracle bit for bit, and the spill and pair counters
+    prove both paths ran. The same variant gives the batch-slot kernel (k_gossip_apply_b, lossless C3
+    part) a 4-subject record dictionary (-DSWIM_DICT_SIDS=4) and a 4-entry spill list: most records
+    find no entry, so the bitmap maxima go through the inbox with them (the exactly-once merge of
+    DESIGN.md §3.15) and the inbox-row scan runs too."""
+    out = _run_variant("libswimhip_hlog7.so", _SPILL_SCRIPT)
+    spills = int(out.split("SPILLS")[-1].split()[0])
+    pairs = int(out.split("PAIRS")[-1].split()[0])
     assert spills > 0, "the spill path never ran"
+    assert pairs > 0, "no receivers were paired"
 
 
 def test_c3long_schedule_small_parity():
