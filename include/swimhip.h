@@ -197,8 +197,8 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp);
  * an exponential delay: a GossipRequest is handled delay / gossipInterval rounds after it was sent,
  * and a ping, ping-req relay or metadata round trip counts only if it returns within its timeout
  * (DESIGN.md §3.16). Draws per message, so, like a probabilistic loss, it needs one gossip per ring
- * slot (SWIM_EINVAL while batch slots are live). Switching back to 0 is refused while delayed messages
- * are in flight. Unsharded handles, up to 65,536 members. */
+ * slot (SWIM_EINVAL while batch slots are live). Messages already in flight keep their arrival rounds
+ * when the mean changes (or is reset to 0). Unsharded handles, up to 65,536 members. */
 int swim_set_delay(swim_handle* h, uint32_t mean_ms);
 /* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
  * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */

@@ -199,6 +199,7 @@ struct GossipMap {
 struct Batch {
   int64_t t;
   uint32_t tick;
+  uint32_t dmean;  // the mean delay its messages were sent under (their arrival rounds)
   uint32_t w0;
   std::vector<uint64_t> bits;
 };
@@ -248,8 +249,8 @@ struct oracle_handle {
   // its exponential draw as a threshold table: dthr[k] = the smallest 32-bit uniform whose delay
   // -ln(1 - u/2^32) * mean (NE:358-368) is >= k ms, for every k a 32-bit draw can reach
   uint32_t delay_mean = 0;
-  std::vector<uint32_t> dthr;
-  uint32_t dmax_rounds = 0;  // the longest gossip delay a draw can give, in rounds
+  std::map<uint32_t, std::vector<uint32_t>> dthr;  // per mean ever set (batches keep their own)
+  uint32_t dmax_rounds = 0;  // the longest gossip delay any mean set so far can give, in rounds
   // GossipRequests delayed past their round: delivered at the start of round
   // `arrive`'s onGossipReq step to process `to`, if it still runs
   struct Flight {
@@ -342,15 +343,16 @@ bool delivered(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst
 // delay in whole ms, from the second word of the message's draw (the first is its loss draw, so one
 // Philox block decides both): (long)(-ln(1 - x) * meanDelay) with x = u / 2^32, read from the
 // threshold table (exact integer compares, no floating point per message).
-uint32_t delay_of_draw(const oracle_handle* h, uint32_t u) {
-  if (h->delay_mean == 0) return 0;
-  return (uint32_t)(std::upper_bound(h->dthr.begin(), h->dthr.end(), u) - h->dthr.begin()) - 1u;
+uint32_t delay_of_draw(const oracle_handle* h, uint32_t mean, uint32_t u) {
+  if (mean == 0) return 0;
+  const std::vector<uint32_t>& t = h->dthr.at(mean);
+  return (uint32_t)(std::upper_bound(t.begin(), t.end(), u) - t.begin()) - 1u;
 }
 uint32_t msg_delay(const oracle_handle* h, uint32_t kind, uint32_t src, uint32_t dst, uint32_t c, uint32_t tick) {
   if (h->delay_mean == 0) return 0;
   const uint32_t rs = route(h, src), rd = route(h, dst);
   if (rs == NONE || rd == NONE) return 0;  // not sent at all (out_ok fails)
-  return delay_of_draw(h, draw4(h->seed, kind, rs, rd, c, tick).v[1]);
+  return delay_of_draw(h, h->delay_mean, draw4(h->seed, kind, rs, rd, c, tick).v[1]);
 }
 
 void perm_keys(const oracle_handle* h, uint32_t kind, uint32_t member, uint32_t epoch, uint32_t* k) {
@@ -748,9 +750,9 @@ void gossip_round(oracle_handle* h, uint32_t q) {
   // NetworkEmulator.evaluateDelay of the same message in whole gossip rounds:
   // sent in round t, it is handled by onGossipReq in round t + delay / gossipInterval
   const uint32_t gint = (uint32_t)h->cfg.gossip_interval_ms;
-  auto delay_rounds = [&](uint32_t src, uint32_t dst, uint32_t gid, uint32_t tk) -> uint32_t {
-    if (h->delay_mean == 0) return 0;
-    return delay_of_draw(h, draw4(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk).v[1]) / gint;
+  auto delay_rounds = [&](uint32_t mean, uint32_t src, uint32_t dst, uint32_t gid, uint32_t tk) -> uint32_t {
+    if (mean == 0) return 0;
+    return delay_of_draw(h, mean, draw4(h->seed, K_GOSSIP, src, dst, h->registry[gid].hash, tk).v[1]) / gint;
   };
   // GPI:144-146 "gossips.isEmpty()" on the start-of-round state of every member
   std::vector<uint8_t> nonempty(h->N, 0);
@@ -808,7 +810,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
               // the batch counts for the current GossipState only (created in round inf - 1); a
               // delayed message counts from the round it arrived in (before this round's sends)
               if (!not_lost(p, s, g, bt.tick)) continue;
-              const int64_t arrive = bt.t + delay_rounds(p, s, g, bt.tick);
+              const int64_t arrive = bt.t + delay_rounds(bt.dmean, p, s, g, bt.tick);
               if (arrive < me.gossips.inf[g & (h->rc - 1)] - 1 || arrive >= r) continue;
               S[w - wlo] |= 1ull << (g & 63);
               ++nsupp;
@@ -828,7 +830,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
       }
       // the link part of delivered(): both alive, no partition cut, no outbound / inbound block
       if (!nsend || !pm.alive || h->loss_bp >= 10000 || !link_ok(h, s, p)) continue;
-      Sent st{rp, s, Batch{r, tick, 0, {}}};
+      Sent st{rp, s, Batch{r, tick, h->delay_mean, 0, {}}};
       uint32_t k0 = 0, k1 = nw;
       while (k0 < k1 && !(W[k0] & ~S[k0])) ++k0;
       while (k1 > k0 && !(W[k1 - 1] & ~S[k1 - 1])) --k1;
@@ -843,7 +845,7 @@ void gossip_round(oracle_handle* h, uint32_t q) {
         for (uint64_t cand = h->delay_mean ? eff : eff & ~held; cand; cand &= cand - 1) {
           const uint32_t g = ((wlo + k) << 6) + (uint32_t)__builtin_ctzll(cand);
           if (!not_lost(s, rp, g, tick)) continue;
-          const uint32_t dr = delay_rounds(s, rp, g, tick);
+          const uint32_t dr = delay_rounds(h->delay_mean, s, rp, g, tick);
           if (dr) {
             h->flights.push_back({r + (int64_t)dr, rp, s, g});
             h->registry[g].inflight++;
@@ -1163,16 +1165,15 @@ int oracle_set_loss(oracle_handle* h, uint32_t loss_bp) {
 // delay part. The threshold table: dthr[k] = ceil(2^32 * (1 - exp(-k / mean))).
 int oracle_set_delay(oracle_handle* h, uint32_t mean_ms) {
   if (!h || mean_ms > 60000) return SWIM_EINVAL;
-  h->delay_mean = mean_ms;
-  h->dthr.clear();
-  h->dmax_rounds = 0;
-  if (!mean_ms) return SWIM_OK;
+  h->delay_mean = mean_ms;  // messages already sent keep their arrival rounds (Batch::dmean, flights)
+  if (!mean_ms || h->dthr.count(mean_ms)) return SWIM_OK;
+  std::vector<uint32_t>& t = h->dthr[mean_ms];
   for (uint32_t k = 0;; ++k) {
-    const double t = std::ceil(std::ldexp(-std::expm1(-(double)k / (double)mean_ms), 32));
-    if (t > 4294967295.0) break;
-    h->dthr.push_back((uint32_t)t);
+    const double v = std::ceil(std::ldexp(-std::expm1(-(double)k / (double)mean_ms), 32));
+    if (v > 4294967295.0) break;
+    t.push_back((uint32_t)v);
   }
-  h->dmax_rounds = (uint32_t)(h->dthr.size() - 1) / (uint32_t)h->cfg.gossip_interval_ms;
+  h->dmax_rounds = std::max(h->dmax_rounds, (uint32_t)(t.size() - 1) / (uint32_t)h->cfg.gossip_interval_ms);
   return SWIM_OK;
 }
 

@@ -404,7 +404,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 8, "k_gossip_select", [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
-        if (P.delay_on)
+        if (P.dq)  // rings exist once a delay was set; messages in flight arrive even after it is reset
           timed(h, 10, "k_gossip_pairdelay", [&] { hipLaunchKernelGGL(k_gossip_pairdelay, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
         if (W > 1) {  // (1) registrations with receivers on other shards
@@ -765,7 +765,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.dthr_n = 0;
   P.dq = nullptr;
   P.dq_head = nullptr;
+  P.dq_rhead = nullptr;
   P.dqcap = 0;
+  P.dq_live = 0;
   P.gint = (uint32_t)c.gossip_interval_ms;
   P.pto = (uint32_t)std::max(0, c.ping_timeout_ms);
   P.pint = (uint32_t)std::max(0, c.ping_interval_ms);
@@ -1075,16 +1077,7 @@ int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
   KP& P = h->base;
   if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_set_delay: not supported on sharded handles");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_set_delay: a period is in flight");
-  if (mean_ms == 0) {
-    if (P.delay_on) {  // messages in flight keep travelling only while delays are on
-      uint32_t* d = reinterpret_cast<uint32_t*>(h->d_digest);
-      HIPC(h, hipMemsetAsync(d, 0, 4, h->stream));
-      hipLaunchKernelGGL(k_dq_pending, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, h->stream, P, d);
-      uint32_t pending = 0;
-      HIPC(h, hipMemcpyAsync(&pending, d, 4, hipMemcpyDeviceToHost, h->stream));
-      HIPC(h, hipStreamSynchronize(h->stream));
-      if (pending) return fail(h, SWIM_EINVAL, "swim_set_delay(0): delayed messages are still in flight");
-    }
+  if (mean_ms == 0) {  // new messages travel at once; those in flight still arrive (k_gossip_pull)
     P.delay_on = 0;
     P.batch_commit = (h->cfg.gossip_batching == 0 && P.loss_mode != 1u) ? 1u : 0u;
     return SWIM_OK;
@@ -1118,20 +1111,29 @@ int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
   }
   HIPC(h, hipMemcpyAsync(const_cast<uint32_t*>(P.dthr), thr.data(), thr.size() * 4, hipMemcpyHostToDevice, h->stream));
   P.dthr_n = (uint32_t)thr.size();
+  // an entry matters until its message arrived and left the infectedFrom horizon: the per-round
+  // head history (256 rounds) must reach that far back
+  const uint32_t live = (P.dthr_n - 1u) / P.gint + P.hzn + 1u;
+  if (live >= 256u) return fail(h, SWIM_EINVAL, "swim_set_delay: delays this long (in gossip rounds) exceed the ring history");
   if (!P.dq) {  // per receiver: messages in flight plus the arrived ones still inside the horizon
-    const uint32_t cap = 4096;
-    if ((uint64_t)P.nloc * cap > (1ull << 28))
+    if (P.nloc > 65536u)
       return fail(h, SWIM_EINVAL, "swim_set_delay: the delayed-message rings are sized for clusters up to 65,536 members");
+    uint32_t cap = 65536;  // entries per receiver, within 2 GiB of rings
+    while (cap > 4096u && (uint64_t)P.nloc * cap * 16u > (2ull << 30)) cap >>= 1;
     uint4* dq = nullptr;
-    uint32_t* head = nullptr;
+    uint32_t *head = nullptr, *rhead = nullptr;
     int rc = dalloc(h, &dq, (size_t)P.nloc * cap);
     if (!rc) rc = dalloc(h, &head, h->N);
+    if (!rc) rc = dalloc(h, &rhead, (size_t)P.nloc * 256u);
     if (rc) return rc;
     HIPC(h, hipMemsetAsync(head, 0, (size_t)h->N * 4, h->stream));
+    HIPC(h, hipMemsetAsync(rhead, 0, (size_t)P.nloc * 256u * 4, h->stream));
     P.dq = dq;
     P.dq_head = head;
+    P.dq_rhead = rhead;
     P.dqcap = cap;
   }
+  P.dq_live = std::max(P.dq_live, live);  // entries pushed under an earlier, longer mean stay covered
   HIPC(h, hipStreamSynchronize(h->stream));
   P.delay_on = 1;
   P.batch_commit = 0;  // one gossip per slot while delays are on

@@ -308,7 +308,9 @@ struct KP {
   uint32_t gint, pto, pint, mto;  // gossip interval, ping timeout, ping interval, metadata timeout (ms)
   uint4* dq;             // [nloc][dqcap] per receiver: delayed GossipRequests {sender, slot, arrival round, flags}
   uint32_t* dq_head;     // [N] entries ever appended
+  uint32_t* dq_rhead;    // [nloc][256] dq_head at the start of each round's pull (mod 256)
   uint32_t dqcap;        // power of two
+  uint32_t dq_live;      // rounds an entry can matter after it was pushed: longest delay + horizon + 1
   Ctl* ctl;
   unsigned long long* stat_shards;  // [STAT_SHARDS][STAT_STRIDE]
 };
@@ -378,6 +380,21 @@ constexpr uint32_t IHCAP = 512;  // in-history entries per member (~f per round 
                                  // with the in-degree tail of 10^6 members)
 constexpr uint32_t MAXREC = 16;  // records one pruned pair may carry
 constexpr uint32_t DQ_ARRIVED = 1u;      // delayed-message entry flag: handled by its receiver
+
+// The positions [*lo, *hi) of receiver p's delayed-message ring that can still matter in this
+// round: pushed within the last dq_live rounds (an older entry arrived and left the infectedFrom
+// horizon), and still in the ring. A stale head of a round p's pull did not run in is older,
+// so the window only grows (still exact).
+__device__ __forceinline__ void dq_window(const KP& P, uint32_t p, uint32_t* lo, uint32_t* hi) {
+  const uint32_t h = P.dq_head[p];
+  uint32_t l = h > P.dqcap ? h - P.dqcap : 0u;
+  if (P.round >= P.dq_live) {
+    const uint32_t l1 = P.dq_rhead[lrow(P, p) * 256u + ((P.round - P.dq_live) & 255u)];
+    if (l1 > l && l1 <= h) l = l1;
+  }
+  *lo = l;
+  *hi = h;
+}
 constexpr uint32_t DQ_PAIR = 0x10000u;   // k_gossip_select: the chosen peer delivered delayed messages
 constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
 

@@ -1662,11 +1662,12 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       }
       if (!__any(young)) break;
     }
-    if (P.delay_on) {  // delayed messages from a chosen peer that arrived within the horizon (§3.16)
-      const uint32_t dh = P.dq_head[m], nv = dh < P.dqcap ? dh : P.dqcap;
+    if (P.dq) {  // delayed messages from a chosen peer that arrived within the horizon (§3.16)
+      uint32_t q0, q1;
+      dq_window(P, m, &q0, &q1);
       const uint4* dq = P.dq + lrow(P, m) * P.dqcap;
-      for (uint32_t j = lane; j < nv; j += 64u) {
-        const uint4 e = dq[j];
+      for (uint32_t j = q0 + lane; j < q1; j += 64u) {
+        const uint4 e = dq[j & (P.dqcap - 1u)];
         if ((e.w & DQ_ARRIVED) && e.z < r && e.z + P.hzn >= r)
           for (uint32_t q = 0; q < np; ++q)
             if (s_peers[w][q] == e.x) atomicOr(&s_nrec[w][q], DQ_PAIR);
@@ -1811,11 +1812,12 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
   for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
     if (!P.sp_dq[i]) continue;  // (uniform per wave)
     const uint4 sp = P.sp_list[i];  // {sender, peer, records, window offset}
-    const uint32_t dh = P.dq_head[sp.x], nv = dh < P.dqcap ? dh : P.dqcap;
+    uint32_t q0, q1;
+    dq_window(P, sp.x, &q0, &q1);
     const uint4* dq = P.dq + lrow(P, sp.x) * P.dqcap;
     uint32_t removed = 0;
-    for (uint32_t j = lane; j < nv; j += 64u) {
-      const uint4 e = dq[j];  // {peer that sent it, ring slot, arrival round, flags}
+    for (uint32_t j = q0 + lane; j < q1; j += 64u) {
+      const uint4 e = dq[j & (P.dqcap - 1u)];  // {peer that sent it, ring slot, arrival round, flags}
       if (e.x != sp.y || !(e.w & DQ_ARRIVED) || e.z >= r || e.z + P.hzn < r) continue;
       const uint32_t ws = (e.y >> 5) & (W32 - 1u);
       const uint2 ap = P.actpos[ws];  // listed this round, as this very word?
@@ -1831,17 +1833,6 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
     }
   }
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
-}
-
-// delayed messages still in flight (swim_set_delay(0) is refused while any is)
-__global__ void k_dq_pending(KP P, uint32_t* out) {
-  const uint32_t p = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.row0 + P.nloc) return;
-  const uint32_t dh = P.dq_head[p], nv = dh < P.dqcap ? dh : P.dqcap;
-  const uint4* dq = P.dq + lrow(P, p) * P.dqcap;
-  bool any = false;
-  for (uint32_t j = 0; j < nv && !any; ++j) any = dq[j].z >= P.round && !(dq[j].w & DQ_ARRIVED);
-  if (any && P.alive[p]) atomicOr(out, 1u);
 }
 
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
@@ -2028,9 +2019,11 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   uint32_t* sum = s_sum[threadIdx.x >> 6];
   const uint32_t nsw = (n_act + 31u) >> 5;
-  if ((deg || P.delay_on) && P.alive[p] && n_act) {  // a stopped transport loses every message
+  if ((deg || P.dq) && P.alive[p] && n_act) {  // a stopped transport loses every message
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
+    if (P.dq && lane == 0)  // where this round's pushes start (dq_window)
+      P.dq_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.dq_head[p];
     // (with delays every message needs its draw, held gossip or not: no skipping)
     const uint32_t* lackr =
         (!P.delay_on && nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
@@ -2210,14 +2203,15 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
 
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
-    if (P.delay_on) {  // delayed messages arriving this round (after the senders' plain nb stores)
+    if (P.dq) {  // delayed messages arriving this round (after the senders' plain nb stores)
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const uint32_t dh = P.dq_head[p], nv = dh < P.dqcap ? dh : P.dqcap;
+      uint32_t q0, q1;
+      dq_window(P, p, &q0, &q1);
       uint4* dq = P.dq + lrow(P, p) * P.dqcap;
-      for (uint32_t j = lane; j < nv; j += 64u) {
-        const uint4 e = dq[j];
+      for (uint32_t j = q0 + lane; j < q1; j += 64u) {
+        const uint4 e = dq[j & (P.dqcap - 1u)];
         if (e.z != P.round || (e.w & DQ_ARRIVED)) continue;
-        dq[j].w = e.w | DQ_ARRIVED;  // counts for infectedFrom from now on (k_gossip_select)
+        dq[j & (P.dqcap - 1u)].w = e.w | DQ_ARRIVED;  // counts for infectedFrom from now on (k_gossip_select)
         const uint32_t ws = (e.y >> 5) & (W32 - 1u), bit = 1u << (e.y & 31u);
         if (hbr[ws] & bit) continue;  // held (after this round's sweep): no new GossipState
         const uint2 ap = P.actpos[ws];

@@ -11,7 +11,10 @@ wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
 lg = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 periods = int(sys.argv[3]) if len(sys.argv) > 3 else 60
 w = bench.WORKLOADS[wl]
-c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=1 << lg, sync_capacity=8192)
+kw = {"tracked_subjects": w["tracked"]} if w.get("tracked") else {}
+c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=1 << lg, sync_capacity=8192, **kw)
+if w["loss"]:
+    c.set_loss(w["loss"])
 c.step(3)
 bench.inject_faults(c, wl, 3, 1)
 t = time.time()
@@ -23,6 +26,7 @@ for p in range(periods):
         print("period", p, "ERROR", e, flush=True)
         break
     s = c.stats()
-    print(f"period {p} created {s['gossips_created']} live {s['live_gossip_slots']} syncs {s['syncs_delivered']} "
+    print(f"period {p} created {s['gossips_created']} live {s['live_gossip_slots']} records {s['live_gossip_records']} "
+          f"syncs {s['syncs_delivered']} "
           f"removed {s['events_removed']} dt {time.time() - t1:.3f}s", flush=True)
 c.close()
