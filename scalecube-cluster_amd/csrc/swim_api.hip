@@ -1026,10 +1026,13 @@ int swim_destroy(swim_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
 #ifdef SWIM_APPLY_PROF
   {  // k_gossip_apply phase profile (wall clock at 100 MHz, summed over workgroups)
-    unsigned long long ph[4] = {0, 0, 0, 0};
-    if (hipMemcpy(ph, h->base.dbg_log, sizeof ph, hipMemcpyDeviceToHost) == hipSuccess)
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpy(ph, h->base.dbg_log, sizeof ph, hipMemcpyDeviceToHost) == hipSuccess) {
       std::fprintf(stderr, "apply phases (workgroup-ms): init %.1f compact %.1f items %.1f subjects %.1f\n",
                    ph[0] / 1e5, ph[1] / 1e5, ph[2] / 1e5, ph[3] / 1e5);
+      std::fprintf(stderr, "apply_b phases (wave-ms): bitmap init %.1f words+records %.1f merge %.1f spill %.1f\n",
+                   ph[4] / 1e5, ph[5] / 1e5, ph[6] / 1e5, ph[7] / 1e5);
+    }
   }
 #endif
   free_all(h);

@@ -2667,7 +2667,19 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   };
+#ifdef SWIM_APPLY_PROF  // per-wave phase wall clock (100 MHz), summed: dbg_log u64 [4..7]
+  unsigned long long tp = wall_clock64();
+#define APPLYB_MARK(q)                                                                     \
+  if (lane == 0) {                                                                         \
+    const unsigned long long tn = wall_clock64();                                          \
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 4 + (q), tn - tp);        \
+    tp = tn;                                                                               \
+  }
+#else
+#define APPLYB_MARK(q)
+#endif
   for (uint32_t t = lane; t < bw; t += 64u) s_bm[t] = 0u;
+  APPLYB_MARK(0);
   for (uint32_t li = blockIdx.x * AW_WAVES + wv; li < n_list; li += gridDim.x * AW_WAVES) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
@@ -2800,6 +2812,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
       }
     }
     wsync();
+    APPLYB_MARK(1);
     const uint32_t snap = P.cnt[p];
     auto apply = [&](uint32_t subj, uint32_t r1) {
       ++nsubj;
@@ -2845,6 +2858,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
       }
     }
     wsync();
+    APPLYB_MARK(2);
     const uint32_t nsp = min(s_misc[0], AW_SPILL);
     if (__any(rowscan)) {  // every spilled subject: the inbox row's nonzero cells
       __threadfence();
@@ -2861,6 +2875,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
     if (lane == 0) atomicAdd(&P.held[p], total);
     nspills += lane == 0 ? s_misc[0] : 0u;
     wsync();  // the spill counter is reset for the wave's next receiver
+    APPLYB_MARK(3);
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
   add_stat(P, ST_APPLY_WORDS, nwords);

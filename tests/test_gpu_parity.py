@@ -219,6 +219,9 @@ from oracle_py import OracleCluster
 from swimhip import SwimCluster
 a, b = scenarios.run_pair("lan288_restart_join_loss5", SwimCluster, OracleCluster)
 spills = a.stats()["apply_spills"]
+# a lossy run with few gossips in flight: small receipt sets, which k_gossip_apply pairs
+a2, b2 = scenarios.run_pair("lan256_loss5_crash3", SwimCluster, OracleCluster)
+spills += a2.stats()["apply_spills"]
 import bench
 from swimhip import ClusterConfig
 n = 1024
@@ -234,7 +237,7 @@ for _ in range(6):
     sx, sy = x.stats(), y.stats()
     assert {{k: sx[k] for k in scenarios.PARITY_KEYS}} == {{k: sy[k] for k in scenarios.PARITY_KEYS}}
 spills += x.stats()["apply_spills"]
-pairs = a.stats()["apply_pairs"] + x.stats()["apply_pairs"]
+pairs = a.stats()["apply_pairs"] + a2.stats()["apply_pairs"] + x.stats()["apply_pairs"]
 radix = a.stats()["commit_radix"] + x.stats()["commit_radix"]
 print("SPILLS", spills, "PAIRS", pairs, "RADIX", radix, "RECORDS", x.stats()["apply_records"])
 """

@@ -12,7 +12,7 @@ lg = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 periods = int(sys.argv[3]) if len(sys.argv) > 3 else 60
 w = bench.WORKLOADS[wl]
 kw = {"tracked_subjects": w["tracked"]} if w.get("tracked") else {}
-c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=1 << lg, sync_capacity=8192, **kw)
+c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=1 << lg, sync_capacity=w.get("scap", 0), **kw)
 if w["loss"]:
     c.set_loss(w["loss"])
 c.step(3)
