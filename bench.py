@@ -126,6 +126,11 @@ def kernel_bytes(name, d, rounds_per_period=5):
     return 0
 
 
+# kernel class (swim_kernel_time index names) -> the kernels rocprof sees under it
+KERNEL_NAMES = {"k_gossip_apply": ["k_gossip_apply", "k_gossip_apply_b"],
+                "k_gossip_pairwin": ["k_gossip_pairfill", "k_gossip_pairprune", "k_gossip_pairdelay"]}
+
+
 def pmc_traffic(kernel, workload="c3", world=1, steps=None, warmup=None):
     """HBM bytes per launch of `kernel` from the committed PMC summary of exactly this run: the same
     workload, --steps and --warmup on one GPU (tools/gpu_pmc.sh: separate FETCH_SIZE and WRITE_SIZE
@@ -139,8 +144,13 @@ def pmc_traffic(kernel, workload="c3", world=1, steps=None, warmup=None):
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    k = d.get(kernel)
-    return None if k is None else k["fetch_bytes_x2"] + k["write_bytes"]
+    # a kernel class may be one of several kernels (k_gossip_apply is k_gossip_apply_b while the
+    # ring holds batch slots): the one of the class this window dispatched most
+    cands = [d[n] for n in KERNEL_NAMES.get(kernel, [kernel]) if n in d]
+    if not cands:
+        return None
+    k = max(cands, key=lambda v: v.get("dispatches", 0))
+    return k["fetch_bytes_x2"] + k["write_bytes"]
 
 
 def roofline_of(name, ktimes, d, world, rounds_per_period=5):
