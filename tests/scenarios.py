@@ -225,6 +225,9 @@ SCENARIOS_EXTRA = {
     # C4's schedule shape (BASELINE configs[3]: LAN defaults, 1 % loss, 0.1 % simultaneous crash)
     # at 4,096 members
     "lan4096_c4_shape": (ClusterConfig.defaultLanConfig(), 4096, 13, lambda c: _lan_loss(c, 4, 16, 1.0, t0=3)),
+    # C5's shape (BASELINE configs[4]: N x K views, concurrent crashes, LAN, no loss: gossip batches)
+    # at 4,096 members with 64 crashes, past the first suspicion timeouts (65 periods at b = 13)
+    "nxk4096_c5_shape": (ClusterConfig.defaultLanConfig(), 4096, 19, lambda c: _lan_loss(c, 64, 70, 0.0, t0=3)),
 }
 
 

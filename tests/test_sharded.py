@@ -20,25 +20,29 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
 
 
-def _exchange_worker(rank, world, port):
-    """Drive ShardedSwimCluster._exchange with host buffers and check every op's semantics."""
-    _init(rank, world, port)
+def _exchange_worker(rank, world, port, backend="gloo"):
+    """Drive ShardedSwimCluster._exchange and check every op's semantics: host buffers over gloo,
+    or (backend "nccl") HBM buffers over RCCL, the path bench.py --gpus N takes."""
+    _init(rank, world, port, backend)
     try:
         c = object.__new__(ShardedSwimCluster)
         c._dist, c._torch, c._group = dist, torch, None
-        c.rank, c.world, c._gloo = rank, world, True
-        c._send = torch.zeros(64, dtype=torch.int32)
-        c._recv = torch.zeros(256, dtype=torch.int32)
+        c.rank, c.world, c._gloo = rank, world, backend == "gloo"
+        dev = "cpu" if backend == "gloo" else "cuda:0"
+        c._send = torch.zeros(64, dtype=torch.int32, device=dev)
+        c._recv = torch.zeros(256, dtype=torch.int32, device=dev)
         x = c._x = nat.SwimXchg()
         # all-gather of unequal contributions, padded to the max
         n = 2 + 3 * rank
-        c._send[:n] = torch.arange(n, dtype=torch.int32) + 100 * rank
+        c._send[:n] = torch.arange(n, dtype=torch.int32, device=dev) + 100 * rank
         x.op, x.send_words = nat.X_ALLGATHER, n
         c._exchange(c._status(None))
         m = int(x.recv_stride)
@@ -79,6 +83,15 @@ def _exchange_worker(rank, world, port):
 
 def test_exchange_protocol_gloo_cpu():
     mp.spawn(_exchange_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
+def test_exchange_protocol_rccl_one_rank():
+    """The RCCL ("nccl" backend) calls of the sharded path — status all-gather, all_gather_into_tensor
+    and all_to_all_single on int32 HBM buffers with split sizes — on a one-rank group: RCCL refuses
+    two ranks on one GPU, so this is how far the collectives can be exercised before the driver's
+    multi-GPU run."""
+    mp.spawn(_exchange_worker, args=(1, _free_port(), "nccl"), nprocs=1, join=True)
 
 
 def _parity_worker(rank, world, port, names):
@@ -142,6 +155,29 @@ def _c4_worker(rank, world, port):
                            compare_every=4)
     finally:
         dist.destroy_process_group()
+
+
+def _c5_worker(rank, world, port):
+    import scenarios
+    from swimhip import SwimCluster
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        scenarios.run_pair("nxk4096_c5_shape", lambda *a, **k: ShardedSwimCluster(*a, tracked_subjects=256, **k),
+                           lambda *a, **k: SwimCluster(*a, tracked_subjects=256, **k), compare_every=5)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_c5_shape_world4_matches_unsharded():
+    """C5's shape (BASELINE configs[4]: N x K views with K = 256, 256 concurrent crashes ... here 64
+    of 4,096 members, LAN, gossip batches) over 4 observer-row shards (gloo, ranks sharing cuda:0):
+    column requests all-gathered and allocated in subject order on every shard, SYNC rows of K
+    columns, batch slots committed identically everywhere; bit-exact with the unsharded N x K
+    handle, which the parity suite pins to the dense oracle."""
+    mp.spawn(_c5_worker, args=(4, _free_port()), nprocs=4, join=True)
 
 
 @pytest.mark.gpu
