@@ -1034,6 +1034,14 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
 int swim_destroy(swim_handle* h) {
   if (!h) return SWIM_EINVAL;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+#ifdef SWIM_SEL_PROF
+  {  // k_gossip_select phase profile (wall clock at 100 MHz, summed over waves)
+    unsigned long long ph[12] = {};
+    if (hipMemcpy(ph, h->base.dbg_log, sizeof ph, hipMemcpyDeviceToHost) == hipSuccess)
+      std::fprintf(stderr, "select phases (wave-ms): holdings %.1f peers %.1f infectedFrom %.1f register %.1f\n",
+                   ph[8] / 1e5, ph[9] / 1e5, ph[10] / 1e5, ph[11] / 1e5);
+  }
+#endif
 #ifdef SWIM_APPLY_PROF
   {  // k_gossip_apply phase profile (wall clock at 100 MHz, summed over workgroups)
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};

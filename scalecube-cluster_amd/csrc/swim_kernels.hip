@@ -1357,6 +1357,17 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+#ifdef SWIM_SEL_PROF  // per-wave phase wall clock (100 MHz), summed: dbg_log u64 [8..11]
+  unsigned long long tp = wall_clock64();
+#define SEL_MARK(q)                                                                        \
+  if (lane == 0) {                                                                         \
+    const unsigned long long tn = wall_clock64();                                          \
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 8 + (q), tn - tp);        \
+    tp = tn;                                                                               \
+  }
+#else
+#define SEL_MARK(q)
+#endif
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const bool mine = m < P.row0 + P.nloc;
   const bool active = mine && P.alive[m] && lo < hi;
@@ -1591,6 +1602,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     }
     if (lack_ok && lane == 0) P.lack_round[m] = r;
   }
+  SEL_MARK(0);
   uint32_t np = 0;
   if (any) {
     // selectGossipMembers, wave-cooperative: lanes test 64 consecutive positions of the
@@ -1654,6 +1666,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (lane < np) P.peers[(size_t)m * P.f + lane] = s_peers[w][lane];
   }
+  SEL_MARK(1);
   // spreadGossipsTo is a no-op for an empty window: only non-empty windows reach receivers
   const bool reg = __any(win_l) && np > 0u;
   // GossipRequest messages: every window gossip to every alive peer (GPI:225-239), counted here
@@ -1721,6 +1734,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       }
     }
   }
+  SEL_MARK(2);
   if (reg && lane < np) {
     uint32_t p = s_peers[w][lane];
     if (P.rerouted && route(P, p) != NONE) p = route(P, p);  // the process at p's address receives it
@@ -1734,6 +1748,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       e[1] = p;
     }
   }
+  SEL_MARK(3);
   nclear = wave_sum(nclear);
   if (any && lane == 0 && nclear) P.held[m] -= nclear;
   if (mine && lane == 0) P.npeers[m] = reg ? np : 0u;
