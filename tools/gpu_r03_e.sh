@@ -9,7 +9,7 @@ mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_sharded.py -m gpu -q -p no:cacheprovider \
   --timeout 300 --timeout-method thread -k "spill or radix or nxk_shards or rccl or c5_shape or delay" > $out/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $out/status.log; [ $rc -le 1 ] || exit $rc
-for v in prof_nobm prof; do
+for v in prof_nobm prof selprof; do
   SWIMHIP_LIB=variants_ab/libswimhip_$v.so timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --converge 0 \
     --no-cpu-baseline > $out/bench_$v.json 2> $out/bench_$v.err
   rc=$?; echo "$v rc=$rc" >> $out/status.log; [ $rc -le 1 ] || exit $rc
