@@ -916,6 +916,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   }
   ALLOC(P.ih, NL * IHCAP);
   ALLOC(P.ih_head, N);
+  ALLOC(P.ih_snd, NL * IHCAP);
+  ALLOC(P.ih_rhead, NL * 256);
   ALLOC(P.dbg_send, 2ull * N);
   ALLOC(P.dbg_log, 256 * 8);
   ALLOC(P.rec_hdr, P.rcap);
@@ -1003,6 +1005,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.wsum, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.ih_rhead, 0, NL * 256 * 4, s);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.lack_round, (size_t)N, NONE);
   (void)hipMemsetAsync(P.dbg_send, 0, (size_t)N * 16, s);
   (void)hipMemsetAsync(P.dbg_log, 0, 256 * 8 * 4, s);

@@ -295,6 +295,8 @@ struct KP {
   uint32_t* dbg_log;             // [256][8] round, window bits, alive peers, peers, peer ids x3, suppressed
   uint4* ih;           // [nloc][IHCAP] in-history ring: {sender, round, record or NONE, 0}
   uint32_t* ih_head;   // [N] entries ever appended
+  uint32_t* ih_snd;    // [nloc][IHCAP] the sender of each entry: select scans these 4 B only
+  uint32_t* ih_rhead;  // [nloc][256] ih_head at the start of each round's k_gossip_inhist (mod 256)
   uint4* rec_hdr;      // [RCAP] delivery records: {deliverer, owner (receiver), round, body offset}
   uint32_t* rec_len;   // [RCAP] body words (the active list length of that round)
   uint32_t* rec_body;  // [BCAP] per position of that round's active list: the gossips delivered

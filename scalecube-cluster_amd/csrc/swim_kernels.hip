@@ -154,6 +154,7 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
     P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
     if (P.meta_view) P.meta_view[lrow(P, x) * P.W + c] = 0u;
   }
+  for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) P.ih_rhead[lrow(P, x) * 256u + t] = 0u;
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;
     P.cnt_delta[x] = 0;
@@ -1680,30 +1681,32 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     if (lane < MAXF) s_nrec[w][lane] = 0u;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // the entries appended since round r - hzn (the per-round head history; a stale head is
+    // older, so the window only grows): their senders (4 B each), the whole entry on a match
     const uint32_t head = P.ih_head[m];
-    const uint32_t nvalid = head < IHCAP ? head : IHCAP;
+    uint32_t first = head > IHCAP ? head - IHCAP : 0u;
+    if (r >= P.hzn) {
+      const uint32_t h0 = P.ih_rhead[lrow(P, m) * 256u + ((r - P.hzn) & 255u)];
+      if (h0 > first && h0 <= head) first = h0;
+    }
     const uint4* ring = P.ih + lrow(P, m) * IHCAP;
-    for (uint32_t b0 = 0; b0 < nvalid; b0 += 64u) {
-      const uint32_t j = b0 + lane;
-      bool young = false;
-      if (j < nvalid) {
-        const uint4 e = ring[(head - 1u - j) & (IHCAP - 1u)];
-        young = e.y + P.hzn >= r;
-        if (young)
-          for (uint32_t q = 0; q < np; ++q)
-            if (s_peers[w][q] == e.x) {
-              if (e.z == NONE) {  // a delivery predicted never to be sent back: cannot stay exact
-                ifrom_overflow(P, IF_MISPREDICT);
-              } else {
-                const uint32_t c = atomicAdd(&s_nrec[w][q], 1u);
-                if (c < MAXREC)
-                  s_rec[w][q][c] = e.z;
-                else
-                  ifrom_overflow(P, IF_MAXREC);
-              }
-            }
-      }
-      if (!__any(young)) break;
+    const uint32_t* snd = P.ih_snd + lrow(P, m) * IHCAP;
+    for (uint32_t j = first + lane; j < head; j += 64u) {
+      const uint32_t x = snd[j & (IHCAP - 1u)];
+      for (uint32_t q = 0; q < np; ++q)
+        if (s_peers[w][q] == x) {
+          const uint4 e = ring[j & (IHCAP - 1u)];
+          if (e.y + P.hzn < r) break;  // too old to suppress anything
+          if (e.z == NONE) {  // a delivery predicted never to be sent back: cannot stay exact
+            ifrom_overflow(P, IF_MISPREDICT);
+          } else {
+            const uint32_t c = atomicAdd(&s_nrec[w][q], 1u);
+            if (c < MAXREC)
+              s_rec[w][q][c] = e.z;
+            else
+              ifrom_overflow(P, IF_MAXREC);
+          }
+        }
     }
     if (P.dq) {  // delayed messages from a chosen peer that arrived within the horizon (§3.16)
       uint32_t q0, q1;
@@ -1939,6 +1942,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
+  if (lane == 0) P.ih_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.ih_head[p];  // k_gossip_select's window
   const uint32_t deg = P.in_cnt[p];
   if (!deg || !P.alive[p] || P.loss_mode == 2u) return;  // nothing can be delivered
   const uint32_t r = P.round, n_act = P.ctl->n_act;
@@ -2017,6 +2021,7 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
       uint4* slot = ring + (pos & (IHCAP - 1u));
       if (pos >= IHCAP && (*slot).y + P.hzn >= r) ifrom_overflow(P, IF_INHIST);
       *slot = make_uint4(sid, r, rec, 0u);
+      P.ih_snd[lrow(P, p) * IHCAP + (pos & (IHCAP - 1u))] = sid;
     }
     ihh += (uint32_t)__popcll(reach);
   }
