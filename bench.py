@@ -55,11 +55,12 @@ WORKLOADS = {
                     n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
+    # BASELINE configs[4] as stated: needs >= 2 GPUs (the storm keeps ~1.8e5 batch slots live, and
+    # every member keeps an infection round per slot: 2^18 x 2^20 bytes does not fit one GPU)
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
                     "crashes (concurrent churn), suspicion-timeout sweep",
-               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 17, tracked=256),
-    # round 2's stand-in for C5 (before gossip batches, DESIGN.md §3.12, its 256-crash storm did not
-    # fit one GPU): the full-size N x K geometry with the churn per-gossip holdings could hold
+               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
+    # C5's full size with the churn one GPU holds at that size (tests/test_gpu_fullsize.py)
     "c5g": dict(desc="C5 geometry at 1,048,576 members: N x K tracked-subject views (K = 256), LAN defaults, 8 "
                      "simultaneous crashes, suspicion-timeout sweep",
                 n=1 << 20, preset="lan", loss=0.0, crash_n=8, part=0, gcap=1 << 17, tracked=256),

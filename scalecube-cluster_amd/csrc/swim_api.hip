@@ -280,7 +280,6 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
     if (h->dict_on) {
       hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
-      if (P.g_bm) hipLaunchKernelGGL(k_dict_bm, dim3(1024), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, DICT_SIDS / 256)), dim3(256), 0, s, P);
     }
   });
@@ -837,14 +836,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.d_last, DICT_IDS);
     ALLOC(P.d_free, DICT_SIDS);
   }
-  // entry bitmaps of big batch slots: GC x 8 KiB (1 GiB at the C3 ring), when the dictionary is
-  // wide enough for whole-bitmap ORs and the ring is at most 2^18 slots
-  P.g_bm = nullptr;
-  P.g_bmok = nullptr;
-  if (h->dict_on && BM_ON && h->GC <= (1u << 18)) {
-    ALLOC(P.g_bm, (size_t)h->GC * DICT_WORDS);
-    ALLOC(P.g_bmok, h->GC);
-  }
   ALLOC(P.wsum, h->GC / 32);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
@@ -992,7 +983,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.last_removed, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.meta_cur, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
-  if (P.g_bmok) (void)hipMemsetAsync(P.g_bmok, 0, h->GC, s);
   if (h->dict_on) {
     (void)hipMemsetAsync(P.sid_of, 0xFF, (size_t)N * 4, s);
     (void)hipMemsetAsync(P.d_subj, 0xFF, (size_t)DICT_SIDS * 4, s);

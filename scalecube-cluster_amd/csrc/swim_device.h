@@ -234,11 +234,6 @@ struct KP {
   uint32_t* d_last;   // [DICT_IDS] unwrapped index + 1 of the newest ring record naming the entry
   uint32_t* d_free;   // [DICT_SIDS] stack of free blocks
   uint32_t* c_id;     // [CC] entry of each record-ring record; ID_USER, or ID_NONE (slow path)
-  // Entry bitmaps of big batch slots: a slot of >= BM_MIN records whose records
-  // all have entries gets its records' entries as a DICT_WORDS-word bitmap at commit, which a
-  // receiver ORs into its own instead of one LDS atomic per record (nullptr: off)
-  uint32_t* g_bm;     // [GC][DICT_WORDS]
-  uint8_t* g_bmok;    // [GC] 1: the slot's bitmap is complete
   uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
                       // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
@@ -364,15 +359,7 @@ constexpr uint32_t ID_NONE = NONE;               // c_id of a record that found 
 constexpr uint32_t DICT_LOCK = 0xFFFFFFFEu;      // sid_of while k_dict_claim allocates the block
 static_assert(DICT_SIDS >= 4 && (DICT_SIDS & (DICT_SIDS - 1)) == 0 && DICT_SIDS <= (1u << 16),
               "SWIM_DICT_SIDS: a power of two in 4 .. 65536");
-#ifndef SWIM_BM_MIN
-#define SWIM_BM_MIN 256
-#endif
-constexpr uint32_t BM_MIN = SWIM_BM_MIN;  // records of a batch slot that earn it an entry bitmap
-// whole-bitmap ORs go 16 B per lane: only for dictionaries of >= 64 words (not the tiny test variant)
-#ifndef SWIM_BM
-#define SWIM_BM 1
-#endif
-constexpr bool BM_ON = SWIM_BM && DICT_WORDS >= 64 && DICT_WORDS % 4 == 0;
+
 
 // the unwrapped index of the live record ring's first record: the oldest possibly-live slot's
 // first one (the ring's end when no slot is live)

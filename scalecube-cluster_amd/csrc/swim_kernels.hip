@@ -672,36 +672,6 @@ __global__ void k_dict_entries(KP P) {
   }
 }
 
-// Entry bitmaps of the commit's big batch slots: one workgroup per slot clears the slot's bitmap
-// and ORs in its records' entries; a record without an entry (no block / ways left, or a user
-// gossip) marks the bitmap incomplete, and apply walks that slot's records instead.
-__global__ void __launch_bounds__(256) k_dict_bm(KP P) {
-  __shared__ uint32_t s_bad;
-  const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount;
-  for (uint32_t g = g0 + blockIdx.x; (int32_t)(g1 - g) > 0; g += gridDim.x) {
-    const uint32_t s = g & P.gmask;
-    const uint2 cr = P.g_cref[s];
-    if (cr.y - cr.x < BM_MIN) {
-      if (threadIdx.x == 0) P.g_bmok[s] = 0;
-      continue;
-    }
-    uint32_t* bm = P.g_bm + (size_t)s * DICT_WORDS;
-    for (uint32_t t = threadIdx.x; t < DICT_WORDS; t += blockDim.x) bm[t] = 0u;
-    if (threadIdx.x == 0) s_bad = 0u;
-    __syncthreads();
-    for (uint32_t x = cr.x + threadIdx.x; x != cr.y && (x - cr.x) < (cr.y - cr.x); x += blockDim.x) {
-      const uint32_t id = P.c_id[x & P.cmask];
-      if (id < DICT_IDS)
-        atomicOr(&bm[id >> 5], 1u << (id & 31u));
-      else
-        s_bad = 1u;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) P.g_bmok[s] = s_bad ? 0 : 1;
-    __syncthreads();  // s_bad is reset for the next slot
-  }
-}
-
 // Entries no live record names are emptied; a block left empty goes back on the stack (its
 // subject gets a block again with its next record).
 __global__ void k_dict_free(KP P) {
@@ -2698,7 +2668,6 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
 constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per workgroup
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
-static_assert(!BM_ON || AW_WORDS % 4u == 0u, "entry bitmaps are ORed 16 B at a time: keep each wave's LDS 16-B aligned");
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
 __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
@@ -2798,29 +2767,11 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
         const uint32_t o = wave_owner(off, q);
         const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(ws, (int)o, 64), oo = __shfl(off, (int)o, 64);
         uint2 cr = make_uint2(0u, 0u);
-        const uint32_t sl = q < tot ? wo * 32u + kth_set_bit(mo, q - oo) : 0u;
-        if (q < tot) cr = P.g_cref[sl];
+        if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
         const uint32_t len = cr.y - cr.x;
         ent += len;
-        // a big batch with a complete entry bitmap: OR it into the wave's (bw words: plain
-        // read-modify-writes, each lane its own words) instead of one LDS atomic per record
-        const bool viabm = BM_ON && P.g_bm && len >= BM_MIN && 2u * len >= bw && P.g_bmok[sl];
-        for (unsigned long long vb = __ballot(viabm); vb; vb &= vb - 1ull) {
-          const int L = __builtin_ctzll(vb);
-          const uint4* src = reinterpret_cast<const uint4*>(P.g_bm + (size_t)__shfl(sl, L, 64) * DICT_WORDS);
-          for (uint32_t t4 = lane; 4u * t4 < bw; t4 += 64u) {
-            const uint4 v = src[t4];
-            uint4* dst = reinterpret_cast<uint4*>(s_bm) + t4;
-            uint4 o = *dst;
-            o.x |= v.x;
-            o.y |= v.y;
-            o.z |= v.z;
-            o.w |= v.w;
-            *dst = o;
-          }
-        }
         // long ranges (batches): the whole wave walks each, four coalesced records per lane in flight
-        unsigned long long big = __ballot(len >= 64u && !viabm);
+        unsigned long long big = __ballot(len >= 64u);
         while (big) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;

@@ -219,8 +219,9 @@ from oracle_py import OracleCluster
 from swimhip import SwimCluster
 a, b = scenarios.run_pair("lan288_restart_join_loss5", SwimCluster, OracleCluster)
 spills = a.stats()["apply_spills"]
-# a lossy run with few gossips in flight: small receipt sets, which k_gossip_apply pairs
-a2, b2 = scenarios.run_pair("lan256_loss5_crash3", SwimCluster, OracleCluster)
+# a lossy run (one gossip per slot: k_gossip_apply) with more receivers than workgroups and few
+# gossips in flight: small receipt sets, which k_gossip_apply pairs
+a2, b2 = scenarios.run_pair("lan1024_loss5_crash10", SwimCluster, OracleCluster, full_tables=False)
 spills += a2.stats()["apply_spills"]
 import bench
 from swimhip import ClusterConfig
@@ -265,9 +266,7 @@ def test_commit_radix_path_parity():
     chip-wide radix sort (k_rs_hist, k_rs_pass with decoupled look-back, k_rs_commit). At the
     parity sizes only storm phases get there, so a variant built with a 32-gossip LDS sort
     (-DSWIM_CS_SMALL=32) runs the churn scenario and the C3 storm at N = 1,024 through it: bit-exact
-    with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable).
-    The same variant gives every batch slot of >= 8 records an entry bitmap (-DSWIM_BM_MIN=8; the
-    product's 256 is only reached by full-size storms), so apply's whole-bitmap ORs run too."""
+    with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable)."""
     out = _run_variant("libswimhip_cs32.so", _SPILL_SCRIPT)
     radix = int(out.split("RADIX")[-1].split()[0])
     assert radix > 0, "the chip-wide radix sort never ran"
