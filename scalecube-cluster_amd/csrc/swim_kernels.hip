@@ -3473,92 +3473,56 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tot
 // Merge one table into row `obs` (syncMembership, MembershipProtocolImpl.java:463-473),
 // cells in parallel, gossip sequence numbers assigned in cell order by a block scan.
 // `ack_out` (may be null) receives the row after the merge (onSync's SYNC_ACK payload).
-#ifndef SWIM_SYNC_MU
-#define SWIM_SYNC_MU 4
-#endif
-constexpr uint32_t SYNC_MU = SWIM_SYNC_MU;  // quads per thread per step of a dense SYNC merge
 __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint32_t* src, uint32_t* ack_out,
                                           uint32_t attempt, uint32_t reason, uint32_t snap, uint32_t& seq, Tally& T,
-                                          uint32_t& created, uint32_t* lds4, uint32_t* lds_recs) {
+                                          uint32_t& created, uint32_t* lds4) {
   uint32_t* row = P.view + lrow(P, obs) * P.W;
-  const uint32_t nc = ncells(P);
-  if (!P.nxk && (P.W & 3u) == 0u) {
-    // Dense rows, 16-B aligned: each thread takes SYNC_MU consecutive quads (16 cells) per step, all
-    // loads issued together, so a 65,536-cell row is 16 steps (one barrier each) instead of 64.
-    // Cells the incoming record does not override (the common case) never enter updateMembership;
-    // the few that do are applied one by one (their gossip records parked in LDS), and gossips are
-    // numbered in subject order: a thread's cells are consecutive, threads in order.
-    uint32_t* my = lds_recs + 4u * SYNC_MU * threadIdx.x;
-    for (uint32_t c0 = 0; c0 < nc; c0 += 256u * 4u * SYNC_MU) {
-      const uint32_t cb = c0 + 4u * SYNC_MU * threadIdx.x;
-      uint4 s4[SYNC_MU], v4[SYNC_MU];
-#pragma unroll
-      for (uint32_t u = 0; u < SYNC_MU; ++u) {
-        const uint32_t c = cb + 4u * u;
-        s4[u] = c < nc ? *reinterpret_cast<const uint4*>(src + c) : make_uint4(0u, 0u, 0u, 0u);
-        v4[u] = c < nc ? *reinterpret_cast<const uint4*>(row + c) : make_uint4(0u, 0u, 0u, 0u);
-      }
-      uint32_t ovm = 0;  // cells whose incoming record overrides the row's
-#pragma unroll
-      for (uint32_t u = 0; u < SYNC_MU; ++u) {
-        const uint32_t sv[4] = {s4[u].x, s4[u].y, s4[u].z, s4[u].w}, vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k)
-          if (sv[k] != 0u && is_overrides(sv[k], vv[k])) ovm |= 1u << (4u * u + k);
-      }
-      uint32_t recm = 0;  // cells whose update is to be spread
-      for (uint32_t m = ovm; m; m &= m - 1u) {
-        const uint32_t k = (uint32_t)__builtin_ctz(m);
-        const uint32_t rec = apply_record(P, obs, cb + k, src[cb + k], reason, attempt, snap, T);
-        if (rec) {
-          my[k] = rec;
-          recm |= 1u << k;
-        }
-      }
-      if (ack_out) {
-#pragma unroll
-        for (uint32_t u = 0; u < SYNC_MU; ++u) {
-          const uint32_t c = cb + 4u * u;
-          if (c >= nc) continue;
-          const uint4 v = ((ovm >> (4u * u)) & 0xFu) ? *reinterpret_cast<const uint4*>(row + c) : v4[u];
-          *reinterpret_cast<uint4*>(ack_out + c) = v;
-        }
-      }
-      if (__syncthreads_or(recm != 0u)) {  // gossip sequence numbers in subject order
-        uint32_t total;
-        uint32_t o = seq + block_excl_scan256((uint32_t)__popc(recm), &total, lds4);
-        for (uint32_t m = recm; m; m &= m - 1u) {
-          const uint32_t k = (uint32_t)__builtin_ctz(m);
-          emit_gossip(P, obs, cb + k, my[k], o++);
-        }
-        created += total;
-        seq += total;
-      }
-    }
-    return;
-  }
+  // Dense rows: cell = subject, 4 cells per thread (16-B loads) when rows are 16-B aligned.
   // N x K rows: one column per thread, walked in subject order (colorder) so gossip sequence
   // numbers come out exactly as in the dense table; untracked subjects hold BASELINE on both
   // sides, and equal records never override (MembershipProtocolImpl.java:489).
-  for (uint32_t c0 = 0; c0 < nc; c0 += 256u) {
-    const uint32_t c = c0 + threadIdx.x;
-    uint32_t rec = 0, subj = 0;
+  // Cells the incoming record does not override (the common case) never enter updateMembership.
+  const uint32_t nc = ncells(P);
+  const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
+  for (uint32_t c0 = 0; c0 < nc; c0 += 256u * per) {
+    const uint32_t c = c0 + per * threadIdx.x;
+    uint32_t recs[4], cells[4], nrec = 0;
     if (c < nc) {
-      const uint32_t cc = P.nxk ? P.colorder[c] : c;
-      const uint32_t sv = src[cc];
-      uint32_t vv = row[cc];
-      if (sv != 0u && is_overrides(sv, vv)) {
-        subj = subj_of(P, cc);
-        rec = apply_record(P, obs, subj, sv, reason, attempt, snap, T);
-        vv = row[cc];
+      uint32_t sv[4], vv[4], cv[4];
+      if (per == 4u) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(src + c);
+        const uint4 v4 = *reinterpret_cast<const uint4*>(row + c);
+        sv[0] = s4.x, sv[1] = s4.y, sv[2] = s4.z, sv[3] = s4.w;
+        vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+        cv[0] = c, cv[1] = c + 1u, cv[2] = c + 2u, cv[3] = c + 3u;
+      } else {
+        cv[0] = P.nxk ? P.colorder[c] : c;
+        sv[0] = src[cv[0]];
+        vv[0] = row[cv[0]];
       }
-      if (ack_out) ack_out[cc] = vv;
+      for (uint32_t k = 0; k < per; ++k) {
+        if (sv[k] == 0u || !is_overrides(sv[k], vv[k])) continue;
+        const uint32_t subj = subj_of(P, cv[k]);
+        const uint32_t rec = apply_record(P, obs, subj, sv[k], reason, attempt, snap, T);
+        vv[k] = row[cv[k]];
+        if (rec) {
+          recs[nrec] = rec;
+          cells[nrec] = subj;
+          ++nrec;
+        }
+      }
+      if (ack_out) {
+        if (per == 4u)
+          *reinterpret_cast<uint4*>(ack_out + c) = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+        else
+          ack_out[cv[0]] = vv[0];
+      }
     }
-    if (__syncthreads_or(rec != 0u)) {
+    if (__syncthreads_or(nrec != 0u)) {  // gossip sequence numbers in subject order
       uint32_t total;
-      const uint32_t off = block_excl_scan256(rec != 0u ? 1u : 0u, &total, lds4);
-      if (rec) emit_gossip(P, obs, subj, rec, seq + off);
-      created += total;
+      const uint32_t off = block_excl_scan256(nrec, &total, lds4);
+      for (uint32_t k = 0; k < nrec; ++k) emit_gossip(P, obs, cells[k], recs[k], seq + off + k);
+      created += nrec;
       seq += total;
     }
   }
@@ -3570,7 +3534,6 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
-  __shared__ uint32_t s_recs[256 * 4 * SYNC_MU];  // merge_row's spread records, per thread
   const uint32_t j = P.row0 + blockIdx.x;
   if (j >= P.row0 + P.nloc) return;
   uint32_t cntj = P.recv_count[j];
@@ -3607,7 +3570,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
       const uint32_t slot = P.jslot[from];
       src = P.stage_sync + (size_t)slot * P.W;
       ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
-      merge_row(P, j, src, ack, 0x80000000u | from, SWIM_R_SYNC, snap, seq, T, created, s_lds4, s_recs);
+      merge_row(P, j, src, ack, 0x80000000u | from, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
       continue;
     }
     if (is_local(P, from)) {
@@ -3623,7 +3586,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
         P.xsend[g + 1] = j;
       }
     }
-    merge_row(P, j, src, ack, q, SWIM_R_SYNC, snap, seq, T, created, s_lds4, s_recs);
+    merge_row(P, j, src, ack, q, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
   add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * ncells(P) : 0u);
@@ -3635,7 +3598,6 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
 __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
-  __shared__ uint32_t s_recs[256 * 4 * SYNC_MU];  // merge_row's spread records, per thread
   const uint32_t i = P.row0 + blockIdx.x;
   if (i >= P.row0 + P.nloc) return;
   uint32_t kd[3], to[3], n = 0;  // kind 0 / 1: request 2i + kind; kind 2: the initial SYNC's first ack
@@ -3679,7 +3641,7 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
       attempt = (to[k] << 1) | kd[k];
       src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.W + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
     }
-    merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4, s_recs);
+    merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
