@@ -3172,30 +3172,39 @@ __global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
 constexpr uint32_t SW_COLS = 64;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   SWIM_GUARD(P);
-  __shared__ uint32_t s_col[SW_COLS], s_rem[SW_COLS], s_min[SW_COLS];
+  __shared__ uint32_t s_raw[SW_COLS], s_col[SW_COLS], s_rem[SW_COLS], s_min[SW_COLS];
   Tally T;
   uint32_t fired = 0;
-  const uint32_t n = P.ctl->due_count, tid = threadIdx.x;
+  const uint32_t n = P.ctl->due_count, tid = threadIdx.x, lane = tid & 63u;
   const uint32_t nob = (P.nloc + 255u) / 256u, ncb = (n + SW_COLS - 1u) / SW_COLS;
   for (uint32_t u = blockIdx.x; u < nob * ncb; u += gridDim.x) {
     const uint32_t ob = u % nob, c0 = (u / nob) * SW_COLS;  // neighbouring workgroups: neighbouring observers
     const uint32_t nc = min(SW_COLS, n - c0);
     if (tid < nc) {
-      s_col[tid] = P.due[c0 + tid];
+      s_raw[tid] = P.due[c0 + tid];
       s_rem[tid] = 0u;
       s_min[tid] = NONE;
     }
     __syncthreads();
+    if (tid < nc) {  // the chunk's columns in ascending order: a thread's view writes walk its row forward
+      const uint32_t v = s_raw[tid];
+      uint32_t rank = 0;
+      for (uint32_t t = 0; t < nc; ++t) rank += s_raw[t] < v ? 1u : 0u;
+      s_col[rank] = v;
+    }
+    __syncthreads();
     const uint32_t li = ob * 256u + tid;
-    if (li < P.nloc) {
-      const uint32_t i = P.row0 + li;
-      const bool alive = P.alive[i] != 0;
+    {  // every lane of the workgroup runs the loop (observers past nloc read nothing): the per-wave
+       // reductions below see whole waves
+      const bool valid = li < P.nloc;
+      const uint32_t i = P.row0 + (valid ? li : 0u);
+      const bool alive = valid && P.alive[i] != 0;
       uint32_t removed = 0;
       for (uint32_t k0 = 0; k0 < nc; k0 += 4u) {
-        uint32_t v[4];
+        uint32_t v[4], smin[4] = {NONE, NONE, NONE, NONE}, remm = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q)  // four columns' deadlines in flight
-          v[q] = k0 + q < nc ? P.dl[(size_t)s_col[k0 + q] * P.nloc + li] : 0u;
+          v[q] = (valid && k0 + q < nc) ? P.dl[(size_t)s_col[k0 + q] * P.nloc + li] : 0u;
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q) {
           if (!v[q]) continue;
@@ -3206,8 +3215,8 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
             continue;
           }
           const uint32_t dl = v[q] - 1u;
-          if (dl > P.period) {  // still standing: the column's minimum
-            if (dl < s_min[k]) atomicMin(&s_min[k], dl);
+          if (dl > P.period) {  // still standing: the column's minimum (reduced per wave below)
+            smin[q] = dl;
             continue;
           }
           *dp = 0u;
@@ -3228,10 +3237,24 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
           // the counts applied once per observer and once per column
           *cellp = SWIM_ABSENT;
           ++removed;
-          atomicAdd(&s_rem[k], 1u);
+          remm |= 1u << q;  // counted per wave below
           T.accepted++;
           T.removed++;
           push_event(P, i, subj, SWIM_EV_REMOVED, SWIM_R_SUSPICION_TIMEOUT, r0);
+        }
+        // per column: the wave's removals (one LDS add) and standing minimum (one LDS min)
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          const uint32_t k = k0 + q;
+          if (k >= nc) continue;  // (uniform)
+          const uint32_t nrem = (uint32_t)__popcll(__ballot((remm >> q) & 1u));
+          uint32_t mn = smin[q];
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, o, 64));
+          if (lane == 0) {
+            if (nrem) atomicAdd(&s_rem[k], nrem);
+            if (mn != NONE) atomicMin(&s_min[k], mn);
+          }
         }
       }
       if (removed) atomicSub(&P.cnt_delta[i], (int32_t)removed);
