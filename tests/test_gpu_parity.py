@@ -71,6 +71,7 @@ NXK = {
     "local128_partition_heal": 128,
     "local48_links": 48,
     "local24_inbound_blocks": 24,
+    "local64_delay100_loss10": 64,
 }
 
 
