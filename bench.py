@@ -102,13 +102,16 @@ def kernel_bytes(name, d, rounds_per_period=5):
     if name == "k_gossip_pull":  # receiver holds word r/w + receipts word per active window word, one
         return 12 * d["gossip_pull_words"] + 4 * d["gossip_probes"]  # sender window word per probe
     if name == "k_gossip_apply":
-        # per receipt word: receipts r/w (8 B: read, clear), holdings r/w (8), newest/oldest round (1),
-        # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4);
-        # per subject run one ring record (8 B) -- with batch slots the run top's
-        # record range instead (8 B, read in both passes) and 8 B per gossip record it expands;
-        # per subject the table cell and its deadline (8 B)
+        # per receipt word: receipts r/w (8 B: read, clear), holdings r/w (8), newest/oldest round (2),
+        # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4).
+        # One-gossip slots (k_gossip_apply): per subject run one ring record (8 B), per subject the
+        # table cell and its deadline (8 B). Batch slots (k_gossip_apply_b):
+        # per run top its record range (8 B), per record its dictionary entry id (4 B), per merged
+        # subject block the entry's record, the block's subject and the table cell (12 B)
         recs = d.get("apply_records", 0)
-        return 93 * d["apply_words"] + (16 if recs else 8) * d["apply_runs"] + 8 * recs + 8 * d["apply_subjects"]
+        if recs:
+            return 93 * d["apply_words"] + 8 * d["apply_runs"] + 4 * recs + 12 * d["apply_subjects"]
+        return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
     if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write and
         return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"]  # the view cell read + write
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
