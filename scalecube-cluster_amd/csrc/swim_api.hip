@@ -486,7 +486,12 @@ int period_resume(swim_handle* h, swim_xchg* x) {
                                h->n_in_pairs);
         }
         timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
-        timed(h, 1, "k_gossip_pull", [&] { hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 1, "k_gossip_pull", [&] {
+          if (P.dq)
+            hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+          else
+            hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+        });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
           if (P.batched)  // batch slots in the ring: expand their records

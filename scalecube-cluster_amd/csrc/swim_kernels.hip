@@ -2023,7 +2023,10 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 #ifndef SWIM_PULL_WAVES
 #define SWIM_PULL_WAVES 1
 #endif
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
+// DQ: this handle has delayed-message rings. The delay paths get an instance of
+// their own, so the common one keeps its registers (4 waves per SIMD instead of 3).
+template <bool DQ>
+__device__ __forceinline__ void pull_body(const KP& P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
@@ -2039,14 +2042,14 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   uint32_t* sum = s_sum[threadIdx.x >> 6];
   const uint32_t nsw = (n_act + 31u) >> 5;
-  if ((deg || P.dq) && P.alive[p] && n_act) {  // a stopped transport loses every message
+  if ((deg || DQ) && P.alive[p] && n_act) {  // a stopped transport loses every message
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
-    if (P.dq && lane == 0)  // where this round's pushes start (dq_window)
+    if (DQ && lane == 0)  // where this round's pushes start (dq_window)
       P.dq_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.dq_head[p];
     // (with delays every message needs its draw, held gossip or not: no skipping)
     const uint32_t* lackr =
-        (!P.delay_on && nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
+        (!(DQ && P.delay_on) && nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
     if (nsw <= NSUM)
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
@@ -2129,7 +2132,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
           prev[i] = 0u;
           if (wcv[i] == WC_NONE) continue;
           ++words;
-          if (!P.delay_on && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
+          if (!(DQ && P.delay_on) && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
           todo |= 1u << i;
           anyall |= wcv[i] == WC_ALL ? 1u : 0u;
           anymix |= wcv[i] == WC_MIXED ? 1u : 0u;
@@ -2184,7 +2187,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
               ++probes;
               if (!((reach >> (q0 + j)) & 1ull)) continue;
               uint32_t cand = win & ~hw[i] & ~u[i] & ~prev[i];
-              if (P.delay_on) {  // evaluateLoss + evaluateDelay per message, held gossip or not (§3.16)
+              if (DQ && P.delay_on) {  // evaluateLoss + evaluateDelay per message, held gossip or not (§3.16)
                 cand = 0u;
                 for (uint32_t need = win; need; need &= need - 1u) {
                   const uint32_t b = (uint32_t)__builtin_ctz(need);
@@ -2223,7 +2226,7 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
 
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
     }
-    if (P.dq) {  // delayed messages arriving this round (after the senders' plain nb stores)
+    if (DQ) {  // delayed messages arriving this round (after the senders' plain nb stores)
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       uint32_t q0, q1;
       dq_window(P, p, &q0, &q1);
@@ -2262,6 +2265,9 @@ __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
   add_stat(P, ST_G_PROBES, probes);  // (receipts are counted by k_gossip_apply, in gossips)
   add_stat(P, ST_G_PULLW, words);
 }
+
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true>(P); }
 
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
