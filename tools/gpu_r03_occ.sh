@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${1:-r03occ}
 mkdir -p $out
-for v in base product sw6 sw7b1; do
+for v in ${OCC_VARIANTS:-base product sw6 sw7b1}; do
   lib=variants_ab/libswimhip_$v.so; [ $v = product ] && lib=scalecube-cluster_amd/swimhip/libswimhip.so
   SWIMHIP_LIB=$lib timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --converge 0 \
     --no-cpu-baseline > $out/c3_$v.json 2> $out/c3_$v.err
