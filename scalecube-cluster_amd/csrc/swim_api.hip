@@ -247,6 +247,8 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
     h->base.batched = 1u;
     h->cur.batched = 1u;
     P.batched = 1u;
+    // the live one-gossip slots committed before get their counts too (slot_gossips reads them)
+    hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P, 1u);
   }
   CSort C{h->ck[0], h->cv[0], h->ck[1], h->cv[1], h->cs_ghist, h->cs_ctr, h->cs_stat, h->cs_maxt, 0u, 0u};
   // key = subject << 32 | record (user gossips: subject N + origin) or origin << 32 | subject
@@ -274,7 +276,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
       hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n, C);
     }
     // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights)
-    if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P);
+    if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P, 0u);
     // the record dictionary of the batched apply: every commit while batching is
     // enabled, so records committed before the first batch have their entries too
     if (h->dict_on) {
@@ -842,6 +844,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.d_free, DICT_SIDS);
   }
   ALLOC(P.wsum, h->GC / 32);
+  ALLOC(P.scnt, h->GC);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
   ALLOC(P.nsum, NL * NSUM);
@@ -998,6 +1001,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_cref, 0, (size_t)h->GC * 8, s);
   (void)hipMemsetAsync(P.wsum, 0, (size_t)(h->GC / 32) * 4, s);
+  (void)hipMemsetAsync(P.scnt, 0, (size_t)h->GC * 2, s);
   (void)hipMemsetAsync(P.held, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_head, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.ih_rhead, 0, NL * 256 * 4, s);

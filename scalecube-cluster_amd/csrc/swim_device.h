@@ -216,6 +216,8 @@ struct KP {
   uint32_t* c_hash;   // [CC] its canonical id hash (GossipProtocolImpl.generateGossipId, :211-213)
   uint32_t cmask;     // CC - 1
   uint32_t* wsum;     // [GC/32] gossips in a word's slots (counters weight a slot by its gossips)
+  uint16_t* scnt;     // [GC] gossips of each slot (SCNT_SAT: that many or more, read g_cref), by word: a
+                      // window's count is 4 x 16-B loads and masked adds, not one g_cref load per slot
   uint32_t batch_commit;  // this phase's commit groups gossips into batches by origin (loss_mode != 1)
   uint32_t batched;       // batching is on and has been used: counters weight slots, apply expands records
   uint32_t trace;         // swim_trace mask: SWIM_TRACE_FD puts FailureDetectorEvents into the event ring
@@ -417,15 +419,37 @@ __device__ __forceinline__ uint32_t ncells(const KP& P) {
 // gossips in the slots `bits` of bitmap word ws (GossipRequest / receipt counters count gossips,
 // not slots): popcount while every slot holds one gossip, else the word's total when the mask
 // covers it, else the slots' record ranges one by one
+// scnt saturates here (a test build lowers it so the exact fallback runs)
+#ifndef SWIM_SCNT_SAT
+#define SWIM_SCNT_SAT 0xFFFF
+#endif
+constexpr uint32_t SCNT_SAT = SWIM_SCNT_SAT;
+static_assert(SCNT_SAT >= 1u && SCNT_SAT <= 0xFFFFu, "SWIM_SCNT_SAT: 1 .. 65535");
 __device__ __forceinline__ uint32_t slot_gossips(const KP& P, uint32_t ws, uint32_t bits) {
   if (!P.batched || !bits) return (uint32_t)__popc(bits);
   if (bits == 0xFFFFFFFFu) return P.wsum[ws];
-  uint32_t n = 0;
-  while (bits) {
-    const uint32_t b = (uint32_t)__builtin_ctz(bits);
-    bits &= bits - 1u;
+  const uint4* cp = reinterpret_cast<const uint4*>(P.scnt + (size_t)ws * 32u);
+  const uint4 c0 = cp[0], c1 = cp[1], c2 = cp[2], c3 = cp[3];  // all in flight together
+  const uint32_t cw[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                           c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+  uint32_t n = 0, big = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 16u; ++q) {
+    const uint32_t lo = cw[q] & 0xFFFFu, hi = cw[q] >> 16;
+    if ((bits >> (2u * q)) & 1u) {
+      n += lo;
+      big |= (lo == SCNT_SAT ? 1u : 0u) << (2u * q);
+    }
+    if ((bits >> (2u * q + 1u)) & 1u) {
+      n += hi;
+      big |= (hi == SCNT_SAT ? 1u : 0u) << (2u * q + 1u);
+    }
+  }
+  while (big) {  // slots of SCNT_SAT gossips or more (a SYNC merge of a huge table): their exact count
+    const uint32_t b = (uint32_t)__builtin_ctz(big);
+    big &= big - 1u;
     const uint2 r = P.g_cref[ws * 32u + b];
-    n += r.y - r.x;
+    n += (r.y - r.x) - SCNT_SAT;
   }
   return n;
 }

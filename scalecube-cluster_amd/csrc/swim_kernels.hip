@@ -595,20 +595,27 @@ __global__ void k_multi_live(KP P, uint32_t* out) {
   }
 }
 
-// Gossips per bitmap word (wsum) of the words the last commit wrote slots into
-__global__ void k_commit_wsum(KP P) {
-  const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount;
+// Gossips per bitmap word (wsum) and per slot (scnt) of the words the last commit wrote slots into,
+// or (all) of every word that may be live (batch slots start: the words committed before them)
+__global__ void k_commit_wsum(KP P, uint32_t all) {
+  const uint32_t g1 = P.ctl->gcount;
+  const uint32_t g0 = all ? (g1 - P.ctl->glo > P.GC ? g1 - P.GC : P.ctl->glo) : P.ctl->g_prev;
   const uint32_t w0 = g0 >> 5, w1 = (g1 + 31u) >> 5;
   const uint32_t* cref = reinterpret_cast<const uint32_t*>(P.g_cref);
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += gridDim.x * blockDim.x) {
     uint32_t sum = 0;
+    const uint32_t ws = w & ((P.GC >> 5) - 1u);
     for (uint32_t b = 0; b < 32u; ++b) {
       const uint32_t id = (w << 5) + b;
-      if ((int32_t)(g1 - id) <= 0) continue;  // not created yet (the word's slots from earlier commits count)
-      const uint32_t s = id & P.gmask;
-      sum += cref[2u * s + 1u] - cref[2u * s];
+      uint32_t c = 0;
+      if ((int32_t)(g1 - id) > 0) {  // created (the word's slots from earlier commits count)
+        const uint32_t s = id & P.gmask;
+        c = cref[2u * s + 1u] - cref[2u * s];
+      }
+      sum += c;
+      P.scnt[ws * 32u + b] = (uint16_t)(c < SCNT_SAT ? c : SCNT_SAT);
     }
-    P.wsum[w & ((P.GC >> 5) - 1u)] = sum;
+    P.wsum[ws] = sum;
   }
 }
 
