@@ -2680,10 +2680,17 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 #endif
 constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
 constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per workgroup
+#ifndef SWIM_AW_ILP
+#define SWIM_AW_ILP 4
+#endif
+constexpr uint32_t AW_ILP = SWIM_AW_ILP;          // record-entry loads in flight per lane
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
-__global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
+#ifndef SWIM_AW_MINW
+#define SWIM_AW_MINW 1
+#endif
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(KP P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -2789,15 +2796,15 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
           const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
-          for (uint32_t x0 = b0; x0 != b1; x0 += min(256u, b1 - x0)) {
-            uint32_t id[4];
+          for (uint32_t x0 = b0; x0 != b1; x0 += min(64u * AW_ILP, b1 - x0)) {
+            uint32_t id[AW_ILP];
 #pragma unroll
-            for (uint32_t u = 0; u < 4u; ++u) {
+            for (uint32_t u = 0; u < AW_ILP; ++u) {
               const uint32_t x = x0 + 64u * u + lane;
               id[u] = (x - b0) < (b1 - b0) ? P.c_id[x & P.cmask] : DICT_IDS;
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 4u; ++u) {
+            for (uint32_t u = 0; u < AW_ILP; ++u) {
               const uint32_t x = x0 + 64u * u + lane;
               if ((x - b0) < (b1 - b0)) record(x, id[u]);
             }
@@ -2806,10 +2813,10 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
         // short ranges (single gossips, small batches): flattened across the lanes
         uint32_t etot;
         const uint32_t eoff = wave_excl_scan(len < 64u ? len : 0u, &etot);
-        for (uint32_t e0 = 0; e0 < etot; e0 += 256u) {
-          uint32_t xs[4], id[4];
+        for (uint32_t e0 = 0; e0 < etot; e0 += 64u * AW_ILP) {
+          uint32_t xs[AW_ILP], id[AW_ILP];
 #pragma unroll
-          for (uint32_t u = 0; u < 4u; ++u) {
+          for (uint32_t u = 0; u < AW_ILP; ++u) {
             const uint32_t ee = e0 + 64u * u + lane;
             const uint32_t eo = wave_owner(eoff, ee);
             const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
@@ -2817,7 +2824,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES) k_gossip_apply_b(KP P) {
             id[u] = ee < etot ? P.c_id[xs[u] & P.cmask] : DICT_IDS;
           }
 #pragma unroll
-          for (uint32_t u = 0; u < 4u; ++u)
+          for (uint32_t u = 0; u < AW_ILP; ++u)
             if (e0 + 64u * u + lane < etot) record(xs[u], id[u]);
         }
       }
