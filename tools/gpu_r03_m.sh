@@ -7,4 +7,4 @@ mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread \
   > $out/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $out/status.log; [ $rc -le 1 ] || exit $rc
-OCC_VARIANTS="product sw5 nosg" bash tools/gpu_r03_occ.sh ${1:-r03m}/ab
+OCC_VARIANTS="product sw5 ilp8 nosg" bash tools/gpu_r03_occ.sh ${1:-r03m}/ab
