@@ -2862,40 +2862,56 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         ++created;
       }
     };
-    // per block with set entries: the max of its set entries' records, merged once (bitmap words
-    // cleared on the way; four words per lane loaded together)
-    for (uint32_t t0 = 0; t0 < bw; t0 += 256u) {
-      uint32_t wd[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4u; ++u) {
-        const uint32_t t = t0 + 64u * u + lane;
-        wd[u] = t < bw ? s_bm[t] : 0u;
-        if (wd[u]) s_bm[t] = 0u;
+    auto merge = [&](uint32_t subj, uint32_t best) {
+      if (via_inbox) {
+        spill(subj, best);
+      } else {
+        const uint32_t c = cell_get(P, p, subj);
+        if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
+          apply(subj, best);
+        else
+          ++nsubj;
       }
+    };
+    // per block with set entries: the max of its set entries' records, merged once. The blocks
+    // with set bits of 512 bitmap words are flattened across the wave (one block per lane: its
+    // eight entry records in two 16-B loads beside its subject), then the words are cleared.
+    static_assert(DICT_WAYS == 8, "a bitmap byte per block");
+    for (uint32_t t0 = 0; t0 < bw; t0 += 512u) {
+      uint32_t bm = 0u;  // bit 4u + j: word t0 + 64u + lane has set entries in its block j
 #pragma unroll
-      for (uint32_t u = 0; u < 4u; ++u) {
-        while (wd[u]) {
-          const uint32_t sh = (uint32_t)__builtin_ctz(wd[u]) & ~(DICT_WAYS - 1u);  // the block's first bit
-          uint32_t m = (wd[u] >> sh) & ((1u << DICT_WAYS) - 1u);
-          wd[u] &= ~(((1u << DICT_WAYS) - 1u) << sh);
-          const uint32_t base = 32u * (t0 + 64u * u + lane) + sh;  // entry id of the block's way 0
-          uint32_t best = 0u;
-          while (m) {
-            best = max(best, P.d_rec[base + (uint32_t)__builtin_ctz(m)]);
-            m &= m - 1u;
-          }
+      for (uint32_t u = 0; u < 8u; ++u) {
+        const uint32_t t = t0 + 64u * u + lane;
+        const uint32_t w = t < bw ? s_bm[t] : 0u;
+        const uint32_t nz = (uint32_t)((w & 0xFFu) != 0u) | ((uint32_t)((w & 0xFF00u) != 0u) << 1) |
+                            ((uint32_t)((w & 0xFF0000u) != 0u) << 2) | ((uint32_t)((w >> 24) != 0u) << 3);
+        bm |= nz << (4u * u);
+      }
+      uint32_t tot;
+      const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
+      for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
+        const uint32_t q = q0 + lane;
+        const uint32_t o = wave_owner(off, q);
+        const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
+        if (q < tot) {
+          const uint32_t b = kth_set_bit(bo, q - oo);
+          const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
+          const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
+          const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
+          const uint4 r0 = dr[0], r1 = dr[1];
           const uint32_t subj = P.d_subj[base / DICT_WAYS];
-          if (via_inbox) {
-            spill(subj, best);
-          } else {
-            const uint32_t c = cell_get(P, p, subj);
-            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
-              apply(subj, best);
-            else
-              ++nsubj;
-          }
+          const uint32_t m = (s_bm[t] >> (8u * j)) & 0xFFu;
+          uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
+                              max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
+          best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
+                               max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
+          merge(subj, best);
         }
       }
+      wsync();  // every lane has read its blocks' bits
+#pragma unroll
+      for (uint32_t u = 0; u < 8u; ++u)
+        if ((bm >> (4u * u)) & 0xFu) s_bm[t0 + 64u * u + lane] = 0u;
     }
     wsync();
     APPLYB_MARK(2);
