@@ -2774,6 +2774,10 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         if ((bits & 0xFFFFu) && (prior & 0xFFFFu)) v0 = dp[0];
         if ((bits >> 16) && (prior >> 16)) v1 = dp[1];
         receive_word(P, p, ws, bits, prior, v0, v1);
+#ifdef SWIM_APPLY_PROF
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 14, bits == ~0u ? 1ull : 0ull);
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 15, 1ull);
+#endif
         nbr[kv] = 0u;  // nb is all-zero between rounds
         ++nwords;
         rm = run_tops(bits, rs);
@@ -2790,6 +2794,16 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
         const uint32_t len = cr.y - cr.x;
         ent += len;
+#ifdef SWIM_APPLY_PROF  // receipt words received whole, and the records they carry: dbg_log u64 [12..15]
+        {
+          const bool fw = __shfl((uint32_t)(bits == ~0u), (int)o, 64) != 0u;
+          const unsigned long long rf = wave_sum(fw && q < tot ? len : 0u), ra = wave_sum(q < tot ? len : 0u);
+          if (lane == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 12, rf);
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 13, ra);
+          }
+        }
+#endif
         // long ranges (batches): the whole wave walks each, four coalesced records per lane in flight
         unsigned long long big = __ballot(len >= 64u);
         while (big) {

@@ -21,7 +21,10 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $out/c3.json 2> $ou
   && echo "c3 prof ok" >> $out/status.log \
   && timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $out/l2 -o run -- \
        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --converge 0 > $out/l2_bench.json 2> $out/l2_bench.err \
-  && echo "l2 ok" >> $out/status.log
+  && echo "l2 ok" >> $out/status.log \
+  && SWIMHIP_LIB=variants_ab/libswimhip_aprof.so timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --converge 0 \
+       --no-cpu-baseline > $out/aprof.json 2> $out/aprof.err \
+  && echo "aprof ok" >> $out/status.log
 rc=$?
 echo "rc=$rc" >> $out/status.log
 exit $rc
