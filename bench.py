@@ -248,7 +248,14 @@ def _oracle_run(args):
     dt = time.perf_counter() - t0
     receipts = c.stats()["gossip_first_receipts"] - r0
     c.close()
-    return n, done, dt, receipts
+    import resource
+
+    return n, done, dt, receipts, resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+
+
+# host memory the CPU replicas may hold together (the box caps one command at 270 GiB; the bench's own
+# process holds the GPU handle beside them)
+CPU_MEM_BUDGET = 128 << 30
 
 
 def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
@@ -260,9 +267,13 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
     aggregate; the single-thread rate is reported beside it."""
     import multiprocessing as mp
 
-    n, done, dt, rcpt = _oracle_run((workload, warmup, seed, max_periods, budget_s))
+    # the single-thread sample in a child of its own, so that its peak resident set is the oracle's
+    with mp.get_context("spawn").Pool(1) as pool:
+        n, done, dt, rcpt, rss = pool.apply(_oracle_run, ((workload, warmup, seed, max_periods, budget_s),))
     single = n * done / dt
-    cores = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU is 16
+    # the box's CPU share for one GPU is 16; a lossy storm's oracle state grows by GBs per period
+    # (C2: ~36 GB per replica after 20 periods), so the replicas are also bounded by host memory
+    cores = max(1, min(16, os.cpu_count() or 1, CPU_MEM_BUDGET // max(1, int(rss * 1.25))))
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(cores) as pool:
         res = pool.map(_oracle_run, [(workload, warmup, seed + k, done, None) for k in range(cores)])
@@ -272,6 +283,7 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
     w = WORKLOADS[workload]
     return {"value": agg, "unit": "member-periods/s", "cores": cores, "kind": "port",
             "single_thread": {"value": single, "cores": 1, "periods": done, "seconds": round(dt, 2),
+                              "peak_rss_gb": round(rss / 2**30, 2),
                               "gossip_first_receipts_per_s": rcpt / dt},
             "gossip_first_receipts_per_s": sum(r[3] for r in res) / max(r[2] for r in res),
             "sample": f"oracle (C++ restatement of the reference's per-member logic) on the same schedule at {n} of "
