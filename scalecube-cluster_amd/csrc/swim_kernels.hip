@@ -2684,6 +2684,10 @@ constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per wor
 #define SWIM_AW_ILP 4
 #endif
 constexpr uint32_t AW_ILP = SWIM_AW_ILP;          // record-entry loads in flight per lane
+#ifndef SWIM_AW_VILP
+#define SWIM_AW_VILP 2
+#endif
+constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flight per lane (long ranges)
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
@@ -2794,11 +2798,13 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
         const uint32_t len = cr.y - cr.x;
         ent += len;
-#ifdef SWIM_APPLY_PROF  // receipt words received whole, and the records they carry: dbg_log u64 [12..15]
+#ifdef SWIM_APPLY_PROF  // receipt words received whole, and the records they carry: dbg_log u64 [12..16]
         {
           const bool fw = __shfl((uint32_t)(bits == ~0u), (int)o, 64) != 0u;
           const unsigned long long rf = wave_sum(fw && q < tot ? len : 0u), ra = wave_sum(q < tot ? len : 0u);
+          const unsigned long long rl = wave_sum(q < tot && len >= 64u ? len : 0u);
           if (lane == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 16, rl);
             atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 12, rf);
             atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 13, ra);
           }
@@ -2810,6 +2816,27 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
           const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
+#ifndef SWIM_AW_SCALAR
+          // aligned 16-B quads of entry ids from the quad holding b0: 4 records per lane per load
+          const uint32_t a0 = b0 & ~3u, span = b1 - a0;
+          for (uint32_t x0 = 0; x0 < span; x0 += 256u * AW_VILP) {
+            uint4 v[AW_VILP];
+#pragma unroll
+            for (uint32_t u = 0; u < AW_VILP; ++u) {
+              const uint32_t d = x0 + 256u * u + 4u * lane;
+              v[u] = d < span ? *reinterpret_cast<const uint4*>(P.c_id + ((a0 + d) & P.cmask))
+                              : make_uint4(DICT_IDS, DICT_IDS, DICT_IDS, DICT_IDS);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < AW_VILP; ++u) {
+              const uint32_t x = a0 + x0 + 256u * u + 4u * lane;
+              const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+              for (uint32_t k = 0; k < 4u; ++k)
+                if ((x + k - b0) < (b1 - b0)) record(x + k, ids[k]);
+            }
+          }
+#else
           for (uint32_t x0 = b0; x0 != b1; x0 += min(64u * AW_ILP, b1 - x0)) {
             uint32_t id[AW_ILP];
 #pragma unroll
@@ -2823,6 +2850,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
               if ((x - b0) < (b1 - b0)) record(x, id[u]);
             }
           }
+#endif
         }
         // short ranges (single gossips, small batches): flattened across the lanes
         uint32_t etot;
