@@ -2688,6 +2688,10 @@ constexpr uint32_t AW_ILP = SWIM_AW_ILP;          // record-entry loads in fligh
 #define SWIM_AW_VILP 2
 #endif
 constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flight per lane (long ranges)
+#ifndef SWIM_AW_MILP
+#define SWIM_AW_MILP 1
+#endif
+constexpr uint32_t AW_MILP = SWIM_AW_MILP;        // dictionary blocks merged per lane per step
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
@@ -2904,17 +2908,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         ++created;
       }
     };
-    auto merge = [&](uint32_t subj, uint32_t best) {
-      if (via_inbox) {
-        spill(subj, best);
-      } else {
-        const uint32_t c = cell_get(P, p, subj);
-        if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
-          apply(subj, best);
-        else
-          ++nsubj;
-      }
-    };
     // per block with set entries: the max of its set entries' records, merged once. The blocks
     // with set bits of 512 bitmap words are flattened across the wave (one block per lane: its
     // eight entry records in two 16-B loads beside its subject), then the words are cleared.
@@ -2931,6 +2924,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
       }
       uint32_t tot;
       const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
+#if SWIM_AW_MILP == 1
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
         const uint32_t o = wave_owner(off, q);
@@ -2947,9 +2941,63 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
                               max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
           best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
                                max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
-          merge(subj, best);
+          if (via_inbox) {
+            spill(subj, best);
+          } else {
+            const uint32_t c = cell_get(P, p, subj);
+            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
+              apply(subj, best);
+            else
+              ++nsubj;
+          }
         }
       }
+#else
+      // AW_MILP blocks per lane per step: their entry loads, then their cells, then the merges
+      // (one block per subject, so a merge never changes another block's cell)
+      for (uint32_t q0 = 0; q0 < tot; q0 += 64u * AW_MILP) {
+        uint32_t subj[AW_MILP], best[AW_MILP], cv[AW_MILP];
+        uint4 r0[AW_MILP], r1[AW_MILP];
+        uint32_t mm[AW_MILP];
+#pragma unroll
+        for (uint32_t i = 0; i < AW_MILP; ++i) {
+          const uint32_t q = q0 + 64u * i + lane;
+          const uint32_t o = wave_owner(off, q);
+          const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
+          mm[i] = 0u;
+          subj[i] = 0u;
+          if (q < tot) {
+            const uint32_t b = kth_set_bit(bo, q - oo);
+            const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
+            const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
+            const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
+            r0[i] = dr[0];
+            r1[i] = dr[1];
+            subj[i] = P.d_subj[base / DICT_WAYS];
+            mm[i] = (s_bm[t] >> (8u * j)) & 0xFFu;  // nonzero: the block has set entries
+          }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < AW_MILP; ++i) {
+          const uint32_t m = mm[i];
+          best[i] = max(max(max((m & 1u) ? r0[i].x : 0u, (m & 2u) ? r0[i].y : 0u),
+                            max((m & 4u) ? r0[i].z : 0u, (m & 8u) ? r0[i].w : 0u)),
+                        max(max((m & 16u) ? r1[i].x : 0u, (m & 32u) ? r1[i].y : 0u),
+                            max((m & 64u) ? r1[i].z : 0u, (m & 128u) ? r1[i].w : 0u)));
+          cv[i] = (m && !via_inbox) ? cell_get(P, p, subj[i]) : 0u;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < AW_MILP; ++i) {
+          if (!mm[i]) continue;
+          if (via_inbox)
+            spill(subj[i], best[i]);
+          else if (is_overrides(best[i], cv[i]) || (P.nxk && P.colmap[subj[i]] == NONE))  // (the latter: OV_TRACK)
+            apply(subj[i], best[i]);
+          else
+            ++nsubj;
+        }
+      }
+#endif
       wsync();  // every lane has read its blocks' bits
 #pragma unroll
       for (uint32_t u = 0; u < 8u; ++u)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3: the whole -m gpu suite with 16-B entry-id loads over long record ranges in the batched
-# apply, its A/B on C3 20/5 (per-lane 4-B loads: scal; four 16-B loads in flight: vilp4), and the
+# apply, its A/B on C3 20/5 (per-lane 4-B loads: scal; four 16-B loads in flight: vilp4; two dictionary blocks per lane per merge step: milp2), and the
 # apply phase profile (records in long ranges).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${1:-r03q}
@@ -8,7 +8,7 @@ mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread \
   > $out/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $out/status.log; [ $rc -le 1 ] || exit $rc
-OCC_VARIANTS="product scal vilp4" bash tools/gpu_r03_occ.sh ${1:-r03q}/ab || exit $?
+OCC_VARIANTS="product scal vilp4 milp2" bash tools/gpu_r03_occ.sh ${1:-r03q}/ab || exit $?
 SWIMHIP_LIB=variants_ab/libswimhip_aprof.so timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --converge 0 \
   --no-cpu-baseline > $out/aprof.json 2> $out/aprof.err
 rc=$?; echo "aprof rc=$rc" >> $out/status.log; exit $rc
