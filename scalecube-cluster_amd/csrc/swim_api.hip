@@ -1053,11 +1053,13 @@ int swim_destroy(swim_handle* h) {
       std::fprintf(stderr, "apply_b phases (wave-ms): bitmap init %.1f words+records %.1f merge %.1f spill %.1f\n",
                    ph[4] / 1e5, ph[5] / 1e5, ph[6] / 1e5, ph[7] / 1e5);
     }
-    unsigned long long fw[17] = {};
+    unsigned long long fw[20] = {};
     if (hipMemcpy(fw, h->base.dbg_log, sizeof fw, hipMemcpyDeviceToHost) == hipSuccess)
       std::fprintf(stderr, "apply_b receipt words received whole %llu of %llu; their records %llu of %llu\n", fw[14],
                    fw[15], fw[12], fw[13]);
     std::fprintf(stderr, "apply_b records in ranges of >= 64 records: %llu\n", fw[16]);
+    std::fprintf(stderr, "apply_b words+records split (wave-ms): words %.1f long ranges %.1f short ranges %.1f\n",
+                 fw[17] / 1e5, fw[18] / 1e5, fw[19] / 1e5);
   }
 #endif
   free_all(h);

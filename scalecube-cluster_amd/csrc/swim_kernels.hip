@@ -2727,6 +2727,17 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
 #define APPLYB_MARK(q)
 #endif
   for (uint32_t t = lane; t < bw; t += 64u) s_bm[t] = 0u;
+#ifdef SWIM_APPLY_PROF
+  unsigned long long t_w = 0, t_big = 0, t_short = 0, tq = 0;  // words / long ranges / short ranges
+#define APPLYB_SUB(acc)                \
+  {                                    \
+    const unsigned long long tn = wall_clock64(); \
+    acc += tn - tq;                    \
+    tq = tn;                           \
+  }
+#else
+#define APPLYB_SUB(acc)
+#endif
   APPLYB_MARK(0);
   for (uint32_t li = blockIdx.x * AW_WAVES + wv; li < n_list; li += gridDim.x * AW_WAVES) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
@@ -2770,6 +2781,9 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
     // one receipt word per lane (kv = its active-list position, or NONE): holdings, infection
     // rounds and age bounds, then the records of its run tops, flattened across the wave
     auto word = [&](uint32_t kv) {
+#ifdef SWIM_APPLY_PROF
+      tq = wall_clock64();
+#endif
       const uint32_t e = kv != NONE ? P.act[kv] : 0u;
       const uint32_t bits = (kv != NONE && ((e >> 26) & 3u) != WC_NONE) ? nbr[kv] : 0u;
       const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
@@ -2802,6 +2816,9 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
         const uint32_t len = cr.y - cr.x;
         ent += len;
+#ifdef SWIM_APPLY_PROF
+        if (__any(len != 0u)) APPLYB_SUB(t_w);
+#endif
 #ifdef SWIM_APPLY_PROF  // receipt words received whole, and the records they carry: dbg_log u64 [12..16]
         {
           const bool fw = __shfl((uint32_t)(bits == ~0u), (int)o, 64) != 0u;
@@ -2856,6 +2873,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
           }
 #endif
         }
+        APPLYB_SUB(t_big);
         // short ranges (single gossips, small batches): flattened across the lanes
         uint32_t etot;
         const uint32_t eoff = wave_excl_scan(len < 64u ? len : 0u, &etot);
@@ -2873,6 +2891,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
           for (uint32_t u = 0; u < AW_ILP; ++u)
             if (e0 + 64u * u + lane < etot) record(xs[u], id[u]);
         }
+        APPLYB_SUB(t_short);
       }
     };
     if (!summ) {
@@ -3030,6 +3049,13 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
   add_stat(P, ST_APPLY_SPILL, nspills);
   add_stat(P, ST_APPLY_RECS, nrecs);
   add_stat(P, ST_GOSSIP_RECEIPTS, nrcpt);
+#ifdef SWIM_APPLY_PROF
+  if (lane == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 17, t_w);
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 18, t_big);
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 19, t_short);
+  }
+#endif
   flush_tally(P, T);
 }
 
