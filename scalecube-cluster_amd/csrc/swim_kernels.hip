@@ -2875,6 +2875,22 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         }
         APPLYB_SUB(t_big);
         // short ranges (single gossips, small batches): flattened across the lanes
+#ifdef SWIM_AW_SHORT_LANE  // (A/B: each lane walks its own short range)
+        {
+          const uint32_t s0 = len < 64u ? cr.x : 0u, sl = len < 64u ? len : 0u;
+          for (uint32_t d0 = 0; __any(d0 < sl); d0 += AW_ILP) {
+            uint32_t id[AW_ILP];
+#pragma unroll
+            for (uint32_t u = 0; u < AW_ILP; ++u) id[u] = d0 + u < sl ? P.c_id[(s0 + d0 + u) & P.cmask] : DICT_IDS;
+#pragma unroll
+            for (uint32_t u = 0; u < AW_ILP; ++u)
+              if (d0 + u < sl) record(s0 + d0 + u, id[u]);
+          }
+        }
+        if (false) {
+#else
+        {
+#endif
         uint32_t etot;
         const uint32_t eoff = wave_excl_scan(len < 64u ? len : 0u, &etot);
         for (uint32_t e0 = 0; e0 < etot; e0 += 64u * AW_ILP) {
@@ -2890,6 +2906,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
 #pragma unroll
           for (uint32_t u = 0; u < AW_ILP; ++u)
             if (e0 + 64u * u + lane < etot) record(xs[u], id[u]);
+        }
         }
         APPLYB_SUB(t_short);
       }
