@@ -2688,6 +2688,10 @@ constexpr uint32_t AW_ILP = SWIM_AW_ILP;          // record-entry loads in fligh
 #define SWIM_AW_VILP 2
 #endif
 constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flight per lane (long ranges)
+#ifndef SWIM_AW_QILP
+#define SWIM_AW_QILP 2
+#endif
+constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
 #ifndef SWIM_AW_MILP
 #define SWIM_AW_MILP 1
 #endif
@@ -2874,17 +2878,34 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
 #endif
         }
         APPLYB_SUB(t_big);
-        // short ranges (single gossips, small batches): flattened across the lanes
-#ifdef SWIM_AW_SHORT_LANE  // (A/B: each lane walks its own short range)
+        // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
+        // flattened across the lanes, one quad per lane per load (one owner search per quad)
+#ifndef SWIM_AW_SHORT_REC
         {
-          const uint32_t s0 = len < 64u ? cr.x : 0u, sl = len < 64u ? len : 0u;
-          for (uint32_t d0 = 0; __any(d0 < sl); d0 += AW_ILP) {
-            uint32_t id[AW_ILP];
+          const bool sh = len != 0u && len < 64u;
+          const uint32_t nq = sh ? ((cr.x & 3u) + len + 3u) >> 2 : 0u;
+          uint32_t qtot;
+          const uint32_t qoff = wave_excl_scan(nq, &qtot);
+          for (uint32_t e0 = 0; e0 < qtot; e0 += 64u * AW_QILP) {
+            uint4 v[AW_QILP];
+            uint32_t qb[AW_QILP], bx[AW_QILP], bl[AW_QILP];
 #pragma unroll
-            for (uint32_t u = 0; u < AW_ILP; ++u) id[u] = d0 + u < sl ? P.c_id[(s0 + d0 + u) & P.cmask] : DICT_IDS;
+            for (uint32_t u = 0; u < AW_QILP; ++u) {
+              const uint32_t ee = e0 + 64u * u + lane;
+              const uint32_t eo = wave_owner(qoff, ee);
+              bx[u] = __shfl(cr.x, (int)eo, 64);
+              bl[u] = ee < qtot ? __shfl(len, (int)eo, 64) : 0u;
+              qb[u] = (bx[u] & ~3u) + 4u * (ee - __shfl(qoff, (int)eo, 64));
+              v[u] = ee < qtot ? *reinterpret_cast<const uint4*>(P.c_id + (qb[u] & P.cmask))
+                               : make_uint4(DICT_IDS, DICT_IDS, DICT_IDS, DICT_IDS);
+            }
 #pragma unroll
-            for (uint32_t u = 0; u < AW_ILP; ++u)
-              if (d0 + u < sl) record(s0 + d0 + u, id[u]);
+            for (uint32_t u = 0; u < AW_QILP; ++u) {
+              const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+              for (uint32_t k = 0; k < 4u; ++k)
+                if ((qb[u] + k - bx[u]) < bl[u]) record(qb[u] + k, ids[k]);
+            }
           }
         }
         if (false) {
