@@ -2893,9 +2893,11 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
             for (uint32_t u = 0; u < AW_QILP; ++u) {
               const uint32_t ee = e0 + 64u * u + lane;
               const uint32_t eo = wave_owner(qoff, ee);
+              // (every lane shuffles: a lane past qtot may own nothing yet be another lane's source)
               bx[u] = __shfl(cr.x, (int)eo, 64);
-              bl[u] = ee < qtot ? __shfl(len, (int)eo, 64) : 0u;
-              qb[u] = (bx[u] & ~3u) + 4u * (ee - __shfl(qoff, (int)eo, 64));
+              const uint32_t lo = __shfl(len, (int)eo, 64), oo = __shfl(qoff, (int)eo, 64);
+              bl[u] = ee < qtot ? lo : 0u;
+              qb[u] = (bx[u] & ~3u) + 4u * (ee - oo);
               v[u] = ee < qtot ? *reinterpret_cast<const uint4*>(P.c_id + (qb[u] & P.cmask))
                                : make_uint4(DICT_IDS, DICT_IDS, DICT_IDS, DICT_IDS);
             }
