@@ -2880,7 +2880,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         APPLYB_SUB(t_big);
         // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
         // flattened across the lanes, one quad per lane per load (one owner search per quad)
-#ifndef SWIM_AW_SHORT_REC
+#ifdef SWIM_AW_SHORT_QUAD  // (A/B build until its parity run)
         {
           const bool sh = len != 0u && len < 64u;
           const uint32_t nq = sh ? ((cr.x & 3u) + len + 3u) >> 2 : 0u;
