@@ -2692,10 +2692,6 @@ constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flig
 #define SWIM_AW_QILP 2
 #endif
 constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
-#ifndef SWIM_AW_MILP
-#define SWIM_AW_MILP 1
-#endif
-constexpr uint32_t AW_MILP = SWIM_AW_MILP;        // dictionary blocks merged per lane per step
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
@@ -2835,13 +2831,12 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
           }
         }
 #endif
-        // long ranges (batches): the whole wave walks each, four coalesced records per lane in flight
+        // long ranges (batches): the whole wave walks each, 16-B quads of entry ids per lane
         unsigned long long big = __ballot(len >= 64u);
         while (big) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
           const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
-#ifndef SWIM_AW_SCALAR
           // aligned 16-B quads of entry ids from the quad holding b0: 4 records per lane per load
           const uint32_t a0 = b0 & ~3u, span = b1 - a0;
           for (uint32_t x0 = 0; x0 < span; x0 += 256u * AW_VILP) {
@@ -2861,21 +2856,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
                 if ((x + k - b0) < (b1 - b0)) record(x + k, ids[k]);
             }
           }
-#else
-          for (uint32_t x0 = b0; x0 != b1; x0 += min(64u * AW_ILP, b1 - x0)) {
-            uint32_t id[AW_ILP];
-#pragma unroll
-            for (uint32_t u = 0; u < AW_ILP; ++u) {
-              const uint32_t x = x0 + 64u * u + lane;
-              id[u] = (x - b0) < (b1 - b0) ? P.c_id[x & P.cmask] : DICT_IDS;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < AW_ILP; ++u) {
-              const uint32_t x = x0 + 64u * u + lane;
-              if ((x - b0) < (b1 - b0)) record(x, id[u]);
-            }
-          }
-#endif
         }
         APPLYB_SUB(t_big);
         // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
@@ -2983,7 +2963,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
       }
       uint32_t tot;
       const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
-#if SWIM_AW_MILP == 1
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
         const uint32_t o = wave_owner(off, q);
@@ -3011,52 +2990,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
           }
         }
       }
-#else
-      // AW_MILP blocks per lane per step: their entry loads, then their cells, then the merges
-      // (one block per subject, so a merge never changes another block's cell)
-      for (uint32_t q0 = 0; q0 < tot; q0 += 64u * AW_MILP) {
-        uint32_t subj[AW_MILP], best[AW_MILP], cv[AW_MILP];
-        uint4 r0[AW_MILP], r1[AW_MILP];
-        uint32_t mm[AW_MILP];
-#pragma unroll
-        for (uint32_t i = 0; i < AW_MILP; ++i) {
-          const uint32_t q = q0 + 64u * i + lane;
-          const uint32_t o = wave_owner(off, q);
-          const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
-          mm[i] = 0u;
-          subj[i] = 0u;
-          if (q < tot) {
-            const uint32_t b = kth_set_bit(bo, q - oo);
-            const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
-            const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
-            const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
-            r0[i] = dr[0];
-            r1[i] = dr[1];
-            subj[i] = P.d_subj[base / DICT_WAYS];
-            mm[i] = (s_bm[t] >> (8u * j)) & 0xFFu;  // nonzero: the block has set entries
-          }
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < AW_MILP; ++i) {
-          const uint32_t m = mm[i];
-          best[i] = max(max(max((m & 1u) ? r0[i].x : 0u, (m & 2u) ? r0[i].y : 0u),
-                            max((m & 4u) ? r0[i].z : 0u, (m & 8u) ? r0[i].w : 0u)),
-                        max(max((m & 16u) ? r1[i].x : 0u, (m & 32u) ? r1[i].y : 0u),
-                            max((m & 64u) ? r1[i].z : 0u, (m & 128u) ? r1[i].w : 0u)));
-          cv[i] = (m && !via_inbox) ? cell_get(P, p, subj[i]) : 0u;
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < AW_MILP; ++i) {
-          if (!mm[i]) continue;
-          if (via_inbox)
-            spill(subj[i], best[i]);
-          else if (is_overrides(best[i], cv[i]) || (P.nxk && P.colmap[subj[i]] == NONE))  // (the latter: OV_TRACK)
-            apply(subj[i], best[i]);
-          else
-            ++nsubj;
-        }
-      }
-#endif
       wsync();  // every lane has read its blocks' bits
 #pragma unroll
       for (uint32_t u = 0; u < 8u; ++u)
