@@ -2680,10 +2680,6 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 #endif
 constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
 constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per workgroup
-#ifndef SWIM_AW_ILP
-#define SWIM_AW_ILP 4
-#endif
-constexpr uint32_t AW_ILP = SWIM_AW_ILP;          // record-entry loads in flight per lane
 #ifndef SWIM_AW_VILP
 #define SWIM_AW_VILP 2
 #endif
@@ -2860,7 +2856,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         APPLYB_SUB(t_big);
         // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
         // flattened across the lanes, one quad per lane per load (one owner search per quad)
-#ifdef SWIM_AW_SHORT_QUAD  // (A/B build until its parity run)
         {
           const bool sh = len != 0u && len < 64u;
           const uint32_t nq = sh ? ((cr.x & 3u) + len + 3u) >> 2 : 0u;
@@ -2889,27 +2884,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
                 if ((qb[u] + k - bx[u]) < bl[u]) record(qb[u] + k, ids[k]);
             }
           }
-        }
-        if (false) {
-#else
-        {
-#endif
-        uint32_t etot;
-        const uint32_t eoff = wave_excl_scan(len < 64u ? len : 0u, &etot);
-        for (uint32_t e0 = 0; e0 < etot; e0 += 64u * AW_ILP) {
-          uint32_t xs[AW_ILP], id[AW_ILP];
-#pragma unroll
-          for (uint32_t u = 0; u < AW_ILP; ++u) {
-            const uint32_t ee = e0 + 64u * u + lane;
-            const uint32_t eo = wave_owner(eoff, ee);
-            const uint32_t bx = __shfl(cr.x, (int)eo, 64), bo = __shfl(eoff, (int)eo, 64);
-            xs[u] = bx + ee - bo;
-            id[u] = ee < etot ? P.c_id[xs[u] & P.cmask] : DICT_IDS;
-          }
-#pragma unroll
-          for (uint32_t u = 0; u < AW_ILP; ++u)
-            if (e0 + 64u * u + lane < etot) record(xs[u], id[u]);
-        }
         }
         APPLYB_SUB(t_short);
       }
