@@ -664,6 +664,25 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 // exclusive prefix sum over the 64 lanes; *total = sum over the wave (all lanes must call)
+#ifdef SWIM_DPP_SCAN
+// one DPP step of the scan: v from the lane the control selects, 0 where that lane is out of the
+// row or masked off (old = 0, bound_ctrl off)
+template <int CTRL, int ROWM>
+__device__ __forceinline__ uint32_t dpp_in(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  uint32_t x = v;
+  x += dpp_in<0x111, 0xF>(x);  // row_shr:1 .. row_shr:8: inclusive scans of the four 16-lane rows
+  x += dpp_in<0x112, 0xF>(x);
+  x += dpp_in<0x114, 0xF>(x);
+  x += dpp_in<0x118, 0xF>(x);
+  x += dpp_in<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+  x += dpp_in<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+  *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  return x - v;
+}
+#else
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t x = v;
@@ -675,6 +694,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   *total = __shfl(x, 63, 64);
   return x - v;
 }
+#endif
 
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {
   v = wave_sum(v);
