@@ -663,14 +663,15 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// exclusive prefix sum over the 64 lanes; *total = sum over the wave (all lanes must call)
-#ifdef SWIM_DPP_SCAN
-// one DPP step of the scan: v from the lane the control selects, 0 where that lane is out of the
+// one DPP step of a wave scan: v from the lane the control selects, 0 where that lane is out of the
 // row or masked off (old = 0, bound_ctrl off)
 template <int CTRL, int ROWM>
 __device__ __forceinline__ uint32_t dpp_in(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
 }
+// exclusive prefix sum over the 64 lanes; *total = sum over the wave (all lanes must call). DPP
+// row shifts and broadcasts move the partial sums between lanes in the VALU instead of six
+// LDS-routed lane shuffles (C3: k_gossip_apply_b 189 -> 183 ms per 20 periods)
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
   uint32_t x = v;
   x += dpp_in<0x111, 0xF>(x);  // row_shr:1 .. row_shr:8: inclusive scans of the four 16-lane rows
@@ -682,19 +683,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
 }
-#else
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
-}
-#endif
 
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {
   v = wave_sum(v);

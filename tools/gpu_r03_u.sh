@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 final tree: the whole -m gpu suite, the C3 20/5 bench line with its CPU baseline, the
+# Round-3 final tree (also after the DPP wave scans): the whole -m gpu suite, the C3 20/5 bench line with its CPU baseline, the
 # rocprofv3 kernel stats of the same window, and the FETCH_SIZE / WRITE_SIZE passes (tools/gpu_pmc.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
