@@ -315,12 +315,8 @@ __device__ __forceinline__ uint32_t cs_n(const KP& P, const uint4* stg, uint32_t
 
 __device__ __forceinline__ uint32_t cs_block_scan(uint32_t v, uint32_t* total, uint32_t* lds) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
+  uint32_t wt;
+  const uint32_t x = wave_excl_scan(v, &wt) + v;  // the wave's inclusive scan (DPP)
   if (lane == 63u) lds[w] = x;
   __syncthreads();
   uint32_t base = 0, tot = 0;
@@ -1043,12 +1039,8 @@ __device__ __forceinline__ void register_sender(const KP& P, uint32_t p, uint32_
 
 __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* total, uint32_t* lds16) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
+  uint32_t wt;
+  const uint32_t x = wave_excl_scan(v, &wt) + v;  // the wave's inclusive scan (DPP)
   if (lane == 63u) lds16[w] = x;
   __syncthreads();
   uint32_t base = 0, tot = 0;
@@ -2304,12 +2296,8 @@ static_assert(!SWIM_APPLY_PAIR || APPLY_THREADS == 1024, "SWIM_APPLY_PAIR needs 
 __device__ __forceinline__ uint32_t block_excl_scan_part(uint32_t v, uint32_t* total, uint32_t* lds16, bool pair,
                                                          uint32_t half) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
+  uint32_t wt;
+  const uint32_t x = wave_excl_scan(v, &wt) + v;  // the wave's inclusive scan (DPP)
   if (lane == 63u) lds16[w] = x;
   __syncthreads();
   const uint32_t k0 = pair ? 8u * half : 0u, k1 = pair ? k0 + 8u : blockDim.x / 64u;
@@ -3572,12 +3560,8 @@ __global__ void k_sync_scatter(KP P) {
 
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* total, uint32_t* lds4) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
+  uint32_t wt;
+  const uint32_t x = wave_excl_scan(v, &wt) + v;  // the wave's inclusive scan (DPP)
   if (lane == 63u) lds4[w] = x;
   __syncthreads();
   uint32_t base = 0, tot = 0;
