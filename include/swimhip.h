@@ -315,6 +315,13 @@ int swim_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint
  * Random123 philox4x32_10 known-answer vectors apply directly (tests/test_philox_kat.py). */
 int swim_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abc_tick, uint32_t* out4, uint64_t n);
 
+/* Device check of the scans every compaction is built on (no reference counterpart): for n
+ * inputs (a multiple of 1,024), the exclusive prefix sum within each 64-lane wave and each wave's
+ * total (n / 64 entries), and the exclusive prefix sum within each 1,024-thread workgroup and each
+ * workgroup's total (n / 1,024 entries), computed by gfx950 kernels. No handle needed. */
+int swim_kat_scan(const uint32_t* in, uint64_t n, uint32_t* wave_excl, uint32_t* wave_tot, uint32_t* block_excl,
+                  uint32_t* block_tot);
+
 /* Debug: the gossips a member holds, as (gossip hash, infection round) pairs. */
 int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uint32_t* out_inf, uint32_t cap,
                         uint32_t* n_out);

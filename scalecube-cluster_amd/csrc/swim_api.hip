@@ -61,6 +61,7 @@ struct swim_handle {
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
+  uint32_t* crash_ids = nullptr;  // [N] the members one swim_crash call stops (allocated on first use)
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
@@ -1125,29 +1126,21 @@ int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
                   "(DESIGN.md 3.12): set the delay before they are created, or create with gossip_batching = 1");
   }
   // dthr[k] = ceil(2^32 (1 - exp(-k / mean))) for every k a 32-bit draw can reach (the oracle
-  // computes the same table with the same expression)
+  // computes the same table with the same expression). Built and checked on the host first: a
+  // refused call leaves the handle exactly as it was (the live table, dq_live and the rings).
   std::vector<uint32_t> thr;
   for (uint32_t k = 0;; ++k) {
     const double t = std::ceil(std::ldexp(-std::expm1(-(double)k / (double)mean_ms), 32));
     if (t > 4294967295.0) break;
     thr.push_back((uint32_t)t);
   }
-  if (thr.size() > h->dthr_cap) {  // (a smaller earlier table stays allocated until swim_destroy)
-    uint32_t* dt = nullptr;
-    int rc = dalloc(h, &dt, thr.size());
-    if (rc) return rc;
-    P.dthr = dt;
-    h->dthr_cap = (uint32_t)thr.size();
-  }
-  HIPC(h, hipMemcpyAsync(const_cast<uint32_t*>(P.dthr), thr.data(), thr.size() * 4, hipMemcpyHostToDevice, h->stream));
-  P.dthr_n = (uint32_t)thr.size();
   // an entry matters until its message arrived and left the infectedFrom horizon: the per-round
   // head history (256 rounds) must reach that far back
-  const uint32_t live = (P.dthr_n - 1u) / P.gint + P.hzn + 1u;
+  const uint32_t live = ((uint32_t)thr.size() - 1u) / P.gint + P.hzn + 1u;
   if (live >= 256u) return fail(h, SWIM_EINVAL, "swim_set_delay: delays this long (in gossip rounds) exceed the ring history");
+  if (!P.dq && P.nloc > 65536u)
+    return fail(h, SWIM_EINVAL, "swim_set_delay: the delayed-message rings are sized for clusters up to 65,536 members");
   if (!P.dq) {  // per receiver: messages in flight plus the arrived ones still inside the horizon
-    if (P.nloc > 65536u)
-      return fail(h, SWIM_EINVAL, "swim_set_delay: the delayed-message rings are sized for clusters up to 65,536 members");
     uint32_t cap = 65536;  // entries per receiver, within 2 GiB of rings
     while (cap > 4096u && (uint64_t)P.nloc * cap * 16u > (2ull << 30)) cap >>= 1;
     uint4* dq = nullptr;
@@ -1163,6 +1156,15 @@ int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
     P.dq_rhead = rhead;
     P.dqcap = cap;
   }
+  if (thr.size() > h->dthr_cap) {  // (a smaller earlier table stays allocated until swim_destroy)
+    uint32_t* dt = nullptr;
+    int rc = dalloc(h, &dt, thr.size());
+    if (rc) return rc;
+    P.dthr = dt;
+    h->dthr_cap = (uint32_t)thr.size();
+  }
+  HIPC(h, hipMemcpyAsync(const_cast<uint32_t*>(P.dthr), thr.data(), thr.size() * 4, hipMemcpyHostToDevice, h->stream));
+  P.dthr_n = (uint32_t)thr.size();
   P.dq_live = std::max(P.dq_live, live);  // entries pushed under an earlier, longer mean stay covered
   HIPC(h, hipStreamSynchronize(h->stream));
   P.delay_on = 1;
@@ -1302,13 +1304,24 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
   std::vector<uint8_t> alive(h->N);
   HIPC(h, hipMemcpyAsync(alive.data(), h->base.alive, h->N, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  for (uint32_t k = 0; k < n; ++k)
+    if (ids[k] >= h->N) return SWIM_EINVAL;
+  std::vector<uint32_t> down;  // the distinct members this call stops
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t c = ids[k];
-    if (c >= h->N) return SWIM_EINVAL;
     if (!alive[c]) continue;
     alive[c] = 0;
-    hipLaunchKernelGGL(k_crash, dim3(blocks_for(h->N, 256)), dim3(256), 0, h->stream, h->base, c);
-    hipLaunchKernelGGL(k_stop_addr, dim3(1), dim3(64), 0, h->stream, h->base, c);
+    down.push_back(c);
+  }
+  if (!down.empty()) {  // one launch for the whole set (k_crash_many)
+    if (!h->crash_ids) {
+      int rc = dalloc(h, &h->crash_ids, h->N);
+      if (rc) return rc;
+    }
+    HIPC(h, hipMemcpyAsync(h->crash_ids, down.data(), down.size() * 4, hipMemcpyHostToDevice, h->stream));
+    const uint32_t chunks = blocks_for(h->base.W, CRASH_PIECE);
+    hipLaunchKernelGGL(k_crash_many, dim3((uint32_t)down.size() * chunks), dim3(256), 0, h->stream, h->base,
+                       h->crash_ids, (uint32_t)down.size(), chunks);
   }
   HIPC(h, hipMemcpyAsync(h->base.alive, alive.data(), h->N, hipMemcpyHostToDevice, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -1636,6 +1649,30 @@ int swim_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_
   }
   (void)hipFree(din);
   (void)hipFree(dout);
+  return rc;
+}
+
+int swim_kat_scan(const uint32_t* in, uint64_t n, uint32_t* wave_excl, uint32_t* wave_tot, uint32_t* block_excl,
+                  uint32_t* block_tot) {
+  if (!in || !wave_excl || !wave_tot || !block_excl || !block_tot || n % 1024u) return SWIM_EINVAL;
+  if (n == 0) return SWIM_OK;
+  uint32_t *din = nullptr, *dwe = nullptr, *dwt = nullptr, *dbe = nullptr, *dbt = nullptr;
+  int rc = SWIM_OK;
+  if (hipMalloc(&din, n * 4) != hipSuccess || hipMalloc(&dwe, n * 4) != hipSuccess ||
+      hipMalloc(&dwt, n / 16) != hipSuccess || hipMalloc(&dbe, n * 4) != hipSuccess ||
+      hipMalloc(&dbt, n / 256) != hipSuccess)
+    rc = SWIM_EHIP;
+  if (rc == SWIM_OK && hipMemcpy(din, in, n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = SWIM_EHIP;
+  if (rc == SWIM_OK) {
+    hipLaunchKernelGGL(k_kat_scan, dim3((uint32_t)(n / 1024)), dim3(1024), 0, 0, din, dwe, dwt, dbe, dbt);
+    if (hipMemcpy(wave_excl, dwe, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(wave_tot, dwt, n / 16, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(block_excl, dbe, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(block_tot, dbt, n / 256, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = SWIM_EHIP;
+  }
+  for (uint32_t* p : {din, dwe, dwt, dbe, dbt})
+    if (p) (void)hipFree(p);
   return rc;
 }
 

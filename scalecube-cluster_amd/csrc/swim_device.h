@@ -359,6 +359,10 @@ constexpr uint32_t DICT_WORDS = DICT_IDS / 32u;  // a receiver's entry bitmap
 constexpr uint32_t ID_USER = 0xFFFFFFFEu;        // c_id of a user gossip (subject >= N)
 constexpr uint32_t ID_NONE = NONE;               // c_id of a record that found no entry
 constexpr uint32_t DICT_LOCK = 0xFFFFFFFEu;      // sid_of while k_dict_claim allocates the block
+// sid_of of a subject whose claim found no block: DICT_NOBLK | (the commit's first record index &
+// DICT_TAG_MASK); a later commit may claim again (k_dict_claim). Never a block id (< 2^16).
+constexpr uint32_t DICT_NOBLK = 0x80000000u;
+constexpr uint32_t DICT_TAG_MASK = 0x3FFFFFFFu;
 static_assert(DICT_SIDS >= 4 && (DICT_SIDS & (DICT_SIDS - 1)) == 0 && DICT_SIDS <= (1u << 16),
               "SWIM_DICT_SIDS: a power of two in 4 .. 65536");
 
@@ -663,6 +667,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+// The wave scans below use GFX9 DPP row broadcasts (row_bcast:15 / row_bcast:31, controls 0x142 /
+// 0x143), which exist only on GFX9-family targets, and assume 64-lane waves (every GFX9 target is
+// wave64). They also need every lane of the wave active: callers run them in converged code only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "swim_device.h: wave_excl_scan needs a GFX9 (wave64, DPP row_bcast) target such as gfx950"
+#endif
 // one DPP step of a wave scan: v from the lane the control selects, 0 where that lane is out of the
 // row or masked off (old = 0, bound_ctrl off)
 template <int CTRL, int ROWM>

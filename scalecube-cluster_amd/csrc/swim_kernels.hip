@@ -140,11 +140,6 @@ __global__ void k_iota_u32(uint32_t* p, uint32_t n, uint32_t n_id) {
   if (i < n) p[i] = i < n_id ? i : NONE;
 }
 
-// a stopped member's address goes quiet (unless a restarted member already holds it)
-__global__ void k_stop_addr(KP P, uint32_t c) {
-  if (threadIdx.x == 0 && P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
-}
-
 // swim_join / swim_restart: spare slot x starts at address a (ClusterImpl.start, ClusterImpl.java:
 // 170-227) with a table holding only itself ALIVE inc 0 (MembershipProtocolImpl.java:138-142) and
 // fresh protocol state; a restart on another member's address links x into that address's movers.
@@ -176,16 +171,26 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
   }
 }
 
-// swim_crash: transport.stop() — presence no longer counted, timers dropped.
-// Only the shard that owns row c has anything to drop (presence counts are per-shard partials).
-__global__ void k_crash(KP P, uint32_t c) {
-  if (!is_local(P, c)) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
-    atomicSub(&P.ctl->alive_count, 1u);  // N x K: every untracked subject loses this observer
+// swim_crash: transport.stop() of n members at once (distinct, alive): presence no longer counted,
+// timers dropped, the address goes quiet (unless a restarted member already holds it). Only the shard
+// that owns a member's row has presence / timers to drop; workgroup b takes member b / chunks and
+// the b % chunks-th piece of its row.
+constexpr uint32_t CRASH_PIECE = 256u * 16u;  // cells per workgroup
+__global__ void __launch_bounds__(256) k_crash_many(KP P, const uint32_t* ids, uint32_t n, uint32_t chunks) {
+  const uint32_t k = blockIdx.x / chunks, piece = blockIdx.x % chunks;
+  if (k >= n) return;
+  const uint32_t c = ids[k];
+  if (piece == 0u && threadIdx.x == 0u) {
+    if (is_local(P, c)) {
+      atomicSub(&P.ctl->bl_hist[bitlen(P.cnt[c] + 1u)], 1u);
+      atomicSub(&P.ctl->alive_count, 1u);  // N x K: every untracked subject loses this observer
+    }
+    if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;  // the address goes quiet (k_stop_addr)
   }
+  if (!is_local(P, c)) return;
   const uint32_t nc = ncells(P);
-  for (uint32_t cc = blockIdx.x * blockDim.x + threadIdx.x; cc < nc; cc += gridDim.x * blockDim.x) {
+  const uint32_t c0 = piece * CRASH_PIECE, c1 = min(nc, c0 + CRASH_PIECE);
+  for (uint32_t cc = c0 + threadIdx.x; cc < c1; cc += blockDim.x) {
     const uint32_t j = subj_of(P, cc);
     if (j != c && P.view[lrow(P, c) * P.W + cc] != 0u) atomicSub(&P.pres[j], 1u);
     P.dl[(size_t)cc * P.nloc + lrow(P, c)] = 0u;
@@ -617,24 +622,38 @@ __global__ void k_commit_wsum(KP P, uint32_t all) {
 
 // ---- record dictionary, after every commit: claim, entries, free ----
 // A block for each subject of the commit's records that has none: the CAS winner pops a free
-// block (or takes a new one); when none is left the subject keeps NONE and its records take the
-// apply kernel's slow path. No thread waits on another.
+// block (or takes a new one); when none is left the subject is marked with this commit's
+// no-block tag (its records take the apply kernel's slow path) and is not claimed again until a
+// later commit, so a commit makes at most one failed claim per subject. The high-water mark
+// never passes DICT_SIDS (a bounded increment), so it cannot wrap onto blocks in use. No thread
+// waits on another.
 __global__ void k_dict_claim(KP P) {
   const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0, nfree = P.ctl->d_nfree;
+  const uint32_t tag = DICT_NOBLK | (c0 & DICT_TAG_MASK);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t subj = P.c_sr[(c0 + i) & P.cmask].x;
-    if (subj >= P.N || P.sid_of[subj] != NONE) continue;
-    if (atomicCAS(&P.sid_of[subj], NONE, DICT_LOCK) != NONE) continue;
+    if (subj >= P.N) continue;
+    const uint32_t cur = P.sid_of[subj];
+    // a block, a claim in progress, or a claim of this commit that found none
+    if (cur < DICT_SIDS || cur == DICT_LOCK || cur == tag) continue;
+    if (atomicCAS(&P.sid_of[subj], cur, DICT_LOCK) != cur) continue;  // NONE or an older commit's tag
     const uint32_t k = atomicAdd(&P.ctl->d_taken, 1u);
     uint32_t sid = NONE;
     if (k < nfree) {
       sid = P.d_free[nfree - 1u - k];
     } else {
-      const uint32_t hw = atomicAdd(&P.ctl->d_hw, 1u);
-      if (hw < DICT_SIDS) sid = hw;
+      uint32_t hw = __hip_atomic_load(&P.ctl->d_hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (hw < DICT_SIDS) {
+        const uint32_t seen = atomicCAS(&P.ctl->d_hw, hw, hw + 1u);
+        if (seen == hw) {
+          sid = hw;
+          break;
+        }
+        hw = seen;
+      }
     }
     if (sid != NONE) P.d_subj[sid] = subj;
-    P.sid_of[subj] = sid;
+    P.sid_of[subj] = sid != NONE ? sid : tag;
   }
 }
 
@@ -3809,6 +3828,20 @@ __global__ void k_kat_philox4(uint64_t seed, uint32_t kind, const uint32_t* abct
 __global__ void k_kat_philox(uint64_t seed, uint32_t kind, const uint32_t* abct, uint32_t* out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = draw1(seed, kind, abct[4 * i], abct[4 * i + 1], abct[4 * i + 2], abct[4 * i + 3]);
+}
+
+// The scans every kernel builds its compactions on (DPP wave scan, 1,024-thread block scan), on
+// known inputs: one 1,024-thread workgroup per 1,024 elements, every lane active
+__global__ void __launch_bounds__(1024) k_kat_scan(const uint32_t* in, uint32_t* wexcl, uint32_t* wtot,
+                                                   uint32_t* bexcl, uint32_t* btot) {
+  __shared__ uint32_t s_lds[16];
+  const uint64_t i = (uint64_t)blockIdx.x * 1024u + threadIdx.x;
+  const uint32_t v = in[i];
+  uint32_t wt = 0, bt = 0;
+  wexcl[i] = wave_excl_scan(v, &wt);
+  if ((threadIdx.x & 63u) == 0u) wtot[i >> 6] = wt;
+  bexcl[i] = block_excl_scan1024(v, &bt, s_lds);
+  if (threadIdx.x == 0u) btot[blockIdx.x] = bt;
 }
 
 }  // namespace swim

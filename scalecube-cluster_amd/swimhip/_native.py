@@ -186,6 +186,7 @@ SWIM_ONLY = [
     ("swim_kat_is_overrides", _I, [_pU32, _pU32, _pU8, _U64]),
     ("swim_kat_philox", _I, [_U64, _U32, _pU32, _pU32, _U64]),
     ("swim_kat_philox4", _I, [_U64, _U32, _pU32, _pU32, _U64]),
+    ("swim_kat_scan", _I, [_pU32, _U64, _pU32, _pU32, _pU32, _pU32]),
     ("swim_debug_holdings", _I, [_P, _U32, _pU32, _pU32, _U32, _pU32]),
     ("swim_debug_member_state", _I, [_P, _pU32, _U32]),
     ("swim_debug_sends", _I, [_P, _pU64, _U32]),

@@ -313,3 +313,53 @@ def test_c3long_schedule_small_parity():
         sa, sb = a.stats(), b.stats()
         assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
     assert 0 < a.stats()["not_converged"] < 1322  # the cut group's unprobed crashed members, draining
+
+
+def test_refused_set_delay_leaves_the_handle_unchanged():
+    """A set_delay the device refuses (a mean whose longest delay, in gossip rounds, would outrun the
+    256-round head history) must leave the handle as it was: the live threshold table, the ring
+    window and delay_on of the accepted mean. Both sides run 1,000 ms mean delays (LAN: 200 ms
+    rounds); the device then refuses 3,000 ms with SWIM_EINVAL and must stay bit-exact with the
+    oracle, which never saw the refused call."""
+    from swimhip import SwimError
+
+    cfg = ClusterConfig.defaultLanConfig()
+    n = 256
+    a = SwimCluster(cfg, n, seed=21, event_capacity=1 << 20)
+    b = OracleCluster(cfg, n, seed=21, event_capacity=1 << 20)
+    for c in (a, b):
+        c.set_loss(2.0)
+        c.set_delay(1000)
+        c.step(3)
+    with pytest.raises(SwimError) as ei:
+        a.set_delay(3000)
+    assert ei.value.code == -22
+    crashed = scenarios.crash_ids(n, 3, 21)
+    for c in (a, b):
+        c.crash(crashed)
+    for _ in range(6):
+        for c in (a, b):
+            c.step(4)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+        assert [e.key() for e in a.events()] == [e.key() for e in b.events()]
+
+
+# The sharded rehearsals' shapes of BASELINE configs 3 and 4 (tests/test_sharded.py compares their
+# shards with the unsharded handle), pinned to the oracle here: C4's schedule (1 % loss, 0.1 % crash,
+# LAN; one gossip per slot) and C5's (64 concurrent crashes, no loss, gossip batches, past the first
+# suspicion timeouts) at 4,096 members, dense, and C5's as N x K with K = 256 columns against the
+# dense oracle: the many concurrent churn columns C5 is defined by (MembershipProtocolImpl.java:620-647)
+@pytest.mark.parametrize("name", ["lan4096_c4_shape", "nxk4096_c5_shape"])
+def test_sharded_shapes_match_oracle(name):
+    scenarios.run_pair(name, SwimCluster, OracleCluster, compare_every=4)
+
+
+def test_nxk_k256_64_concurrent_crashes_match_dense_oracle():
+    def make_nxk(cfg, n, seed, **kw):
+        return SwimCluster(cfg, n, seed, tracked_subjects=256, **kw)
+
+    a, _ = scenarios.run_pair("nxk4096_c5_shape", make_nxk, OracleCluster, compare_every=5)
+    st = a.stats()
+    assert st["events_removed"] > 200_000  # the 64 columns' suspicion timeouts fired (oracle: 241,919)
