@@ -198,7 +198,7 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp);
  * and a ping, ping-req relay or metadata round trip counts only if it returns within its timeout
  * (DESIGN.md §3.16). Draws per message, so, like a probabilistic loss, it needs one gossip per ring
  * slot (SWIM_EINVAL while batch slots are live). Messages already in flight keep their arrival rounds
- * when the mean changes (or is reset to 0). Unsharded handles, up to 65,536 members. */
+ * when the mean changes (or is reset to 0). Up to 65,536 observer rows per handle (shard). */
 int swim_set_delay(swim_handle* h, uint32_t mean_ms);
 /* Partition groups: messages a->b are lost while period in [t0, t1) and group[a] != group[b]
  * (NetworkEmulator.blockOutbound on both sides of a cut). n must equal n_members. */
@@ -216,7 +216,8 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n);
 /* Graceful leave = Cluster.shutdown() (ClusterImpl.java:370-408): each member's own record
  * becomes DEAD and is spread as a gossip (MembershipProtocolImpl.leaveCluster :203-212); the member
  * keeps running until its own sweep drops that gossip (spread() completes at sweep,
- * GossipProtocolImpl.java:299-302), then stops at the end of that gossip round. Unsharded handles. */
+ * GossipProtocolImpl.java:299-302), then stops at the end of that gossip round. On a sharded handle the
+ * member's shard announces the stop in the next commit exchange (liveness is replicated). */
 int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n);
 
 /* Cluster.updateMetadata (ClusterImpl.java:364-367): each member's metadata changes (a new version;
@@ -224,7 +225,7 @@ int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n);
  * own record ALIVE with incarnation + 1 and spreads it. Observers that accept the new record fetch the
  * metadata (MetadataStoreImpl.fetchMetadata :151-193) and, for a member they already had, emit UPDATED
  * when it differs from the one they stored (onAliveMemberDetected :589-610). Takes effect before the
- * next period. Unsharded handles. */
+ * next period. */
 int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n);
 
 /* Join = a new member's ClusterImpl.start() (ClusterImpl.java:170-227): spare slot `ids[k]` (never
@@ -246,8 +247,19 @@ int swim_restart(swim_handle* h, const uint32_t* old_ids, const uint32_t* new_id
 /* GossipProtocol.spread (GossipProtocol.java:12-29, GossipProtocolImpl.java:124-128): member
  * `origin` spreads a user gossip carrying `tag` (the payload stand-in); it is created before the
  * next period (infectionPeriod = that period's first round), travels like every gossip, and each
- * member's first receipt is a SWIM_EV_GOSSIP event. Unsharded handles. */
+ * member's first receipt is a SWIM_EV_GOSSIP event. */
 int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag);
+/* A message of an external node delivered to simulated member `observer` before the next period
+ * (the wire bridge, swimhip/wire.py: a real JVM member's SYNC / SYNC_ACK / membership gossip, decoded
+ * from the reference's JSON). Each (subjects[k], records[k]) goes through updateMembership in order
+ * (MembershipProtocolImpl.java:481-547) with `reason` SWIM_R_SYNC, SWIM_R_INITIAL_SYNC (syncMembership,
+ * :463-473) or SWIM_R_MEMBERSHIP_GOSSIP (onMembershipGossip, :407-414); records accepted under SYNC
+ * spread as gossips created for the next period's first round (:649-656); a metadata fetch for an
+ * accepted ALIVE record draws with counter SWIM_DELIVER_ATTEMPT | k in that period's FD tick. A stopped
+ * member receives nothing. records[k] must not be SWIM_ABSENT (a SyncData carries present records). */
+#define SWIM_DELIVER_ATTEMPT 0x80000000u
+int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subjects, const uint32_t* records,
+                         uint32_t n, uint32_t reason);
 /* Optional trace streams into the event ring (mask of SWIM_TRACE_*; 0 = off, the default). */
 int swim_trace(swim_handle* h, uint32_t mask);
 

@@ -1307,6 +1307,28 @@ int oracle_spread(oracle_handle* h, uint32_t origin, uint32_t tag) {
   return SWIM_OK;
 }
 
+// A message of an external node (a real JVM member over the wire bridge, swimhip/wire.py) handed
+// to member `obs` before the next period: its records go through updateMembership one by one, in
+// order, with the message's reason (MPI:463-473 syncMembership for SYNC / SYNC_ACK / INITIAL_SYNC,
+// MPI:407-414 onMembershipGossip for a membership gossip). Accepted records spread as gossips
+// created for the next period's first round (reason SYNC; MPI:649-656); metadata fetches draw
+// with attempt SWIM_DELIVER_ATTEMPT | k in that period's FD tick. A stopped member receives nothing.
+int oracle_deliver_records(oracle_handle* h, uint32_t obs, const uint32_t* subj, const uint32_t* rec, uint32_t n,
+                           uint32_t reason) {
+  if (!h || obs >= h->N || (n && (!subj || !rec))) return SWIM_EINVAL;
+  if (reason != SWIM_R_SYNC && reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC) return SWIM_EINVAL;
+  for (uint32_t k = 0; k < n; ++k)
+    if (subj[k] >= h->N || rec[k] == SWIM_ABSENT) return SWIM_EINVAL;
+  Member& me = h->m[obs];
+  if (!me.alive) return SWIM_OK;
+  const uint32_t tick = tick_of(h, 0), snap = me.others;
+  for (uint32_t k = 0; k < n; ++k)
+    update_membership(h, obs, subj[k], rec[k], reason, 0, SWIM_DELIVER_ATTEMPT | k, tick, snap,
+                      (int64_t)h->period * h->G);
+  finish_phase(h);
+  return SWIM_OK;
+}
+
 int oracle_trace(oracle_handle* h, uint32_t mask) {
   if (!h) return SWIM_EINVAL;
   h->trace = mask;

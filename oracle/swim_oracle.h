@@ -40,6 +40,8 @@ int oracle_update_metadata(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_join(oracle_handle* h, const uint32_t* ids, uint32_t n);
 int oracle_restart(oracle_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n);
 int oracle_spread(oracle_handle* h, uint32_t origin, uint32_t tag);
+int oracle_deliver_records(oracle_handle* h, uint32_t obs, const uint32_t* subj, const uint32_t* rec, uint32_t n,
+                           uint32_t reason);
 int oracle_trace(oracle_handle* h, uint32_t mask);
 int oracle_step(oracle_handle* h, uint32_t periods);
 int oracle_drain_events(oracle_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);

@@ -62,6 +62,8 @@ struct swim_handle {
   uint32_t CC = 0;  // record ring of the gossip batches
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
   uint32_t* crash_ids = nullptr;  // [N] the members one swim_crash call stops (allocated on first use)
+  uint32_t* deliver_buf = nullptr;  // swim_deliver_records: subjects, then records (grown on demand)
+  uint32_t deliver_cap = 0;
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
@@ -299,26 +301,39 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t b
     *rc = commit_sorted(h, P, P.stg, 0u, bound);
     return false;
   }
-  // {overflow, stg_count} in one copy: a sharded run stops at the first phase whose buffers
-  // overflowed; the hosts share the error with every rank before the next collective
+  // {overflow, stg_count, n_stop} in one copy: a sharded run stops at the first phase whose
+  // buffers overflowed; the hosts share the error with every rank before the next collective
   // (swimhip/sharded.py, status all-gather).
   static_assert(offsetof(Ctl, stg_count) == offsetof(Ctl, overflow) + 4, "Ctl layout");
-  uint32_t ovn[2] = {0u, 0u};
-  HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 8, hipMemcpyDeviceToHost, s));
+  static_assert(offsetof(Ctl, n_stop) == offsetof(Ctl, overflow) + 8, "Ctl layout");
+  uint32_t ovn[3] = {0u, 0u, 0u};
+  HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 12, hipMemcpyDeviceToHost, s));
   HIPC_RC(h, rc, hipStreamSynchronize(s));
   if (ovn[0]) {
     *rc = check_overflow(h);
     return false;
   }
   const uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
-  if (n) (void)hipMemcpyAsync(h->xsend, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
-  HIPC_RC(h, rc, hipMemsetAsync(&P.ctl->stg_count, 0, 4, s));
+  // Once any member left (n_leaving: the same on every rank, swim_leave is collective), each block
+  // starts with a header {gossips, stopped members, 0, 0} and carries the members this shard
+  // stopped (k_leave_stop) after its gossips: liveness is replicated. Block layout:
+  //   [header (leaves only) | gossips 4n | stopped (leaves only) | wlast W32 | bhi | 32 - blo]
+  const uint32_t ns = h->n_leaving ? std::min(ovn[2], P.nloc) : 0u;
+  const uint32_t hdr = h->n_leaving ? 4u : 0u;
+  uint32_t* xs = reinterpret_cast<uint32_t*>(h->xsend);
+  if (hdr) {
+    const uint32_t head[4] = {n, ns, 0u, 0u};
+    HIPC_RC(h, rc, hipMemcpyAsync(xs, head, 16, hipMemcpyHostToDevice, s));
+  }
+  if (n) (void)hipMemcpyAsync(xs + hdr, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
+  if (ns) (void)hipMemcpyAsync(xs + hdr + 4u * n, P.stop_list, (size_t)ns * 4, hipMemcpyDeviceToDevice, s);
+  HIPC_RC(h, rc, hipMemsetAsync(&P.ctl->stg_count, 0, 8, s));  // stg_count and n_stop
   KP Q = P;
-  Q.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-  hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, 4u * n);
+  Q.xsend = xs;
+  hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, hdr + 4u * n + ns);
   HIPC_RC(h, rc, hipStreamSynchronize(s));
   xchg_clear(x, SWIM_X_ALLGATHER, h->world);
-  x->send_words = 4ull * n + h->GC / 32 + 2;
+  x->send_words = hdr + 4ull * n + ns + h->GC / 32 + 2;
   return true;
 }
 
@@ -328,11 +343,26 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   uint32_t total = 0, offs[SWIM_MAX_WORLD];
   const uint64_t tail = h->GC / 32 + 2;  // wlast + bounds after each shard's gossips
   for (uint32_t q = 0; q < h->world; ++q) {
-    const uint32_t c = (uint32_t)((x->recv_counts[q] - tail) / 4);
-    offs[q] = (uint32_t)(q * x->recv_stride + 4ull * c);
+    const uint32_t* blk = xr + q * x->recv_stride;
+    uint32_t c = 0, ns = 0, hdr = 0;
+    if (h->n_leaving) {  // the block's header: gossips and stopped members
+      uint32_t head[2];
+      HIPC(h, hipMemcpyAsync(head, blk, 8, hipMemcpyDeviceToHost, s));
+      HIPC(h, hipStreamSynchronize(s));
+      c = head[0];
+      ns = head[1];
+      hdr = 4u;
+      if (hdr + 4ull * c + ns + tail != x->recv_counts[q])
+        return fail(h, SWIM_EINVAL, "commit exchange: block header does not match its size");
+      if (ns && q != h->rank)
+        hipLaunchKernelGGL(k_stop_remote, dim3(blocks_for(ns, 256)), dim3(256), 0, s, P, blk + hdr + 4u * c, ns);
+    } else {
+      c = (uint32_t)((x->recv_counts[q] - tail) / 4);
+    }
+    offs[q] = (uint32_t)(q * x->recv_stride + hdr + 4ull * c + ns);
     if (c)
       hipLaunchKernelGGL(k_stage_keys, dim3(blocks_for(c, 256)), dim3(256), 0, s, P,
-                         reinterpret_cast<const uint4*>(xr + q * x->recv_stride), c, total, h->ck[0], h->cv[0]);
+                         reinterpret_cast<const uint4*>(blk + hdr), c, total, h->ck[0], h->cv[0]);
     total += c;
   }
   // liveness maxima first: the commit itself then raises the new words on every shard alike
@@ -813,6 +843,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.alive, N);
   ALLOC(P.leaving, N);
   ALLOC(P.stopf, N);
+  ALLOC(P.stop_list, NL);
   ALLOC(P.leave_slot, N);
   ALLOC(P.addr, N);
   ALLOC(P.occ, N);
@@ -1106,7 +1137,6 @@ int swim_set_loss(swim_handle* h, uint32_t loss_bp) {
 int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
   if (!h || mean_ms > 60000) return SWIM_EINVAL;
   KP& P = h->base;
-  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_set_delay: not supported on sharded handles");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_set_delay: a period is in flight");
   if (mean_ms == 0) {  // new messages travel at once; those in flight still arrive (k_gossip_pull)
     P.delay_on = 0;
@@ -1218,7 +1248,6 @@ int swim_block_inbound(swim_handle* h, uint32_t dst, uint32_t src, int blocked) 
 
 int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n) {
   if (!h || (n && !ids)) return SWIM_EINVAL;
-  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_leave: not supported on sharded handles");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_leave: a period is in flight");
   for (uint32_t k = 0; k < n; ++k)
     if (ids[k] >= h->N) return SWIM_EINVAL;
@@ -1331,7 +1360,6 @@ int swim_crash(swim_handle* h, const uint32_t* ids, uint32_t n) {
 
 int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n) {
   if (!h || (n && !ids)) return SWIM_EINVAL;
-  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_update_metadata: not supported on sharded handles");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_update_metadata: a period is in flight");
   for (uint32_t k = 0; k < n; ++k)
     if (ids[k] >= h->N) return SWIM_EINVAL;
@@ -1357,10 +1385,42 @@ int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n) {
 
 int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag) {
   if (!h || origin >= h->N) return SWIM_EINVAL;
-  if (h->world > 1) return fail(h, SWIM_EINVAL, "swim_spread: not supported on sharded handles");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_spread: a period is in flight");
   hipLaunchKernelGGL(k_spread, dim3(1), dim3(64), 0, h->stream, h->base, origin, tag);
   HIPC(h, hipStreamSynchronize(h->stream));
+  HIPC(h, hipGetLastError());
+  return SWIM_OK;
+}
+
+int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subjects, const uint32_t* records,
+                         uint32_t n, uint32_t reason) {
+  if (!h || observer >= h->N || (n && (!subjects || !records))) return SWIM_EINVAL;
+  if (reason != SWIM_R_SYNC && reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC)
+    return fail(h, SWIM_EINVAL, "swim_deliver_records: reason must be SYNC, INITIAL_SYNC or MEMBERSHIP_GOSSIP");
+  for (uint32_t k = 0; k < n; ++k)
+    if (subjects[k] >= h->N || records[k] == SWIM_ABSENT)
+      return fail(h, SWIM_EINVAL, "swim_deliver_records: subject out of range or an absent record");
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_deliver_records: a period is in flight");
+  if (n == 0) return SWIM_OK;
+  if (2ull * n > h->deliver_cap) {
+    uint32_t* d = nullptr;
+    int rc = dalloc(h, &d, 2ull * n);
+    if (rc) return rc;
+    h->deliver_buf = d;
+    h->deliver_cap = 2u * n;
+  }
+  hipStream_t s = h->stream;
+  HIPC(h, hipMemcpyAsync(h->deliver_buf, subjects, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPC(h, hipMemcpyAsync(h->deliver_buf + n, records, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  KP P;
+  set_phase(h, P, 0);  // the coming period: its deadlines, FD tick and first gossip round
+  if (P.nxk) {  // every shard requests (and so allocates) the same columns
+    hipLaunchKernelGGL(k_deliver_track, dim3(1), dim3(256), 0, s, P, h->deliver_buf, h->deliver_buf + n, n);
+    track_commit(h, P);
+  }
+  hipLaunchKernelGGL(k_deliver, dim3(1), dim3(64), 0, s, P, observer, h->deliver_buf, h->deliver_buf + n, n, reason);
+  hipLaunchKernelGGL(k_finalize, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P);
+  HIPC(h, hipStreamSynchronize(s));
   HIPC(h, hipGetLastError());
   return SWIM_OK;
 }
@@ -1741,7 +1801,8 @@ int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv
   // gossip commits: 4 words per staged gossip (x world when gathered); round maxima: W32 + 2
   const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
   const uint64_t rows = (uint64_t)h->scap * (h->base.W + 2ull);
-  const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2;  // commits carry the liveness maxima too
+  // commits carry the liveness maxima too, and once members leave a header and the stopped members
+  const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2 + 4 + nloc;
   // The window bounds assume every pair ships every active word; the need bitmaps ship only the
   // words a receiver lacks something in, far fewer (k_gossip_need), so both buffers are capped at
   // 2^31 words (8 GiB): C4's shards (32,768 rows of 262,144) would otherwise reserve ~90 GB for a

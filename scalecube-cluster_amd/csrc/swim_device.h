@@ -105,11 +105,12 @@ struct Ctl {
   uint32_t due_count;   // subject columns due for the suspicion sweep
   uint32_t overflow;
   uint32_t stg_count;   // gossips staged by emit_gossip since the last commit
+  uint32_t n_stop;      // sharded: local members stopped since the last commit (stop_list)
   uint32_t n_act;       // active bitmap words this round (k_gossip_prep)
   uint32_t w_beg;       // unwrapped index of the live range's first bitmap word this round
   uint32_t n_alist;     // receivers with first receipts this round (k_gossip_pull)
   uint32_t n_inov;      // entries of in_ov this round
-  uint32_t pad[2];
+  uint32_t pad[1];
   uint32_t bl_hist[32]; // alive members per bit_length(others + 1) (spread/sweep bounds)
   // infectedFrom bookkeeping: monotone counters of the record pools, and the
   // pools' fill at the start of each round (mod 256), so an allocation can check that it does
@@ -198,6 +199,8 @@ struct KP {
   uint8_t* alive;
   uint8_t* leaving;      // [N] graceful leave in progress (MembershipProtocolImpl.leaveCluster, :203-212)
   uint8_t* stopf;        // [N] the leave gossip was swept this round: stop at the round's end
+  uint32_t* stop_list;   // [nloc] sharded: members of this shard stopped since the last commit; the
+                         // commit exchange carries them to every shard (alive / occ are replicated)
   uint32_t* leave_slot;  // [N] ring slot of the member's leave gossip (NONE until committed)
   uint32_t* fd_epoch;
   uint32_t* fd_cursor;

@@ -75,6 +75,18 @@ __global__ void k_leave_stop(KP P) {
   }
   P.alive[c] = 0;
   if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
+  if (P.world > 1u) P.stop_list[atomicAdd(&P.ctl->n_stop, 1u)] = c;  // (<= nloc per commit)
+}
+
+// Sharded: members another shard stopped (k_leave_stop) since the last commit, from the commit
+// exchange: the replicated liveness and address state follow (their rows live on that shard)
+__global__ void k_stop_remote(KP P, const uint32_t* ids, uint32_t n) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t c = ids[k];
+  if (c >= P.N || is_local(P, c)) return;
+  P.alive[c] = 0;
+  if (P.occ[P.addr[c]] == c) P.occ[P.addr[c]] = NONE;
 }
 
 // swim_leave: the member's own record becomes DEAD and is staged as a gossip (committed with the
@@ -105,6 +117,37 @@ __global__ void k_spread(KP P, uint32_t origin, uint32_t tag) {  // one wave; la
     created = 1;
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
+}
+
+// swim_deliver_records: an external node's message to member obs before the next period (the wire
+// bridge): updateMembership of each record in order with the message's reason (MPI:463-473,
+// :407-414), accepted SYNC records spread (MPI:649-656). One wave; lane 0 does the work in order.
+// N x K: an untracked subject's BASELINE record is a no-op (equal records never override); the
+// host requested columns for every other record's subject beforehand (k_deliver_track).
+__global__ void k_deliver(KP P, uint32_t obs, const uint32_t* subj, const uint32_t* rec, uint32_t n, uint32_t reason) {
+  Tally T;
+  uint32_t created = 0;
+  if (threadIdx.x == 0 && P.alive[obs] && is_local(P, obs)) {
+    const uint32_t snap = P.cnt[obs];
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint32_t j = subj[k], r1 = rec[k];
+      if (P.nxk && P.colmap[j] == NONE && r1 == BASELINE) continue;
+      const uint32_t r = apply_record(P, obs, j, r1, reason, SWIM_DELIVER_ATTEMPT | k, snap, T);
+      if (r) {
+        emit_gossip(P, obs, j, r, P.gseq[obs]++);
+        ++created;
+      }
+    }
+  }
+  add_stat(P, ST_GOSSIPS_CREATED, created);
+  flush_tally(P, T);
+}
+
+__device__ __forceinline__ void track_request(const KP& P, uint32_t j);
+// N x K: columns for the delivered records' subjects that leave the baseline
+__global__ void k_deliver_track(KP P, const uint32_t* subj, const uint32_t* rec, uint32_t n) {
+  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
+    if (rec[k] != BASELINE) track_request(P, subj[k]);
 }
 
 // swim_update_metadata: MetadataStoreImpl.updateMetadata (a new version of the member's metadata)
@@ -3074,9 +3117,10 @@ __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uin
       P.rpairs[2 * i + 1] = p;
     }
     const uint32_t* hbr = P.hb + lrow(P, p) * W32;
-    // a delivery p will record (infectedFrom, k_gossip_record) needs the whole window
+    // a delivery p will record (infectedFrom, k_gossip_record) needs the whole window; with message
+    // delays every message of the window draws its loss and delay, held gossip or not (k_gossip_pull_dq)
     const bool all = P.alive[p] && P.loss_mode != 2u && link_open(P, P.xrecv[2 * i], p) &&
-                     may_select(P, p, P.xrecv[2 * i]);
+                     (P.delay_on || may_select(P, p, P.xrecv[2 * i]));
     uint32_t cnt[4], pre[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4u; ++j) {

@@ -169,6 +169,7 @@ def api_table(prefix: str):
         (prefix + "update_metadata", _I, [_P, _pU32, _U32]),
         (prefix + "spread", _I, [_P, _U32, _U32]),
         (prefix + "trace", _I, [_P, _U32]),
+        (prefix + "deliver_records", _I, [_P, _U32, _pU32, _pU32, _U32, _U32]),
         (prefix + "step", _I, [_P, _U32]),
         (prefix + "drain_events", _I, [_P, ctypes.POINTER(SwimEvent), _U64, _pU64]),
         (prefix + "read_view", _I, [_P, _U32, _pU32, _U32]),

@@ -191,6 +191,18 @@ class SwimCluster:
         `origin`; every member's first receipt shows up as an EV_GOSSIP event (GossipProtocol.listen)."""
         self._call("spread", self._h, int(origin), int(tag) & 0xFFFFFFFF)
 
+    def deliver_records(self, observer: int, subjects, records, reason: int = nat.R_SYNC):
+        """A message of an external node (decoded by swimhip.wire) delivered to member `observer`
+        before the next period: updateMembership of each (subject, packed record) in order with
+        `reason` (SYNC / INITIAL_SYNC: syncMembership, MembershipProtocolImpl.java:463-473;
+        MEMBERSHIP_GOSSIP: onMembershipGossip, :407-414)."""
+        s = np.ascontiguousarray(np.asarray(list(subjects), dtype=np.uint32))
+        r = np.ascontiguousarray(np.asarray(list(records), dtype=np.uint32))
+        assert s.shape == r.shape
+        P = ctypes.POINTER(ctypes.c_uint32)
+        self._call("deliver_records", self._h, int(observer), s.ctypes.data_as(P), r.ctypes.data_as(P), len(s),
+                   int(reason))
+
     def trace(self, fd: bool = True):
         """FailureDetector.listen() (FailureDetectorImpl.java:365-368) into the event ring as EV_FD."""
         self._call("trace", self._h, nat.TRACE_FD if fd else 0)

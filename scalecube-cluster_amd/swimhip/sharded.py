@@ -48,12 +48,18 @@ class ShardedSwimCluster(SwimCluster):
 
     # -- collectives ---------------------------------------------------------------------
     def _all_gather_ints(self, vals):
-        t = self._torch.tensor(vals, dtype=self._torch.int64)
-        if not self._gloo:
-            t = t.to(self._send.device)
-        out = [self._torch.empty_like(t) for _ in range(self.world)]
-        self._dist.all_gather(out, t, group=self._group)
-        return [o.cpu().tolist() for o in out]
+        """Every rank's row of ints, in rank order: one collective into one tensor and (RCCL) one
+        device-to-host copy, not one per rank."""
+        torch = self._torch
+        t = torch.tensor(vals, dtype=torch.int64)
+        if self._gloo:
+            out = [torch.empty_like(t) for _ in range(self.world)]
+            self._dist.all_gather(out, t, group=self._group)
+            return [o.tolist() for o in out]
+        t = t.to(self._send.device)
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=t.device)
+        self._dist.all_gather_into_tensor(out, t, group=self._group)
+        return out.view(self.world, -1).cpu().tolist()
 
     def _exchange(self, status):
         """The collective the library described; `status` = every rank's [code, op, counts...]

@@ -179,6 +179,25 @@ def _delay(c, mean_ms, loss, n_crash, before, periods, part=0):
         yield
 
 
+def _user_gossips(c, loss):
+    # GossipProtocol.spread (GossipProtocolImpl.java:124-128) of user payloads by several members,
+    # two in the same period, one after a crash, under loss: every first receipt is a
+    # GossipProtocol.listen() event (SWIM_EV_GOSSIP)
+    c.set_loss(loss)
+    c.step(2)
+    yield
+    c.spread(3, 0xA1)
+    c.spread(40, 0xB2)
+    for _ in range(3):
+        c.step(1)
+        yield
+    c.crash([7])
+    c.spread(63, 0xC3)
+    for _ in range(12):
+        c.step(1)
+        yield
+
+
 SCENARIOS = {
     "c1_local32_crash": (ClusterConfig.defaultLocalConfig(), 32, 1, _c1),
     "lan256_loss5_crash3": (ClusterConfig.defaultLanConfig(), 256, 2, lambda c: _lan_loss(c, 3, 40, 5.0)),
@@ -214,6 +233,7 @@ SCENARIOS = {
     # timeout: delays of up to ~30 rounds, most ping round trips time out) with a partition
     "local64_delay100_loss10": (ClusterConfig.defaultLocalConfig(), 64, 16, lambda c: _delay(c, 100, 10.0, 2, 3, 25)),
     "lan256_delay200_crash3": (ClusterConfig.defaultLanConfig(), 256, 17, lambda c: _delay(c, 200, 0.0, 3, 3, 30)),
+    "local64_user_gossips_loss10": (ClusterConfig.defaultLocalConfig(), 64, 20, lambda c: _user_gossips(c, 10.0)),
     "test48_delay30_partition": (
         test_membership_config().membership(lambda o: o.seedMembers(0, 1)),
         48, 18, lambda c: _delay(c, 30, 5.0, 1, 4, 30, part=8)),

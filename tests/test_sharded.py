@@ -119,6 +119,19 @@ def test_shards_match_unsharded(world, names):
     mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,names", [(2, ["local32_leave2", "lan256_leave3_loss5"]),
+                                         (4, ["local64_delay100_loss10", "lan256_delay200_crash3"]),
+                                         (2, ["test48_delay30_partition", "local64_update_metadata"]),
+                                         (4, ["local64_user_gossips_loss10", "local32_leave2"])])
+def test_shard_lifecycle_and_delays_match_unsharded(world, names):
+    """The calls sharded handles now take: graceful leaves (the leaver's shard
+    announces its stop in the next commit exchange; liveness is replicated), message delays (a
+    receiver shard asks for every window word, since every message draws its delay), metadata
+    updates and user gossips. Bit-exact with the unsharded handle, period by period."""
+    mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
+
+
 def _nxk_worker(rank, world, port, names, k):
     import scenarios
     from swimhip import SwimCluster
