@@ -70,7 +70,7 @@ WORKLOADS = {
     # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows
     "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
                     "0.1% simultaneous crash",
-               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 19, scap=4096),
+               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 21, scap=4096),
     # C4's schedule on ONE GPU in N x K mode (the dense 262,144^2 view needs 8 GPUs): measures the
     # storm C4's 1 % loss and 0.1 % crash create, to size C4's ring (1 % loss: one gossip per slot)
     "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
@@ -455,7 +455,7 @@ def main():
         "gossip_slots": {"live_at_end": s1["live_gossip_slots"], "gossips_live_at_end": s1["live_gossip_records"]},
     }
     c.close()
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N = 1 figure
         out["cpu_baseline"] = cpu_baseline(args.workload, args.warmup, args.cpu_budget, args.seed, args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
