@@ -546,7 +546,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
       case PC_SUSP:  // phase G+1: suspicion timeouts
         set_phase(h, P, G + 1);
         memset_ctl_u32(h, offsetof(Ctl, due_count));
-        timed(h, 7, "k_due", [&] { hipLaunchKernelGGL(k_due, dim3(blocks_for(N, 256)), dim3(256), 0, s, P); });
+        timed(h, 7, "k_due", [&] { hipLaunchKernelGGL(k_due, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 3, "k_susp_sweep", [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(2048), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         // phase G+2: SYNC requests

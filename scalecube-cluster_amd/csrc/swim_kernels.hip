@@ -3300,58 +3300,67 @@ __global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
 // ---------------------------------------------------------------------------------------
 // Suspicion timeouts: stream due subject columns of the deadline matrix.
 // ---------------------------------------------------------------------------------------
-__global__ void k_due(KP P) {  // due cells (dense: subjects; N x K: columns)
+// The due cells (dense: subjects; N x K: columns) in ascending order: one workgroup, an ordered
+// compaction (a block scan per 1,024 cells), so that the sweep's chunks of SW_COLS due cells are
+// neighbours in every view row and their cells share lines
+__global__ void __launch_bounds__(1024) k_due(KP P) {
   SWIM_GUARD(P);
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < ncells(P) && P.colmin[j] <= P.period) {
-    const uint32_t idx = atomicAdd(&P.ctl->due_count, 1u);
-    P.due[idx] = j;
-    P.colmin[j] = NONE;  // rebuilt by the sweep from the deadlines it leaves standing
+  __shared__ uint32_t s_lds[16];
+  const uint32_t nc = ncells(P);
+  uint32_t base = 0;
+  for (uint32_t j0 = 0; j0 < nc; j0 += 1024u) {
+    const uint32_t j = j0 + threadIdx.x;
+    const bool due = j < nc && P.colmin[j] <= P.period;
+    uint32_t tot;
+    const uint32_t off = block_excl_scan1024(due ? 1u : 0u, &tot, s_lds);
+    if (due) {
+      P.due[base + off] = j;
+      P.colmin[j] = NONE;  // rebuilt by the sweep from the deadlines it leaves standing
+    }
+    base += tot;
   }
+  if (threadIdx.x == 0) P.ctl->due_count = base;
 }
 
 // onSuspicionTimeout (MembershipProtocolImpl.java:637-647) over the due deadline columns. A
-// workgroup takes 256 consecutive observers x SW_COLS due columns: each thread walks its observer's
-// cells of those columns (the deadline loads of a column are coalesced across the workgroup, and a
-// thread's view writes stay in its own row: one line per cell in dense rows, a few lines for all
-// of an N x K row's 256 columns). Removals are counted per observer in registers (one cnt_delta
-// update per thread, no per-cell atomics) and per column in LDS (one presence / last-removal /
-// column-minimum update per workgroup and column). (The previous column-major sweep, one 4,096-cell
-// piece of one column per workgroup with an atomic per fired cell, measured 7.7 % of HBM peak on
-// C3's converge window and 1.1 % on C5's geometry.)
+// workgroup takes a tile of 256 consecutive observers x SW_COLS consecutive due cells, in two passes:
+//   1. column-major, over the subject-major deadlines: thread t reads observer t's deadline of each
+//      column (a column's 256 deadlines are one coalesced 1-KiB read), clears the fired and the
+//      stopped ones, keeps the fired columns as a 64-bit mask per observer (LDS), and reduces the
+//      standing minimum and the removals per column (per wave, then LDS);
+//   2. row-major, over the observer-major view: wave w takes rows w, w + 4, ...; lane q clears the
+//      row's cell of due column q when it fired. The due cells ascend (k_due), so the lanes of one
+//      store hit neighbouring cells of one row: lines are written once for all the cells they hold,
+//      not once per cell (the previous sweep: one 128-B line per 4-B cell).
+// Removals are counted per observer (one cnt_delta update) and per column (one presence /
+// last-removal / column-minimum update per workgroup and column). MembershipEvents (REMOVED with
+// the removed record) are allocated per wave and row: one atomic per store instruction.
 constexpr uint32_t SW_COLS = 64;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   SWIM_GUARD(P);
-  __shared__ uint32_t s_raw[SW_COLS], s_col[SW_COLS], s_rem[SW_COLS], s_min[SW_COLS];
+  __shared__ uint32_t s_col[SW_COLS], s_rem[SW_COLS], s_min[SW_COLS];
+  __shared__ unsigned long long s_fire[256];
   Tally T;
   uint32_t fired = 0;
-  const uint32_t n = P.ctl->due_count, tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t n = P.ctl->due_count, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t nob = (P.nloc + 255u) / 256u, ncb = (n + SW_COLS - 1u) / SW_COLS;
   for (uint32_t u = blockIdx.x; u < nob * ncb; u += gridDim.x) {
     const uint32_t ob = u % nob, c0 = (u / nob) * SW_COLS;  // neighbouring workgroups: neighbouring observers
     const uint32_t nc = min(SW_COLS, n - c0);
     if (tid < nc) {
-      s_raw[tid] = P.due[c0 + tid];
+      s_col[tid] = P.due[c0 + tid];
       s_rem[tid] = 0u;
       s_min[tid] = NONE;
     }
     __syncthreads();
-    if (tid < nc) {  // the chunk's columns in ascending order: a thread's view writes walk its row forward
-      const uint32_t v = s_raw[tid];
-      uint32_t rank = 0;
-      for (uint32_t t = 0; t < nc; ++t) rank += s_raw[t] < v ? 1u : 0u;
-      s_col[rank] = v;
-    }
-    __syncthreads();
     const uint32_t li = ob * 256u + tid;
-    {  // every lane of the workgroup runs the loop (observers past nloc read nothing): the per-wave
-       // reductions below see whole waves
+    {  // pass 1 (every lane of the workgroup runs the loop: the per-wave reductions see whole waves)
       const bool valid = li < P.nloc;
       const uint32_t i = P.row0 + (valid ? li : 0u);
       const bool alive = valid && P.alive[i] != 0;
-      uint32_t removed = 0;
+      unsigned long long fm = 0ull;  // fired columns of this observer (ordinary cells: pass 2 clears them)
       for (uint32_t k0 = 0; k0 < nc; k0 += 4u) {
-        uint32_t v[4], smin[4] = {NONE, NONE, NONE, NONE}, remm = 0;
+        uint32_t v[4], smin[4] = {NONE, NONE, NONE, NONE};
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q)  // four columns' deadlines in flight
           v[q] = (valid && k0 + q < nc) ? P.dl[(size_t)s_col[k0 + q] * P.nloc + li] : 0u;
@@ -3370,34 +3379,26 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
             continue;
           }
           *dp = 0u;
-          uint32_t* cellp = P.view + (size_t)li * P.W + j;
-          const uint32_t subj = subj_of(P, j);
-          const bool general = subj == i || (P.rerouted && P.addr[subj] == P.addr[i]);  // (never in practice)
-          // A deadline implies a record: every path that clears a cell clears its deadline too
-          // (DEAD accepted, crash, join, leave stop), so without an event to fill (ecap = 0, the
-          // bench) the view read is skipped and the cell just written.
-          const uint32_t r0 = (general || P.ecap) ? *cellp : SWIM_SUSPECT;
-          if (r0 == 0u) continue;
           ++fired;
-          if (general) {
+          const uint32_t subj = subj_of(P, j);
+          if (subj == i || (P.rerouted && P.addr[subj] == P.addr[i])) {  // (never in practice)
             apply_record(P, i, subj, SWIM_DEAD, SWIM_R_SUSPICION_TIMEOUT, 0u, P.cnt[i], T);
             continue;
           }
           // updateMembership(DEAD) -> onDeadMemberDetected (MPI:571-587) as in apply_record, with
-          // the counts applied once per observer and once per column
-          *cellp = SWIM_ABSENT;
-          ++removed;
-          remm |= 1u << q;  // counted per wave below
+          // the counts applied once per observer and once per column. A deadline implies a record:
+          // every path that clears a cell clears its deadline too (DEAD accepted, crash, join, leave
+          // stop), so the cell is present and pass 2 removes it.
+          fm |= 1ull << k;
           T.accepted++;
           T.removed++;
-          push_event(P, i, subj, SWIM_EV_REMOVED, SWIM_R_SUSPICION_TIMEOUT, r0);
         }
         // per column: the wave's removals (one LDS add) and standing minimum (one LDS min)
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q) {
           const uint32_t k = k0 + q;
           if (k >= nc) continue;  // (uniform)
-          const uint32_t nrem = (uint32_t)__popcll(__ballot((remm >> q) & 1u));
+          const uint32_t nrem = (uint32_t)__popcll(__ballot((fm >> k) & 1ull));
           uint32_t mn = smin[q];
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, o, 64));
@@ -3407,7 +3408,44 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
           }
         }
       }
-      if (removed) atomicSub(&P.cnt_delta[i], (int32_t)removed);
+      if (fm) atomicSub(&P.cnt_delta[i], (int32_t)__popcll(fm));
+      s_fire[tid] = fm;
+    }
+    __syncthreads();
+    // pass 2: the fired cells, row by row, lane q on due column q
+    const uint32_t jq = lane < nc ? s_col[lane] : 0u;
+    const uint32_t sq = lane < nc ? subj_of(P, jq) : 0u;
+    for (uint32_t t = wv; t < 256u; t += 4u) {
+      const unsigned long long fm = s_fire[t];  // (the same word for every lane: a broadcast)
+      if (!fm) continue;  // (uniform)
+      const uint32_t lr = ob * 256u + t;
+      const bool f = (fm >> lane) & 1ull;
+      uint32_t* cellp = P.view + (size_t)lr * P.W + jq;
+      uint32_t r0 = 0u;
+      if (f && P.ecap) r0 = *cellp;  // the removed record, for the REMOVED event
+      if (f) *cellp = SWIM_ABSENT;
+      if (P.ecap) {  // one ring allocation per wave and row
+        const unsigned long long b = __ballot(f);
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&P.ctl->event_count, (uint32_t)__popcll(b));
+        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+        if (f) {
+          if (at >= P.ecap) {
+            atomicOr(&P.ctl->overflow, OV_EVENTS);
+          } else {
+            swim_event e;
+            e.period = P.period;
+            e.observer = P.row0 + lr;
+            e.subject = sq;
+            e.record = r0;
+            e.type = (uint8_t)SWIM_EV_REMOVED;
+            e.reason = (uint8_t)SWIM_R_SUSPICION_TIMEOUT;
+            e.phase = (uint8_t)P.phase;
+            e.pad = 0;
+            P.events[at] = e;
+          }
+        }
+      }
     }
     __syncthreads();
     if (tid < nc) {
