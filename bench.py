@@ -76,6 +76,14 @@ WORKLOADS = {
     "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
                        "0.1% simultaneous crash",
                   n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 18, tracked=1024),
+    # C4's schedule on one GPU at the largest sizes one MI355X holds (the 1 % loss storm
+    # keeps ~1.2e6 one-gossip slots live at 262,144 members, which needs the 8-GPU node's rows)
+    "c4d65": dict(desc="C4 schedule on one GPU at 65,536 members: dense N x N views, LAN defaults, 1% loss, "
+                       "0.1% simultaneous crash",
+                  n=65536, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 20),
+    "c4s": dict(desc="C4 schedule on one GPU at 131,072 members: N x K views (K = 24,576), LAN defaults, 1% loss, "
+                     "0.1% simultaneous crash",
+                n=1 << 17, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 20, tracked=24576),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }

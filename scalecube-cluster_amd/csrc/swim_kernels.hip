@@ -3691,6 +3691,30 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
   // Cells the incoming record does not override (the common case) never enter updateMembership.
   const uint32_t nc = ncells(P);
   const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
+  if (per == 4u) {
+    // Most merges change nothing (a converged or converging cluster): first a barrier-free stream
+    // over both rows, four 16-B steps per thread in flight, writing the SYNC_ACK payload as if no
+    // cell were overridden; only a merge with an overriding cell takes the ordered pass below (which
+    // rewrites the payload).
+    bool any = false;
+    for (uint32_t c0 = 0; c0 < nc; c0 += 4096u) {
+      uint4 s4[4], v4[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4u; ++u) {
+        const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
+        s4[u] = c < nc ? *reinterpret_cast<const uint4*>(src + c) : make_uint4(0u, 0u, 0u, 0u);
+        v4[u] = c < nc ? *reinterpret_cast<const uint4*>(row + c) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4u; ++u) {
+        const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
+        any |= (s4[u].x && is_overrides(s4[u].x, v4[u].x)) || (s4[u].y && is_overrides(s4[u].y, v4[u].y)) ||
+               (s4[u].z && is_overrides(s4[u].z, v4[u].z)) || (s4[u].w && is_overrides(s4[u].w, v4[u].w));
+        if (ack_out && c < nc) *reinterpret_cast<uint4*>(ack_out + c) = v4[u];
+      }
+    }
+    if (!__syncthreads_or(any)) return;
+  }
   for (uint32_t c0 = 0; c0 < nc; c0 += 256u * per) {
     const uint32_t c = c0 + per * threadIdx.x;
     uint32_t recs[4], cells[4], nrec = 0;

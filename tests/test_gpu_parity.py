@@ -318,7 +318,7 @@ def test_c3long_schedule_small_parity():
 def test_refused_set_delay_leaves_the_handle_unchanged():
     """A set_delay the device refuses (a mean whose longest delay, in gossip rounds, would outrun the
     256-round head history) must leave the handle as it was: the live threshold table, the ring
-    window and delay_on of the accepted mean. Both sides run 1,000 ms mean delays (LAN: 200 ms
+    window and delay_on of the accepted mean. Both sides run 300 ms mean delays (LAN: 200 ms
     rounds); the device then refuses 3,000 ms with SWIM_EINVAL and must stay bit-exact with the
     oracle, which never saw the refused call."""
     from swimhip import SwimError
@@ -329,7 +329,7 @@ def test_refused_set_delay_leaves_the_handle_unchanged():
     b = OracleCluster(cfg, n, seed=21, event_capacity=1 << 20)
     for c in (a, b):
         c.set_loss(2.0)
-        c.set_delay(1000)
+        c.set_delay(300)
         c.step(3)
     with pytest.raises(SwimError) as ei:
         a.set_delay(3000)

@@ -24,7 +24,7 @@ periods = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 warmup = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 k = int(sys.argv[5]) if len(sys.argv) > 5 else 0
 kw = {"tracked_subjects": k} if k else {}
-c = SwimCluster(bench.preset_config("lan"), n, seed=1, gossip_capacity=1 << lg, sync_capacity=4096, **kw)
+c = SwimCluster(bench.preset_config("lan"), n, seed=1, gossip_capacity=1 << lg, **kw)
 c.set_loss(1.0)
 crashed = bench.crash_set(n, 0.001, 1)
 rows, err, t = [], None, time.time()
