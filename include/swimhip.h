@@ -128,6 +128,11 @@ typedef struct swim_config {
                                no probabilistic loss is set (exact: they travel identically, DESIGN.md
                                §3.12); 1 = one slot per gossip always                             */
   uint32_t record_capacity; /* gossip records live at once in batch slots (power of two; 0 = default) */
+  uint32_t infection_round_bits; /* per (member, ring slot) storage of the gossip's infection round:
+                               8 = the round mod 2^8; 4 = a 4-bit offset from the slot's creation round,
+                               rounds 15 or more after it in an escape table (exact either way; halves the
+                               largest array); 0 = 4 when the 8-bit array would exceed
+                               96 GiB on this handle, else 8 */
 } swim_config;
 
 typedef struct swim_stats {

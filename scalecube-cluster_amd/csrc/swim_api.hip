@@ -434,7 +434,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           HIPC(h, hipMemsetAsync(P.ctl->xg_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         }
         timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
-        timed(h, 8, "k_gossip_select", [&] { hipLaunchKernelGGL(k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 8, "k_gossip_select", [&] {
+          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+        });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
         if (P.dq)  // rings exist once a delay was set; messages in flight arrive even after it is reset
@@ -528,9 +530,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
           if (P.batched)  // batch slots in the ring: expand their records
-            hipLaunchKernelGGL(k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES), h->apply_lds_b, s, P);
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES),
+                               h->apply_lds_b, s, P);
           else
-            hipLaunchKernelGGL(k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS), h->apply_lds, s, P);
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
+                               h->apply_lds, s, P);
         });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
@@ -627,6 +631,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         break;
       case PC_END: {
         if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        if (P.hd4)  // escape entries of swept / rewritten slots become tombstones
+          timed(h, 7, "k_hx_sweep", [&] { hipLaunchKernelGGL(k_hx_sweep, dim3(1024), dim3(256), 0, s, P); });
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
         if (h->base.njoin) {  // the joins of this period are complete
@@ -658,7 +664,8 @@ int check_overflow(swim_handle* h) {
     char buf[320];
     std::snprintf(buf, sizeof buf,
                   "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 apply spill list, "
-                  "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping, 128 N x K columns); infectedFrom "
+                  "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping, 128 N x K columns, 256 infection-round "
+                  "escape table); infectedFrom "
                   "detail 0x%x (1 misprediction, 2 records per pair, 4 pruned pairs, 8 delivery records, 16 in-history)",
                   ov, why);
     return fail(h, SWIM_EOVERFLOW, buf);
@@ -686,7 +693,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
   if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
     return SWIM_EINVAL;
-  if (c.gossip_batching > 1u ||
+  if ((c.infection_round_bits != 0u && c.infection_round_bits != 4u && c.infection_round_bits != 8u) ||
+      c.gossip_batching > 1u ||
       (c.record_capacity && ((c.record_capacity & (c.record_capacity - 1)) || c.record_capacity < 1024u)))
     return SWIM_EINVAL;
   int ndev = 0;
@@ -763,10 +771,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     const uint32_t per_cu_b = std::max<uint32_t>(
         1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
     h->apply_blocks_b = (uint32_t)std::max(1, cus) * per_cu_b;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gossip_apply_b),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
+    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply), reinterpret_cast<const void*>(&k_gossip_apply_h4)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
+    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b), reinterpret_cast<const void*>(&k_gossip_apply_b_h4)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
@@ -826,7 +834,20 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.inbox, NN);
   ALLOC(P.hb, NL * (h->GC / 32));
   ALLOC(P.wb, NL * (h->GC / 32));
-  ALLOC(P.hd, NL * h->GC);
+  // infection rounds: 8 bits per (member, slot), or 4-bit offsets + the escape table
+  P.hd4 = c.infection_round_bits == 4u || (c.infection_round_bits == 0u && NL * (uint64_t)h->GC > (96ull << 30));
+  ALLOC(P.hd, P.hd4 ? NL * h->GC / 2 : NL * h->GC);
+  P.gc8 = nullptr;
+  P.hx = nullptr;
+  P.hxmask = 0;
+  if (P.hd4) {
+    uint8_t* g8 = nullptr;
+    ALLOC(g8, h->GC);
+    P.gc8 = g8;
+    const uint32_t hxcap = pow2ceil(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, NL * 64ull)));
+    ALLOC(P.hx, hxcap);
+    P.hxmask = hxcap - 1u;
+  }
   ALLOC(P.mmin, NL * (h->GC / 32));
   ALLOC(P.mmax, NL * (h->GC / 32));
   ALLOC(P.colmin, P.W);
@@ -879,8 +900,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.scnt, h->GC);
   ALLOC(P.g_create, h->GC);
   ALLOC(P.nb, NL * (h->GC / 32));
-  ALLOC(P.nsum, NL * NSUM);
-  ALLOC(P.lack, NL * NSUM);
+  P.nsumw = std::min<uint32_t>(NSUM, std::max<uint32_t>(1u, h->GC / 1024u));
+  ALLOC(P.nsum, NL * P.nsumw);
+  ALLOC(P.lack, NL * P.nsumw);
   ALLOC(P.lack_round, N);
   ALLOC(P.stg, P.stg_cap);
   ALLOC(P.xg_pend, 2ull * world * NL * c.gossip_fanout);
@@ -989,6 +1011,11 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
   (void)hipMemsetAsync(P.hb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.wb, 0, NL * (h->GC / 32) * 4, s);
+  if (P.hd4) {
+    (void)hipMemsetAsync(P.hd, 0, NL * (h->GC / 2), s);
+    (void)hipMemsetAsync(const_cast<uint8_t*>(P.gc8), 0, h->GC, s);
+    (void)hipMemsetAsync(P.hx, 0, ((size_t)P.hxmask + 1) * 8, s);
+  }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.W, 256)), dim3(256), 0, s, P.colmin, (size_t)P.W, NONE);
   if (P.nxk) {
     hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmap, (size_t)N, NONE);
@@ -1748,7 +1775,24 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
   std::vector<uint2> cref(GC);
   std::vector<uint8_t> d(GC);
   HIPC(h, hipMemcpy(bits.data(), h->base.hb + lr * (GC / 32), (size_t)GC / 8, hipMemcpyDeviceToHost));
-  HIPC(h, hipMemcpy(d.data(), h->base.hd + lr * GC, (size_t)GC, hipMemcpyDeviceToHost));
+  if (!h->base.hd4) {
+    HIPC(h, hipMemcpy(d.data(), h->base.hd + lr * GC, (size_t)GC, hipMemcpyDeviceToHost));
+  } else {  // 4-bit offsets from the slots' creation rounds, 15 = in the escape table
+    std::vector<uint8_t> nib(GC / 2), g8(GC);
+    std::vector<unsigned long long> hx((size_t)h->base.hxmask + 1);
+    HIPC(h, hipMemcpy(nib.data(), h->base.hd + lr * (GC / 2), (size_t)GC / 2, hipMemcpyDeviceToHost));
+    HIPC(h, hipMemcpy(g8.data(), h->base.gc8, (size_t)GC, hipMemcpyDeviceToHost));
+    HIPC(h, hipMemcpy(hx.data(), h->base.hx, hx.size() * 8, hipMemcpyDeviceToHost));
+    for (uint32_t s = 0; s < GC; ++s) {
+      const uint32_t o = (nib[s >> 1] >> (4u * (s & 1u))) & 0xFu;
+      d[s] = (uint8_t)(g8[s] + o);
+      if (o == 15u) {
+        const unsigned long long key = 1ull + (unsigned long long)lr * GC + s;
+        for (const unsigned long long v : hx)
+          if (v != HX_EMPTY && v != HX_TOMB && (v >> 8) == key) d[s] = (uint8_t)(v & 0xFFu);
+      }
+    }
+  }
   HIPC(h, hipMemcpy(cref.data(), h->base.g_cref, (size_t)GC * 8, hipMemcpyDeviceToHost));
   HIPC(h, hipMemcpy(ch.data(), h->base.c_hash, (size_t)CC * 4, hipMemcpyDeviceToHost));
   uint32_t lo = ctl.glo, hi = ctl.gcount, n = 0;

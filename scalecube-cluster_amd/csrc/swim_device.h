@@ -74,6 +74,7 @@ enum Overflow : uint32_t {
   OV_IFROM = 64u,  // infectedFrom bookkeeping out of capacity or a delivery predicted never to
                    // matter did: results would no longer be exact
   OV_TRACK = 128u,  // N x K: more subjects left the baseline than there are columns
+  OV_HDX = 256u,    // 4-bit infection rounds: the escape table of rounds that do not fit is full
 };
 
 // OV_IFROM causes (Ctl::ov_detail), named in the error message
@@ -187,10 +188,17 @@ struct KP {
   uint8_t* mmin;  // [N][GC/32] oldest / newest infection round (mod 2^8) the member holds in the
   uint8_t* mmax;  //            word (valid while it holds any): most MIXED words resolve per member
   uint8_t* hd;   // [N][GC] infection round mod 2^8, valid where the hb bit is set (exact: an
-                 // alive member's held entry is at most sweep+1 <= sweepmax rounds old, < 2^8)
+                 // alive member's held entry is at most sweep+1 <= sweepmax rounds old, < 2^8).
+                 // hd4 handles: [N][GC/2], per slot a 4-bit offset of the round from the slot's
+                 // creation round (gc8); offset 15 = the round is in the escape table hx
+  uint32_t hd4;           // infection rounds stored as 4-bit offsets
+  const uint8_t* gc8;     // [GC] creation round mod 2^8 of each slot (hd4 handles)
+  unsigned long long* hx; // [hxmask + 1] escape table: (1 + local row * GC + slot) << 8 | round; 0 empty
+  uint32_t hxmask;
   uint32_t* wb;  // [N][GC/32] start-of-round window bitmap written by k_gossip_select (act-indexed)
   uint32_t* nb;  // [N][GC/32] first receipts of the round found by k_gossip_pull (act-indexed)
-  uint32_t* nsum;  // [N][NSUM] bit k: nb[k] != 0 this round (written for receivers with receipts)
+  uint32_t nsumw;  // summary words per member: min(NSUM, GC / 1024) (a list has <= GC / 32 positions)
+  uint32_t* nsum;  // [N][nsumw] bit k: nb[k] != 0 this round (written for receivers with receipts)
   uint32_t* lack;  // [N][NSUM] bit k: after its sweep the member lacks a live gossip of word k of
                    // this round's list that someone may send (k_gossip_select); k_gossip_pull visits only those
   uint32_t* lack_round;  // [N] the round `lack` was last written for the member (otherwise no bitmap)
@@ -350,6 +358,7 @@ __device__ __forceinline__ uint32_t cell_get(const KP& P, uint32_t obs, uint32_t
 }
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t NONE_U32 = NONE;
 
 // record dictionary geometry; tests build a variant with a tiny one
 #ifndef SWIM_DICT_SIDS
@@ -459,6 +468,166 @@ __device__ __forceinline__ uint32_t slot_gossips(const KP& P, uint32_t ws, uint3
     n += (r.y - r.x) - SCNT_SAT;
   }
   return n;
+}
+
+// ---- 4-bit infection rounds (hd4 handles) --------------------------------------
+// A holder's infection round of slot s is never before the slot's creation round and, in a storm,
+// a few rounds after it: the offset (round - creation) mod 2^8 is kept in 4 bits, and an offset of
+// 15 or more goes to an open-addressing escape table keyed by (local row, slot). Decoding gives back
+// exactly the bytes an 8-bit handle stores, so every age test is shared. A stale escape entry (its
+// slot swept or rewritten with a small offset) is never read: lookups happen only for nibble 15,
+// which is written together with a fresh entry; k_hx_sweep tombstones stale entries once a period.
+constexpr unsigned long long HX_EMPTY = 0ull, HX_TOMB = ~0ull;
+constexpr uint32_t HX_PROBE = 64;  // linear-probe bound; beyond it OV_HDX
+__device__ __forceinline__ uint32_t hx_home(const KP& P, unsigned long long key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & P.hxmask;
+}
+// the escaped round of (row, slot); writers: the row's own wave (apply / commit), never two at once
+__device__ __forceinline__ void hx_put(const KP& P, size_t row, uint32_t s, uint32_t round) {
+  const unsigned long long key = 1ull + (unsigned long long)row * P.GC + s;
+  const unsigned long long e = (key << 8) | (round & 0xFFu);
+  uint32_t h = hx_home(P, key), tomb = NONE_U32;
+  for (uint32_t k = 0; k < HX_PROBE; ++k, h = (h + 1u) & P.hxmask) {
+    const unsigned long long v = P.hx[h];
+    if (v == HX_TOMB) {
+      if (tomb == NONE_U32) tomb = h;
+      continue;
+    }
+    if (v != HX_EMPTY && (v >> 8) == key) {  // the key's entry: overwrite
+      P.hx[h] = e;
+      return;
+    }
+    if (v == HX_EMPTY) {  // not in the table: take the first tombstone passed, else this slot
+      if (tomb != NONE_U32 && atomicCAS(&P.hx[tomb], HX_TOMB, e) == HX_TOMB) return;
+      if (atomicCAS(&P.hx[h], HX_EMPTY, e) == HX_EMPTY) return;
+      k = 0;  // lost a race for the slot: start over (bounded: each retry fills a slot)
+      h = hx_home(P, key) - 1u;
+      tomb = NONE_U32;
+    }
+  }
+  atomicOr(&P.ctl->overflow, OV_HDX);
+}
+__device__ __forceinline__ uint32_t hx_get(const KP& P, size_t row, uint32_t s) {
+  const unsigned long long key = 1ull + (unsigned long long)row * P.GC + s;
+  uint32_t h = hx_home(P, key);
+  for (uint32_t k = 0; k < HX_PROBE; ++k, h = (h + 1u) & P.hxmask) {
+    const unsigned long long v = P.hx[h];
+    if (v == HX_EMPTY) break;
+    if (v != HX_TOMB && (v >> 8) == key) return (uint32_t)(v & 0xFFu);
+  }
+  atomicOr(&P.ctl->overflow, OV_BUG);  // a nibble 15 always has its entry
+  return 0u;
+}
+// bytes b of a and b added mod 2^8 each
+__device__ __forceinline__ uint32_t bytes_add(uint32_t a, uint32_t b) {
+  return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+}
+// the 32 infection rounds (mod 2^8) of word ws of local row `row`, as hd stores them (byte b of
+// the 8 dwords = slot b); only the bytes of held slots mean anything
+template <bool HD4>
+__device__ __forceinline__ void hd_load32(const KP& P, size_t row, uint32_t ws, uint4& d0, uint4& d1) {
+  if (!HD4) {
+    const uint4* dp = reinterpret_cast<const uint4*>(P.hd + row * P.GC + (size_t)ws * 32u);
+    d0 = dp[0];
+    d1 = dp[1];
+    return;
+  }
+  const uint4 nb = *reinterpret_cast<const uint4*>(P.hd + row * (P.GC / 2u) + (size_t)ws * 16u);
+  const uint4* gp = reinterpret_cast<const uint4*>(P.gc8 + (size_t)ws * 32u);
+  const uint4 g0 = gp[0], g1 = gp[1];
+  const uint32_t n[4] = {nb.x, nb.y, nb.z, nb.w};
+  uint32_t o[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 4u; ++q) {  // nibbles 8q .. 8q+7 -> bytes of dwords 2q, 2q+1
+    const uint32_t lo = n[q] & 0x0F0F0F0Fu, hi = (n[q] >> 4) & 0x0F0F0F0Fu;
+    o[2 * q] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);      // lo.b0 hi.b0 lo.b1 hi.b1
+    o[2 * q + 1] = __builtin_amdgcn_perm(hi, lo, 0x07030602u);  // lo.b2 hi.b2 lo.b3 hi.b3
+  }
+  const uint32_t g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  uint32_t esc[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8u; ++q) {
+    // bytes equal to 15 (escaped): x = o ^ 0x0F is zero there; exact per byte (no borrow crosses)
+    const uint32_t x = o[q] ^ 0x0F0F0F0Fu;
+    esc[q] = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    o[q] = bytes_add(o[q], g[q]);
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 8u; ++q)
+    while (esc[q]) {  // rare: rounds too far from the slot's creation
+      const uint32_t bb = (uint32_t)__builtin_ctz(esc[q]) >> 3;
+      esc[q] &= esc[q] - 1u;
+      const uint32_t r = hx_get(P, row, ws * 32u + 4u * q + bb);
+      o[q] = (o[q] & ~(0xFFu << (8u * bb))) | (r << (8u * bb));
+    }
+  d0 = make_uint4(o[0], o[1], o[2], o[3]);
+  d1 = make_uint4(o[4], o[5], o[6], o[7]);
+}
+// store the rounds d0/d1 (byte per slot) of the slots in `mask` of word ws; the other slots of the
+// word keep what they hold (their bytes in d0/d1 are ignored: hd4 merges nibbles into the stored word)
+template <bool HD4>
+__device__ __forceinline__ void hd_store32(const KP& P, size_t row, uint32_t ws, uint32_t mask, uint4 d0, uint4 d1) {
+  if (!mask) return;
+  if (!HD4) {
+    uint4* dp = reinterpret_cast<uint4*>(P.hd + row * P.GC + (size_t)ws * 32u);
+    if (mask & 0xFFFFu) dp[0] = d0;
+    if (mask >> 16) dp[1] = d1;
+    return;
+  }
+  uint4* np = reinterpret_cast<uint4*>(P.hd + row * (P.GC / 2u) + (size_t)ws * 16u);
+  const uint4* gp = reinterpret_cast<const uint4*>(P.gc8 + (size_t)ws * 32u);
+  const uint4 g0 = gp[0], g1 = gp[1];
+  const uint32_t g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+  const uint32_t d[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+  uint4 cur = make_uint4(0u, 0u, 0u, 0u);
+  if (mask != 0xFFFFFFFFu) cur = *np;
+  uint32_t n[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+  for (uint32_t b = 0; b < 32u; ++b) {
+    if (!((mask >> b) & 1u)) continue;
+    const uint32_t r = (d[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
+    uint32_t off = (r - ((g[b >> 2] >> (8u * (b & 3u))) & 0xFFu)) & 0xFFu;
+    if (off >= 15u) {
+      hx_put(P, row, ws * 32u + b, r);
+      off = 15u;
+    }
+    const uint32_t sh = 4u * (b & 7u);
+    n[b >> 3] = (n[b >> 3] & ~(0xFu << sh)) | (off << sh);
+  }
+  *np = make_uint4(n[0], n[1], n[2], n[3]);
+}
+
+// onGossipReq's new-gossip branch for the slots `bits` of word ws of local row `row`: their
+// infection round becomes `round`; the word's other held slots (`prior`) keep theirs. v0 / v1 are
+// the word's current rounds (8-bit handles: a 16-slot half is rewritten whole, so it needs them
+// when it keeps some; hd4 handles merge nibbles themselves and ignore them).
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t n);
+template <bool HD4>
+__device__ __forceinline__ void hd_receive(const KP& P, size_t row, uint32_t ws, uint32_t bits, uint32_t prior,
+                                           uint4 v0, uint4 v1, uint32_t round) {
+  const uint32_t rb = (round & 0xFFu) * 0x01010101u;
+  if (HD4) {
+    hd_store32<true>(P, row, ws, bits, make_uint4(rb, rb, rb, rb), make_uint4(rb, rb, rb, rb));
+    return;
+  }
+  uint4* dp = reinterpret_cast<uint4*>(P.hd + row * P.GC + (size_t)ws * 32u);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
+    const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
+    if (!nb16) continue;
+    if (!((prior >> (16 * q)) & 0xFFFFu)) {  // nothing held in these 16 slots: bytes of slots not
+      dp[q] = make_uint4(rb, rb, rb, rb);   // held are never read, so no read-modify-write
+      continue;
+    }
+    uint4 v = q == 0 ? v0 : v1;
+    const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
+    const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
+    v.x = (v.x & ~m0) | (rb & m0);
+    v.y = (v.y & ~m1) | (rb & m1);
+    v.z = (v.z & ~m2) | (rb & m2);
+    v.w = (v.w & ~m3) | (rb & m3);
+    dp[q] = v;
+  }
 }
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bm, uint64_t bit) {

@@ -313,8 +313,12 @@ __device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t c0
     atomicAnd(&P.runw[s >> 5], ~(1u << (s & 31u)));
   // a reused word's stale maximum is older than any live creation round, so max() resets it
   if (P.wlast[s >> 5] < P.create_round) atomicMax(&P.wlast[s >> 5], P.create_round);
+  if (P.gc8) const_cast<uint8_t*>(P.gc8)[s] = (uint8_t)P.create_round;  // hd4: the slot's creation round
   if (is_local(P, origin)) {
-    P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
+    if (P.hd4)  // origin's infectionPeriod = the creation round: offset 0 (other nibbles untouched)
+      atomicAnd(reinterpret_cast<uint32_t*>(P.hd) + lrow(P, origin) * (P.GC / 8u) + (s >> 3), ~(0xFu << (4u * (s & 7u))));
+    else
+      P.hd[lrow(P, origin) * P.GC + s] = (uint8_t)P.create_round;  // origin's infectionPeriod
     const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
     if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
     // newest/oldest infection round the origin holds in the word (same value for the batch)
@@ -667,9 +671,10 @@ __global__ void k_commit_wsum(KP P, uint32_t all) {
 // A block for each subject of the commit's records that has none: the CAS winner pops a free
 // block (or takes a new one); when none is left the subject is marked with this commit's
 // no-block tag (its records take the apply kernel's slow path) and is not claimed again until a
-// later commit, so a commit makes at most one failed claim per subject. The high-water mark
-// never passes DICT_SIDS (a bounded increment), so it cannot wrap onto blocks in use. No thread
-// waits on another.
+// later commit, so a commit makes at most one failed claim per subject: the high-water mark passes
+// DICT_SIDS by at most the commit's subjects (< 2^21), and k_dict_entries clamps it back, so it can
+// never wrap onto blocks in use. (A compare-and-swap loop that never passed DICT_SIDS serialized
+// thousands of claims of one storm commit: C3 18.2 -> 20.6 ms/period.) No thread waits on another.
 __global__ void k_dict_claim(KP P) {
   const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0, nfree = P.ctl->d_nfree;
   const uint32_t tag = DICT_NOBLK | (c0 & DICT_TAG_MASK);
@@ -684,16 +689,9 @@ __global__ void k_dict_claim(KP P) {
     uint32_t sid = NONE;
     if (k < nfree) {
       sid = P.d_free[nfree - 1u - k];
-    } else {
-      uint32_t hw = __hip_atomic_load(&P.ctl->d_hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (hw < DICT_SIDS) {
-        const uint32_t seen = atomicCAS(&P.ctl->d_hw, hw, hw + 1u);
-        if (seen == hw) {
-          sid = hw;
-          break;
-        }
-        hw = seen;
-      }
+    } else {  // (one claim per subject and commit: k_dict_entries clamps the mark back to DICT_SIDS)
+      const uint32_t hw = atomicAdd(&P.ctl->d_hw, 1u);
+      if (hw < DICT_SIDS) sid = hw;
     }
     if (sid != NONE) P.d_subj[sid] = subj;
     P.sid_of[subj] = sid != NONE ? sid : tag;
@@ -708,6 +706,7 @@ __global__ void k_dict_entries(KP P) {
     const uint32_t t = P.ctl->d_taken, f = P.ctl->d_nfree;
     P.ctl->d_nfree = f - min(t, f);
     P.ctl->d_taken = 0u;
+    if (P.ctl->d_hw > DICT_SIDS) P.ctl->d_hw = DICT_SIDS;  // failed claims of the last commit
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t x = c0 + i;
@@ -1200,8 +1199,11 @@ __device__ __forceinline__ uint32_t bytes_gt(uint32_t a, uint32_t t);
 // (or committed for round inf), so (t + 1 - inf) mod 2^8 <= 255 - hzn (swim_create checks that
 // sweepmax + hzn < 256, so the two cases cannot alias)
 __device__ __forceinline__ uint32_t state_since(const KP& P, uint32_t m, uint32_t ws, uint32_t t) {
-  const uint4* dp = reinterpret_cast<const uint4*>(P.hd + lrow(P, m) * P.GC + (size_t)ws * 32u);
-  const uint4 d0 = dp[0], d1 = dp[1];
+  uint4 d0, d1;
+  if (P.hd4)
+    hd_load32<true>(P, lrow(P, m), ws, d0, d1);
+  else
+    hd_load32<false>(P, lrow(P, m), ws, d0, d1);
   const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
   uint32_t late = 0;
 #pragma unroll
@@ -1373,7 +1375,8 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 #endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
+template <bool HD4>
+__device__ __forceinline__ void select_body(const KP& P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
@@ -1413,10 +1416,9 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
     const uint32_t spread = spread_rounds(P, others);
     uint32_t* hbr = P.hb + lrow(P, m) * W32;
     uint32_t* wbr = P.wb + lrow(P, m) * W32;
-    const uint8_t* hdr = P.hd + lrow(P, m) * P.GC;
     uint8_t* mminr = P.mmin + lrow(P, m) * W32;
     const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
-    const bool lack_ok = (n_act + 31u) / 32u <= NSUM;  // the list fits the bitmap (as nsum)
+    const bool lack_ok = (n_act + 31u) / 32u <= P.nsumw;  // the list fits the bitmap (as nsum)
     // SEL_BATCH aligned quads of list entries per lane per step: one 16-B list load and (for a
     // quad of consecutive aligned words, the padded layout of k_gossip_prep) one 16-B holdings
     // load each, all issued together (bytes in flight). Words whose class the member's own age
@@ -1519,8 +1521,8 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       }
       // entries one at a time from the mask, the infection rounds (32 B) of the next
       // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
-      auto hd_of = [&](uint32_t e_) {
-        return reinterpret_cast<const uint4*>(hdr + (size_t)((w_beg + (e_ & ACT_OFF_MASK)) & (W32 - 1u)) * 32u);
+      auto hd_ld = [&](uint32_t e_, uint4& a_, uint4& b_) {
+        hd_load32<HD4>(P, lrow(P, m), (w_beg + (e_ & ACT_OFF_MASK)) & (W32 - 1u), a_, b_);
       };
       uint32_t jn = 0, en = 0;
       uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
@@ -1532,15 +1534,13 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
       if (mixm) {
         jn = (uint32_t)__builtin_ctz(mixm);
         en = SEL_ME(jn);
-        n0 = hd_of(en)[0];
-        n1 = hd_of(en)[1];
+        hd_ld(en, n0, n1);
 #if SWIM_SEL_AHEAD >= 2
         rest &= rest - 1u;
         if (rest) {
           jm = (uint32_t)__builtin_ctz(rest);
           em = SEL_ME(jm);
-          m0 = hd_of(em)[0];
-          m1 = hd_of(em)[1];
+          hd_ld(em, m0, m1);
           rest &= rest - 1u;
         }
 #endif
@@ -1559,16 +1559,14 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
         if (rest) {
           jm = (uint32_t)__builtin_ctz(rest);
           em = SEL_ME(jm);
-          m0 = hd_of(em)[0];
-          m1 = hd_of(em)[1];
+          hd_ld(em, m0, m1);
           rest &= rest - 1u;
         }
 #else
         if (mixm) {
           jn = (uint32_t)__builtin_ctz(mixm);
           en = SEL_ME(jn);
-          n0 = hd_of(en)[0];
-          n1 = hd_of(en)[1];
+          hd_ld(en, n0, n1);
         }
 #endif
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
@@ -1628,7 +1626,7 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
           v |= __shfl_xor(v, 2, 64);
           v |= __shfl_xor(v, 4, 64);
           const uint32_t wq = (k0 + 256u * jq) / 32u + lane / 8u;
-          if ((lane & 7u) == 0u && 32u * wq < n_act) P.lack[lrow(P, m) * NSUM + wq] = v;
+          if ((lane & 7u) == 0u && 32u * wq < n_act) P.lack[lrow(P, m) * P.nsumw + wq] = v;
         }
       }
     }
@@ -1800,6 +1798,8 @@ __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
 }
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) { select_body<false>(P); }
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) { select_body<true>(P); }
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
 
@@ -2110,8 +2110,8 @@ __device__ __forceinline__ void pull_body(const KP& P) {
       P.dq_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.dq_head[p];
     // (with delays every message needs its draw, held gossip or not: no skipping)
     const uint32_t* lackr =
-        (!(DQ && P.delay_on) && nsw <= NSUM && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * NSUM : nullptr;
-    if (nsw <= NSUM)
+        (!(DQ && P.delay_on) && nsw <= P.nsumw && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * P.nsumw : nullptr;
+    if (nsw <= P.nsumw)
       for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
@@ -2282,7 +2282,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
             receipts += (uint32_t)__popc(u[i]);
             sbits |= 1u << ((kq + i) & 31u);
           }
-        if (sbits && nsw <= NSUM) atomicOr(&sum[kq >> 5], sbits);
+        if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
             }
 
       __builtin_amdgcn_wave_barrier();  // s_snd is rewritten by the next chunk
@@ -2306,7 +2306,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
         const uint32_t old = atomicOr(&nbr[ap.y], bit);
         if (!(old & bit)) {
           ++receipts;
-          if (nsw <= NSUM) atomicOr(&sum[ap.y >> 5], 1u << (ap.y & 31u));
+          if (nsw <= P.nsumw) atomicOr(&sum[ap.y >> 5], 1u << (ap.y & 31u));
         }
       }
     }
@@ -2316,10 +2316,10 @@ __device__ __forceinline__ void pull_body(const KP& P) {
       P.alist[DBG_IDX(2ull * idx, 2ull * P.N, "pull alist")] = p;
       P.alist[2 * idx + 1] = total;
     }
-    if (total && nsw <= NSUM) {
+    if (total && nsw <= P.nsumw) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      for (uint32_t t = lane; t < nsw; t += 64u) P.nsum[lrow(P, p) * NSUM + t] = sum[t];
+      for (uint32_t t = lane; t < nsw; t += 64u) P.nsum[lrow(P, p) * P.nsumw + t] = sum[t];
     }
   }
   if (lane == 0) P.in_cnt[p] = 0u;  // ready for the next round
@@ -2384,7 +2384,8 @@ __device__ __forceinline__ uint32_t block_excl_scan_part(uint32_t v, uint32_t* t
 // in an LDS hash sized to the receipt count. A subject that finds no slot within HPROBE probes
 // goes to the global inbox instead (consistently for the whole round) and onto an LDS list.
 // Then one updateMembership per subject.
-__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
+template <bool HD4>
+__device__ __forceinline__ void apply_body(const KP& P) {
   SWIM_GUARD(P);
   // dynamic LDS sized for the cluster (apply_lds_words): small clusters get a smaller table and
   // two workgroups per CU; 2^apply_hlog table slots (keys, values), the spill list, and (N <=
@@ -2418,7 +2419,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     // halves take the same compaction path and meet the same barriers)
     // (a half-table must hold the 64-slot minimum: tables of 128 slots and up)
     const bool pair = SWIM_APPLY_PAIR && hcap_log >= 7u && li2 < n_list && 8u * P.alist[2 * li + 1] <= hcap &&
-                      8u * P.alist[2 * li2 + 1] <= hcap && (n_act + 31u) / 32u <= NSUM;  // uniform
+                      8u * P.alist[2 * li2 + 1] <= hcap && (n_act + 31u) / 32u <= P.nsumw;  // uniform
     const uint32_t half = pair ? (threadIdx.x >> 9) : 0u;
     add_stat(P, ST_APPLY_PAIRS, (pair && threadIdx.x == 0u) ? 1u : 0u);
     const uint32_t tid = pair ? (threadIdx.x & 511u) : threadIdx.x, nthr = pair ? 512u : blockDim.x;
@@ -2449,8 +2450,8 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
     // infection rounds, word liveness, and the lattice max per subject, over the words the
     // receipt summary lists (or every active word when the list is too long to summarize)
     const uint32_t nsw = (n_act + 31u) >> 5;
-    const bool summ = nsw <= NSUM;
-    const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
+    const bool summ = nsw <= P.nsumw;
+    const uint32_t* sumr = P.nsum + lrow(P, p) * P.nsumw;
     const uint32_t n_items = summ ? nsw * 32u : n_act;
     // per word with receipts: holdings, liveness, age bounds, infection rounds (32-B read-modify-
     // write), then one representative per subject run into the LDS table
@@ -2462,25 +2463,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
       P.hb[mi] = prior | bits;  // onGossipReq: the receiver now holds them
       P.mmax[mi] = (uint8_t)(r + 1u);
       if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
-      uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {  // 16 slots per 16 B
-        const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
-        if (!nb16) continue;
-        const uint32_t rb = ((r + 1u) & 0xFFu) * 0x01010101u;
-        if (!((prior >> (16 * q)) & 0xFFFFu)) {  // nothing held in these 16 slots: bytes of slots not
-          dp[q] = make_uint4(rb, rb, rb, rb);   // held are never read, so no read-modify-write
-          continue;
-        }
-        uint4 v = q == 0 ? v0 : v1;
-        const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
-        const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
-        v.x = (v.x & ~m0) | (rb & m0);
-        v.y = (v.y & ~m1) | (rb & m1);
-        v.z = (v.z & ~m2) | (rb & m2);
-        v.w = (v.w & ~m3) | (rb & m3);
-        dp[q] = v;
-      }
+      hd_receive<HD4>(P, lrow(P, p), ws, bits, prior, v0, v1, r + 1u);
       // records ascend within a run, so the run's highest receipt carries its lattice max
       rs |= 1u;
       uint32_t left = bits;
@@ -2529,7 +2512,7 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
         }
       }
     };
-    const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
+    const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;  // (8-bit rounds; hd4 merges nibbles in hd_receive)
     // The list positions with receipts, compacted from the summary into the table's unused tail:
     // the table has 2^lg >= 2 * total slots and a receipt word holds >= 1 receipt, so when
     // 2^lg < hcap the <= total positions fit in hcap - 2^lg >= 2^lg slots. Otherwise every summary
@@ -2580,9 +2563,11 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
           pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
           rv[j] = P.runw[wsv[j]];
           // the infection rounds of a 16-slot half are read only when it keeps some (see process)
-          const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
-          if ((bv[j] & 0xFFFFu) && (pv[j] & 0xFFFFu)) v0[j] = dp[0];
-          if ((bv[j] >> 16) && (pv[j] >> 16)) v1[j] = dp[1];
+          if (!HD4) {
+            const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)wsv[j] * 32u);
+            if ((bv[j] & 0xFFFFu) && (pv[j] & 0xFFFFu)) v0[j] = dp[0];
+            if ((bv[j] >> 16) && (pv[j] >> 16)) v1[j] = dp[1];
+          }
         }
       }
 #pragma unroll
@@ -2636,6 +2621,8 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) {
   add_stat(P, ST_GOSSIP_RECEIPTS, nrcpt);
   flush_tally(P, T);
 }
+__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) { apply_body<false>(P); }
+__global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_h4(KP P) { apply_body<true>(P); }
 
 // ---- batch slots: k_gossip_apply for rings that hold gossip batches ----
 // The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
@@ -2683,6 +2670,7 @@ __device__ __forceinline__ uint32_t run_tops(uint32_t bits, uint32_t rs) {
 // onGossipReq's new-gossip branch for one receipt word of receiver p: it holds the slots now
 // (GossipProtocolImpl.java:175-178), with infectionPeriod r + 1, and the word's age bounds and
 // liveness move with them (k_gossip_apply's `process`, without the record merge)
+template <bool HD4>
 __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t ws, uint32_t bits, uint32_t prior,
                                              uint4 v0, uint4 v1) {
   const uint32_t r = P.round, W32 = P.GC >> 5;
@@ -2691,25 +2679,7 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
   P.hb[mi] = prior | bits;
   P.mmax[mi] = (uint8_t)(r + 1u);
   if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);
-  uint4* dp = reinterpret_cast<uint4*>(P.hd + lrow(P, p) * P.GC + (size_t)ws * 32u);
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t nb16 = (bits >> (16 * q)) & 0xFFFFu;
-    if (!nb16) continue;
-    const uint32_t rb = ((r + 1u) & 0xFFu) * 0x01010101u;
-    if (!((prior >> (16 * q)) & 0xFFFFu)) {
-      dp[q] = make_uint4(rb, rb, rb, rb);
-      continue;
-    }
-    uint4 v = q == 0 ? v0 : v1;
-    const uint32_t m0 = nibble_bytes(nb16 & 0xFu), m1 = nibble_bytes((nb16 >> 4) & 0xFu);
-    const uint32_t m2 = nibble_bytes((nb16 >> 8) & 0xFu), m3 = nibble_bytes(nb16 >> 12);
-    v.x = (v.x & ~m0) | (rb & m0);
-    v.y = (v.y & ~m1) | (rb & m1);
-    v.z = (v.z & ~m2) | (rb & m2);
-    v.w = (v.w & ~m3) | (rb & m3);
-    dp[q] = v;
-  }
+  hd_receive<HD4>(P, lrow(P, p), ws, bits, prior, v0, v1, r + 1u);
 }
 
 // k_gossip_apply when the ring holds batch slots (P.batched): a received slot stands for all the
@@ -2744,7 +2714,8 @@ static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range
 #ifndef SWIM_AW_MINW
 #define SWIM_AW_MINW 1
 #endif
-__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(KP P) {
+template <bool HD4>
+__device__ __forceinline__ void apply_b_body(const KP& P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -2789,8 +2760,8 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t nsw = (n_act + 31u) >> 5;
-    const bool summ = nsw <= NSUM;
-    const uint32_t* sumr = P.nsum + lrow(P, p) * NSUM;
+    const bool summ = nsw <= P.nsumw;
+    const uint32_t* sumr = P.nsum + lrow(P, p) * P.nsumw;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
     uint32_t* inrow = P.inbox + lrow(P, p) * P.W;
     if (lane == 0) s_misc[0] = 0u;
@@ -2838,10 +2809,12 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
         const uint32_t prior = P.hb[lrow(P, p) * W32 + ws];
         const uint32_t rs = P.runw[ws];
         uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
-        const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)ws * 32u);
-        if ((bits & 0xFFFFu) && (prior & 0xFFFFu)) v0 = dp[0];
-        if ((bits >> 16) && (prior >> 16)) v1 = dp[1];
-        receive_word(P, p, ws, bits, prior, v0, v1);
+        if (!HD4) {
+          const uint4* dp = reinterpret_cast<const uint4*>(hdrow + (size_t)ws * 32u);
+          if ((bits & 0xFFFFu) && (prior & 0xFFFFu)) v0 = dp[0];
+          if ((bits >> 16) && (prior >> 16)) v1 = dp[1];
+        }
+        receive_word<HD4>(P, p, ws, bits, prior, v0, v1);
 #ifdef SWIM_APPLY_PROF
         atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 14, bits == ~0u ? 1ull : 0ull);
         atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 15, 1ull);
@@ -3054,6 +3027,23 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
   }
 #endif
   flush_tally(P, T);
+}
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(KP P) { apply_b_body<false>(P); }
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_h4(KP P) { apply_b_body<true>(P); }
+
+// hd4 handles, once a period: escape entries whose slot the row no longer holds with nibble 15
+// (swept, or rewritten with a small offset) become tombstones, so the table holds only live escapes
+__global__ void k_hx_sweep(KP P) {
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h <= P.hxmask; h += gridDim.x * blockDim.x) {
+    const unsigned long long v = P.hx[h];
+    if (v == HX_EMPTY || v == HX_TOMB) continue;
+    const unsigned long long key = (v >> 8) - 1ull;
+    const size_t row = (size_t)(key / P.GC);
+    const uint32_t sl = (uint32_t)(key % P.GC);
+    const bool held = (P.hb[row * (P.GC >> 5) + (sl >> 5)] >> (sl & 31u)) & 1u;
+    const uint32_t nib = (P.hd[row * (P.GC / 2u) + (sl >> 1)] >> (4u * (sl & 1u))) & 0xFu;
+    if (!held || nib != 15u) P.hx[h] = HX_TOMB;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3301,20 +3291,35 @@ __global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
 // Suspicion timeouts: stream due subject columns of the deadline matrix.
 // ---------------------------------------------------------------------------------------
 // The due cells (dense: subjects; N x K: columns) in ascending order: one workgroup, an ordered
-// compaction (a block scan per 1,024 cells), so that the sweep's chunks of SW_COLS due cells are
-// neighbours in every view row and their cells share lines
+// compaction in which each thread takes 64 consecutive cells (16-B loads of the column minima, a
+// 64-bit mask of its due cells) and one block scan places them, so the sweep's chunks of SW_COLS due
+// cells are neighbours in every view row and their cells share lines. (65,536 cells per pass.)
 __global__ void __launch_bounds__(1024) k_due(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds[16];
   const uint32_t nc = ncells(P);
   uint32_t base = 0;
-  for (uint32_t j0 = 0; j0 < nc; j0 += 1024u) {
-    const uint32_t j = j0 + threadIdx.x;
-    const bool due = j < nc && P.colmin[j] <= P.period;
+  for (uint32_t j0 = 0; j0 < nc; j0 += 65536u) {
+    const uint32_t c0 = j0 + 64u * threadIdx.x;
+    unsigned long long m = 0ull;
+    if (c0 + 64u <= nc) {
+      const uint4* cp = reinterpret_cast<const uint4*>(P.colmin + c0);
+#pragma unroll
+      for (uint32_t q = 0; q < 16u; ++q) {
+        const uint4 v = cp[q];
+        m |= (unsigned long long)((v.x <= P.period ? 1u : 0u) | (v.y <= P.period ? 2u : 0u) |
+                                  (v.z <= P.period ? 4u : 0u) | (v.w <= P.period ? 8u : 0u)) << (4u * q);
+      }
+    } else {
+      for (uint32_t k = 0; c0 + k < nc && k < 64u; ++k)
+        if (P.colmin[c0 + k] <= P.period) m |= 1ull << k;
+    }
     uint32_t tot;
-    const uint32_t off = block_excl_scan1024(due ? 1u : 0u, &tot, s_lds);
-    if (due) {
-      P.due[base + off] = j;
+    uint32_t o = base + block_excl_scan1024((uint32_t)__popcll(m), &tot, s_lds);
+    while (m) {
+      const uint32_t j = c0 + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+      P.due[o++] = j;
       P.colmin[j] = NONE;  // rebuilt by the sweep from the deadlines it leaves standing
     }
     base += tot;
@@ -3691,11 +3696,15 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
   // Cells the incoming record does not override (the common case) never enter updateMembership.
   const uint32_t nc = ncells(P);
   const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
+  __shared__ uint32_t s_chk[32];  // 1,024-cell chunks with an overridden cell (rows of <= 2^20 cells)
   if (per == 4u) {
     // Most merges change nothing (a converged or converging cluster): first a barrier-free stream
     // over both rows, four 16-B steps per thread in flight, writing the SYNC_ACK payload as if no
-    // cell were overridden; only a merge with an overriding cell takes the ordered pass below (which
-    // rewrites the payload).
+    // cell were overridden; only the 1,024-cell chunks with an overriding cell take the ordered pass
+    // below (which rewrites their payload).
+    __syncthreads();  // every thread is past the previous merge's reads of s_chk
+    if (threadIdx.x < 32u) s_chk[threadIdx.x] = 0u;
+    __syncthreads();
     bool any = false;
     for (uint32_t c0 = 0; c0 < nc; c0 += 4096u) {
       uint4 s4[4], v4[4];
@@ -3708,14 +3717,20 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #pragma unroll
       for (uint32_t u = 0; u < 4u; ++u) {
         const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
-        any |= (s4[u].x && is_overrides(s4[u].x, v4[u].x)) || (s4[u].y && is_overrides(s4[u].y, v4[u].y)) ||
-               (s4[u].z && is_overrides(s4[u].z, v4[u].z)) || (s4[u].w && is_overrides(s4[u].w, v4[u].w));
+        const bool ov = (s4[u].x && is_overrides(s4[u].x, v4[u].x)) || (s4[u].y && is_overrides(s4[u].y, v4[u].y)) ||
+                        (s4[u].z && is_overrides(s4[u].z, v4[u].z)) || (s4[u].w && is_overrides(s4[u].w, v4[u].w));
+        if (ov) {
+          const uint32_t ch = c >> 10;
+          atomicOr(&s_chk[ch >> 5], 1u << (ch & 31u));
+        }
+        any |= ov;
         if (ack_out && c < nc) *reinterpret_cast<uint4*>(ack_out + c) = v4[u];
       }
     }
     if (!__syncthreads_or(any)) return;
   }
   for (uint32_t c0 = 0; c0 < nc; c0 += 256u * per) {
+    if (per == 4u && !((s_chk[c0 >> 15] >> ((c0 >> 10) & 31u)) & 1u)) continue;  // (uniform)
     const uint32_t c = c0 + per * threadIdx.x;
     uint32_t recs[4], cells[4], nrec = 0;
     if (c < nc) {

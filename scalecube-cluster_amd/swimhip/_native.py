@@ -60,6 +60,7 @@ class SwimConfig(ctypes.Structure):
         ("shard_world", ctypes.c_uint32),
         ("gossip_batching", ctypes.c_uint32),
         ("record_capacity", ctypes.c_uint32),
+        ("infection_round_bits", ctypes.c_uint32),
     ]
 
 

@@ -318,9 +318,9 @@ def test_c3long_schedule_small_parity():
 def test_refused_set_delay_leaves_the_handle_unchanged():
     """A set_delay the device refuses (a mean whose longest delay, in gossip rounds, would outrun the
     256-round head history) must leave the handle as it was: the live threshold table, the ring
-    window and delay_on of the accepted mean. Both sides run 300 ms mean delays (LAN: 200 ms
-    rounds); the device then refuses 3,000 ms with SWIM_EINVAL and must stay bit-exact with the
-    oracle, which never saw the refused call."""
+    window and delay_on of the accepted mean. Both sides run 200 ms mean delays (LAN: 200 ms
+    rounds, the lan256_delay200_crash3 shape); the device then refuses 3,000 ms with SWIM_EINVAL and
+    must stay bit-exact with the oracle, which never saw the refused call."""
     from swimhip import SwimError
 
     cfg = ClusterConfig.defaultLanConfig()
@@ -328,8 +328,7 @@ def test_refused_set_delay_leaves_the_handle_unchanged():
     a = SwimCluster(cfg, n, seed=21, event_capacity=1 << 20)
     b = OracleCluster(cfg, n, seed=21, event_capacity=1 << 20)
     for c in (a, b):
-        c.set_loss(2.0)
-        c.set_delay(300)
+        c.set_delay(200)
         c.step(3)
     with pytest.raises(SwimError) as ei:
         a.set_delay(3000)
@@ -363,3 +362,41 @@ def test_nxk_k256_64_concurrent_crashes_match_dense_oracle():
     a, _ = scenarios.run_pair("nxk4096_c5_shape", make_nxk, OracleCluster, compare_every=5)
     st = a.stats()
     assert st["events_removed"] > 200_000  # the 64 columns' suspicion timeouts fired (oracle: 241,919)
+
+
+# 4-bit infection rounds: the same scenarios with every (member, slot) round kept as
+# a 4-bit offset from the slot's creation round and the far ones in the escape table: partitions,
+# delays and rejoins put rounds far from creation (escapes), so both paths run
+HD4 = ["c1_local32_crash", "lan256_loss5_crash3", "local128_partition_heal", "test64_long_partition_rejoin",
+       "local32_asym_partition_loss20", "lan256_leave3_loss5", "local40_restart_join", "local64_delay100_loss10",
+       "test48_delay30_partition", "local64_user_gossips_loss10"]
+
+
+@pytest.mark.parametrize("name", HD4)
+def test_scenario_parity_hd4(name):
+    def make(cfg, n, seed, **kw):
+        return SwimCluster(cfg, n, seed, infection_round_bits=4, **kw)
+
+    scenarios.run_pair(name, make, OracleCluster)
+
+
+def test_c3_schedule_small_parity_hd4():
+    """The C3 storm at N = 1,024 (batched) with 4-bit rounds: the 16-member cut group receives the
+    storm's gossips 40 periods after their creation, through the escape table."""
+    import bench
+
+    cfg = bench.preset_config("lan")
+    n = 1024
+    a = SwimCluster(cfg, n, seed=1, gossip_capacity=1 << 17, infection_round_bits=4)
+    b = OracleCluster(cfg, n, seed=1)
+    for c in (a, b):
+        c.step(3)
+        bench.inject_faults(c, "c3", 3, 1, n=n)
+    for _ in range(12):
+        for c in (a, b):
+            c.step(5)
+        assert a.digest() == b.digest()
+        sa, sb = a.stats(), b.stats()
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}
+    for i in (0, 64, 333, 1023):
+        assert a.debug_holdings(i) == b.debug_holdings(i)
