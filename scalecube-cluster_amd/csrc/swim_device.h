@@ -470,6 +470,8 @@ __device__ __forceinline__ uint32_t slot_gossips(const KP& P, uint32_t ws, uint3
   return n;
 }
 
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t n);
+
 // ---- 4-bit infection rounds (hd4 handles) --------------------------------------
 // A holder's infection round of slot s is never before the slot's creation round and, in a storm,
 // a few rounds after it: the offset (round - creation) mod 2^8 is kept in 4 bits, and an offset of
@@ -523,9 +525,12 @@ __device__ __forceinline__ uint32_t bytes_add(uint32_t a, uint32_t b) {
   return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
 }
 // the 32 infection rounds (mod 2^8) of word ws of local row `row`, as hd stores them (byte b of
-// the 8 dwords = slot b); only the bytes of held slots mean anything
+// the 8 dwords = slot b); only the bytes of held slots mean anything. hd4: escapes are looked up for
+// the slots of `need` only (held slots whose rounds the caller uses: a slot no longer held may keep a
+// stale nibble 15 whose entry is gone)
 template <bool HD4>
-__device__ __forceinline__ void hd_load32(const KP& P, size_t row, uint32_t ws, uint4& d0, uint4& d1) {
+__device__ __forceinline__ void hd_load32(const KP& P, size_t row, uint32_t ws, uint4& d0, uint4& d1,
+                                          uint32_t need = 0xFFFFFFFFu) {
   if (!HD4) {
     const uint4* dp = reinterpret_cast<const uint4*>(P.hd + row * P.GC + (size_t)ws * 32u);
     d0 = dp[0];
@@ -549,7 +554,7 @@ __device__ __forceinline__ void hd_load32(const KP& P, size_t row, uint32_t ws, 
   for (uint32_t q = 0; q < 8u; ++q) {
     // bytes equal to 15 (escaped): x = o ^ 0x0F is zero there; exact per byte (no borrow crosses)
     const uint32_t x = o[q] ^ 0x0F0F0F0Fu;
-    esc[q] = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    esc[q] = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u & nibble_bytes((need >> (4u * q)) & 0xFu);
     o[q] = bytes_add(o[q], g[q]);
   }
 #pragma unroll
@@ -601,7 +606,6 @@ __device__ __forceinline__ void hd_store32(const KP& P, size_t row, uint32_t ws,
 // infection round becomes `round`; the word's other held slots (`prior`) keep theirs. v0 / v1 are
 // the word's current rounds (8-bit handles: a 16-slot half is rewritten whole, so it needs them
 // when it keeps some; hd4 handles merge nibbles themselves and ignore them).
-__device__ __forceinline__ uint32_t nibble_bytes(uint32_t n);
 template <bool HD4>
 __device__ __forceinline__ void hd_receive(const KP& P, size_t row, uint32_t ws, uint32_t bits, uint32_t prior,
                                            uint4 v0, uint4 v1, uint32_t round) {

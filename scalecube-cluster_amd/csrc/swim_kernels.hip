@@ -1198,10 +1198,10 @@ __device__ __forceinline__ uint32_t bytes_gt(uint32_t a, uint32_t t);
 // of round t about them still applies): infection round inf, state created in round inf - 1
 // (or committed for round inf), so (t + 1 - inf) mod 2^8 <= 255 - hzn (swim_create checks that
 // sweepmax + hzn < 256, so the two cases cannot alias)
-__device__ __forceinline__ uint32_t state_since(const KP& P, uint32_t m, uint32_t ws, uint32_t t) {
+__device__ __forceinline__ uint32_t state_since(const KP& P, uint32_t m, uint32_t ws, uint32_t t, uint32_t need) {
   uint4 d0, d1;
-  if (P.hd4)
-    hd_load32<true>(P, lrow(P, m), ws, d0, d1);
+  if (P.hd4)  // (escapes of the slots asked about that m still holds)
+    hd_load32<true>(P, lrow(P, m), ws, d0, d1, need & P.hb[lrow(P, m) * (P.GC >> 5) + ws]);
   else
     hd_load32<false>(P, lrow(P, m), ws, d0, d1);
   const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
@@ -1522,7 +1522,9 @@ __device__ __forceinline__ void select_body(const KP& P) {
       // entries one at a time from the mask, the infection rounds (32 B) of the next
       // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
       auto hd_ld = [&](uint32_t e_, uint4& a_, uint4& b_) {
-        hd_load32<HD4>(P, lrow(P, m), (w_beg + (e_ & ACT_OFF_MASK)) & (W32 - 1u), a_, b_);
+        const uint32_t wi_ = w_beg + (e_ & ACT_OFF_MASK), ws_ = wi_ & (W32 - 1u);
+        // (hd4: escapes of the held live slots only; the holdings word is cache-resident)
+        hd_load32<HD4>(P, lrow(P, m), ws_, a_, b_, HD4 ? hbr[ws_] & range_mask(wi_ << 5, lo, hi) : 0xFFFFFFFFu);
       };
       uint32_t jn = 0, en = 0;
       uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
@@ -1864,7 +1866,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       if (ap.x != P.round || ap.y >= n_act) continue;
       const uint32_t ea = P.act[ap.y];
       if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
-      const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t);
+      const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t, bits);
       if (supp) removed += slot_gossips(P, wi & (W32 - 1u), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
@@ -1903,7 +1905,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
       if (ap.x != r || ap.y >= n_act) continue;
       const uint32_t ea = P.act[ap.y];
       if (((w_beg + (ea & ACT_OFF_MASK)) & (W32 - 1u)) != ws || ((ea >> 26) & 3u) == WC_NONE) continue;
-      const uint32_t supp = (1u << (e.y & 31u)) & state_since(P, sp.x, ws, e.z);
+      const uint32_t supp = (1u << (e.y & 31u)) & state_since(P, sp.x, ws, e.z, 1u << (e.y & 31u));
       if (supp) removed += slot_gossips(P, ws, atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
