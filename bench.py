@@ -84,13 +84,27 @@ WORKLOADS = {
     "c4s": dict(desc="C4 schedule on one GPU at 131,072 members: N x K views (K = 24,576), LAN defaults, 1% loss, "
                      "0.1% simultaneous crash",
                 n=1 << 17, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 20, tracked=24576),
+    # SURVEY §8(d)'s C3 partition as written (half/half by id parity, healed by SYNC) at the largest
+    # sizes one GPU holds: on heal every SYNC re-spreads each accepted SUSPECT record (~0.47 N^2
+    # gossips), held as batches of one origin's records per commit
+    "c3half8k": dict(desc="C3 schedule with the half/half partition at 8,192 members: dense, LAN defaults, 10% "
+                          "simultaneous crash + id-parity partition for 40 periods healed via SYNC",
+                     n=8192, preset="lan", loss=0.0, crash=0.10, part=40, part_group=4096, gcap=1 << 17,
+                     rcap=1 << 26),
+    "c3half16k": dict(desc="C3 schedule with the half/half partition at 16,384 members: dense, LAN defaults, 10% "
+                           "simultaneous crash + id-parity partition for 40 periods healed via SYNC",
+                      n=16384, preset="lan", loss=0.0, crash=0.10, part=40, part_group=8192, gcap=1 << 18,
+                      rcap=1 << 27),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }
 
 
 def partition_groups(n, group_size):
-    """Group 1 = `group_size` members spread evenly over the id space (ids k * n // group_size)."""
+    """Group 1 = `group_size` members spread evenly over the id space (ids k * n // group_size);
+    group_size = n // 2: the 2-way half/half cut by id parity (SURVEY §8(d) C3 as written)."""
+    if 2 * group_size == n:
+        return (np.arange(n) % 2).astype(np.uint8)
     g = np.zeros(n, dtype=np.uint8)
     g[(np.arange(group_size, dtype=np.int64) * n) // group_size] = 1
     return g
@@ -202,6 +216,8 @@ def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batchi
         cfg = cfg.membership(lambda o: o.seedMembers(list(range(w["seeds"]))))
     # one slot per gossip without batches: the ring of round 2's C3 runs
     gcap = w["gcap"] if batching else max(w["gcap"], w.get("gcap_unbatched", 1 << 20))
+    if w.get("rcap"):
+        kw["record_capacity"] = w["rcap"]
     c = cls(cfg, w["n"], seed=seed, gossip_capacity=gcap, device=device, gossip_batching=batching,
             event_capacity=event_capacity, sync_capacity=w.get("scap", 0), **kw)
     if w["loss"]:
