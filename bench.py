@@ -55,11 +55,12 @@ WORKLOADS = {
                     n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
-    # BASELINE configs[4] as stated: needs >= 2 GPUs (the storm keeps ~1.8e5 batch slots live, and
-    # every member keeps an infection round per slot: 2^18 x 2^20 bytes does not fit one GPU)
+    # BASELINE configs[4] as stated, on one GPU with 4-bit infection rounds (auto above 96 GiB of
+    # 8-bit ones: 2^18 slots x 2^20 members x 0.5 B = 128 GiB)
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
                     "crashes (concurrent churn), suspicion-timeout sweep",
-               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
+               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256,
+               rcap=1 << 23),
     # C5's full size with the churn one GPU holds at that size (tests/test_gpu_fullsize.py)
     "c5g": dict(desc="C5 geometry at 1,048,576 members: N x K tracked-subject views (K = 256), LAN defaults, 8 "
                      "simultaneous crashes, suspicion-timeout sweep",
@@ -70,14 +71,15 @@ WORKLOADS = {
     # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows
     "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
                     "0.1% simultaneous crash",
-               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 21, scap=4096),
+               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 22, scap=4096),
     # C4's schedule on ONE GPU in N x K mode (the dense 262,144^2 view needs 8 GPUs): measures the
     # storm C4's 1 % loss and 0.1 % crash create, to size C4's ring (1 % loss: one gossip per slot)
     "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
                        "0.1% simultaneous crash",
                   n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 18, tracked=1024),
-    # C4's schedule on one GPU at the largest sizes one MI355X holds (DESIGN.md §6: the 1 % loss storm
-    # keeps ~1.2e6 one-gossip slots live at 262,144 members, which needs the 8-GPU node's rows)
+    # C4's schedule on one GPU at the largest sizes one MI355X holds (DESIGN.md §6.4: the 1 % loss storm
+    # keeps 1.04e6 one-gossip slots live at 131,072 members, ~4x per doubling: ~4.2e6 at 262,144, the
+    # 2^22-slot ring of the 8-GPU node's shards, with 4-bit infection rounds)
     "c4d65": dict(desc="C4 schedule on one GPU at 65,536 members: dense N x N views, LAN defaults, 1% loss, "
                        "0.1% simultaneous crash",
                   n=65536, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 20),

@@ -157,12 +157,13 @@ def test_membership_gossip_request_round_trip():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tracked", [0, 16])
+@pytest.mark.parametrize("tracked", [0, 48])
 def test_delivered_records_match_oracle(tracked):
     """swim_deliver_records on the GPU equals the oracle's: a real node's SYNC (SUSPECTs, a self
     SUSPECT that forces refutation, an ALIVE of higher incarnation, a DEAD) and a membership-gossip
     GossipRequest delivered between periods, under 10 % loss (metadata fetches draw), then 12 periods
-    stepped: tables, deadlines, events and counters bit-exact (dense, and N x K with 16 columns)."""
+    stepped: tables, deadlines, events and counters bit-exact (dense, and N x K with 48 columns: 10 % loss over 14
+    periods takes ~20 of the 64 subjects off the baseline)."""
     cfg = ClusterConfig.defaultLocalConfig()
     n = 64
     d = wire.Directory(n)

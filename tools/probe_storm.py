@@ -1,5 +1,5 @@
 """Probe: gossip-storm size of a bench workload on the GPU (live gossip slots per period).
-python tools/probe_storm.py [workload] [log2 ring slots] [periods]"""
+python tools/probe_storm.py [workload] [log2 ring slots] [periods] [log2 record capacity]"""
 import os, sys, time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
@@ -10,8 +10,13 @@ from swimhip.cluster import SwimError
 wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
 lg = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 periods = int(sys.argv[3]) if len(sys.argv) > 3 else 60
+if len(sys.argv) > 4:
+    kw_r = {"record_capacity": 1 << int(sys.argv[4])}
+else:
+    kw_r = {}
 w = bench.WORKLOADS[wl]
 kw = {"tracked_subjects": w["tracked"]} if w.get("tracked") else {}
+kw.update(kw_r)
 c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=1 << lg, sync_capacity=w.get("scap", 0), **kw)
 if w["loss"]:
     c.set_loss(w["loss"])
