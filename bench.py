@@ -17,6 +17,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -136,8 +137,9 @@ def kernel_bytes(name, d, rounds_per_period=5):
         if recs:
             return 93 * d["apply_words"] + 8 * d["apply_runs"] + 4 * recs + 12 * d["apply_subjects"]
         return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
-    if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write and
-        return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"]  # the view cell read + write
+    if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write, the
+        # view cell read + write, and (a handle with an event ring) its 24-B REMOVED event
+        return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"] + 24 * d.get("sweep_events", 0)
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
         return 24 * d["fd_probes"]
     # infectedFrom bookkeeping: in-history ring entries (16 B per registration,
@@ -193,6 +195,18 @@ def roofline_of(name, ktimes, d, world, rounds_per_period=5):
     achieved = per_launch / avg_s / 1e9
     return {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": per_launch,
             "avg_launch_ms": avg_s * 1e3, "launches": launches}
+
+
+def hbm_used_gib(device):
+    """Device memory in use (hipMemGetInfo), GiB: the handle's arrays plus the HIP context."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        free, total = ctypes.c_size_t(), ctypes.c_size_t()
+        if hip.hipSetDevice(int(device)) or hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)):
+            return None
+        return round((total.value - free.value) / 2**30, 1)
+    except OSError:
+        return None
 
 
 def log(msg):
@@ -328,6 +342,7 @@ def main():
     ap.add_argument("--converge", type=int, default=120,
                     help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="no MembershipEvent ring (the round-3 bench handle)")
     ap.add_argument("--unbatched", action="store_true", help="one ring slot per gossip (A/B of DESIGN.md §3.12)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -355,8 +370,16 @@ def main():
     n = w["n"]
     pc = preset_config(w["preset"])
     G = pc.failureDetectorConfig().pingInterval() // pc.gossipConfig().gossipInterval()  # rounds per period
-    c = make_cluster(args.workload, local, args.seed, sharded=world > 1, batching=not args.unbatched)
-    log(f"created {args.workload}: N={n}")
+    # the product path emits MembershipEvents (REMOVED from the suspicion sweep): an event ring that
+    # holds one period's worst case (every crashed member removed by every local row), drained (count
+    # and discard, like a listener that only counts) after every period of the converge window
+    n_crash = w["crash_n"] if "crash_n" in w else int(round(n * w["crash"]))
+    ecap = 0 if args.no_events else 1 << max(16, min(29, (max(1, n_crash) * (n // world) - 1).bit_length()))
+    ecap = min(ecap, w.get("ecap", ecap))
+    c = make_cluster(args.workload, local, args.seed, event_capacity=ecap, sharded=world > 1,
+                     batching=not args.unbatched)
+    hbm_used = hbm_used_gib(local)
+    log(f"created {args.workload}: N={n}, event ring {ecap}, HBM used {hbm_used} GiB")
     c.step(args.warmup)
     log(f"warmup {args.warmup} periods done")
     crashed = inject_faults(c, args.workload, args.warmup, args.seed)
@@ -389,6 +412,7 @@ def main():
     ktimes = c.kernel_times()
     c.kernel_timing(False)
     d = {k: s1[k] - s0[k] for k in s1}
+    n_events = c.discard_events() if ecap else 0  # (none expected: no timeout falls due in the window)
 
     # dominant kernel + roofline over the timed region
     dom = max((k for k in ktimes if k != "bookkeeping"), key=lambda k: ktimes[k][0])
@@ -408,12 +432,14 @@ def main():
         extra = 0
         # the suspicion sweep only has work in the periods whose deadlines fall due: its roofline is
         # taken over those launches (one period at a time, kernel-time and sweep_cells deltas)
-        fire_ms, fire_n, fire_cells, fire_dead = 0.0, 0, 0, 0
+        fire_ms, fire_n, fire_cells, fire_dead, fire_ev = 0.0, 0, 0, 0, 0
         st = c.stats()
         while extra < args.converge and st["not_converged"]:
             k0 = c.kernel_times().get("k_susp_sweep", (0.0, 0))
             c.step(1)
             extra += 1
+            ev = c.discard_events() if ecap else 0
+            n_events += ev
             st1 = c.stats()
             k1 = c.kernel_times().get("k_susp_sweep", (0.0, 0))
             if st1["sweep_cells"] > st["sweep_cells"]:
@@ -421,6 +447,7 @@ def main():
                 fire_n += k1[1] - k0[1]
                 fire_cells += st1["sweep_cells"] - st["sweep_cells"]
                 fire_dead += st1["suspicion_timeouts"] - st["suspicion_timeouts"]
+                fire_ev += ev
             st = st1
             if extra % 5 == 0:
                 log(f"converge: +{extra} periods, not_converged={st['not_converged']}")
@@ -433,7 +460,8 @@ def main():
                 for v in [roofline_of(k, kt2, dc, world, G)] if v}
         if fire_n:
             sweep_rl = roofline_of("k_susp_sweep", {"k_susp_sweep": (fire_ms, fire_n)},
-                                   {"sweep_cells": fire_cells, "suspicion_timeouts": fire_dead}, world)
+                                   {"sweep_cells": fire_cells, "suspicion_timeouts": fire_dead,
+                                    "sweep_events": fire_ev * world}, world)
             conv["k_susp_sweep"] = round(sweep_rl["frac"], 4)
         c.kernel_timing(False)
 
@@ -472,7 +500,10 @@ def main():
         "sweep_roofline": None if sweep_rl is None else {
             "achieved": sweep_rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sweep_rl["frac"],
             "bytes_per_launch": sweep_rl["bytes_per_launch"], "avg_launch_ms": sweep_rl["avg_launch_ms"],
-            "launches": sweep_rl["launches"], "window": "the periods whose suspicion deadlines fell due"},
+            "launches": sweep_rl["launches"], "window": "the periods whose suspicion deadlines fell due",
+            "events": "REMOVED events emitted" if ecap else "no event ring (--no-events)"},
+        "events": {"capacity": ecap, "emitted": n_events} if ecap else None,
+        "hbm_used_gib": hbm_used,
         "work": {k: d[k] for k in ("fd_probes", "gossips_created", "gossip_first_receipts", "syncs_delivered",
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",

@@ -309,7 +309,8 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev);
 /* Begin a period (when none is in flight) or resume it after the described exchange. */
 int swim_shard_step(swim_handle* h, swim_xchg* x);
 
-/* Events in canonical order (period, observer, phase, subject, type, reason, record). */
+/* Events in canonical order (period, observer, phase, subject, type, reason, record). buf = NULL
+ * with cap = 0 discards the pending events and returns their count (no copy, no sort). */
 int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);
 /* One observer's membershipTable as packed cells (n = n_members; the observer's shard). */
 int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n);

@@ -1486,6 +1486,13 @@ int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n
   uint32_t cnt = 0;
   HIPC(h, hipMemcpyAsync(&cnt, &h->base.ctl->event_count, 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  if (!buf && cap == 0) {  // count and discard: a consumer that only counts (bench.py's converge window)
+    HIPC(h, hipMemsetAsync(&h->base.ctl->event_count, 0, 4, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    *n_out = std::min(cnt, h->ecap);
+    if (cnt > h->ecap) return fail(h, SWIM_EOVERFLOW, "event buffer overflow");
+    return SWIM_OK;
+  }
   const uint32_t have = std::min(cnt, h->ecap);
   std::vector<swim_event> ev(have);
   if (have) HIPC(h, hipMemcpyAsync(ev.data(), h->base.events, (size_t)have * sizeof(swim_event), hipMemcpyDeviceToHost, h->stream));

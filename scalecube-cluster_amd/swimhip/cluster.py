@@ -270,6 +270,12 @@ class SwimCluster:
             for e in buf[: n.value]
         ]
 
+    def discard_events(self) -> int:
+        """Drop the pending events, returning how many there were (a listener that only counts)."""
+        n = ctypes.c_uint64()
+        self._call("drain_events", self._h, None, 0, ctypes.byref(n))
+        return int(n.value)
+
     # -- MembershipProtocol-shaped accessors (MembershipProtocol.java:14-65) ----------------
     def members(self, observer: int):
         row = self.view(observer)

@@ -133,14 +133,11 @@ def test_c2_convergence_tail_is_fd_driven():
 
 @pytest.mark.parametrize("workload,min_gossips", [("c5s", 100_000), ("c5g", 1_000)])
 def test_c5_shapes_fullsize_properties(workload, min_gossips):
-    """C5's shape (BASELINE configs[4]: N x K views with K = 256, LAN defaults, concurrent crashes,
-    the suspicion-timeout sweep) at the sizes one GPU holds: its full churn (256 simultaneous
-    crashes) at 262,144 members, and its full size (2^20 members) with 8 crashes. The full config
-    (2^20 members AND 256 crashes) needs more than one GPU: its SYNC re-spread storm keeps ~1.8e5
-    gossip batches live (4x the 44,268 measured at 2^18, tools/probe_storm.py), and every member
-    keeps an infection round per live batch slot — 2^18 slots x 2^20 members = 256 GiB of them on
-    one GPU, 32 GiB per GPU on the 8-GPU node C5 names. The SYNC re-spread storm
-    (each accepted SUSPECT record re-gossiped, MembershipProtocolImpl.java:649-656) is held by
+    """C5 (BASELINE configs[4]: 2^20 members, N x K views with K = 256, LAN defaults, 256 concurrent
+    crashes, the suspicion-timeout sweep) as stated, on one GPU with 4-bit infection rounds (the
+    8-bit ones would be 2^18 slots x 2^20 members = 256 GiB), plus its two round-3
+    shapes: the full churn at 262,144 members and the full size with 8 crashes. The SYNC re-spread
+    storm (each accepted SUSPECT record re-gossiped, MembershipProtocolImpl.java:649-656) is held by
     gossip batches. After 120 periods every crashed member is gone from every
     alive view (suspicion timeout 95 / 105 periods), no alive member was removed, no buffer
     overflowed, and a second handle with the same seed reaches the same digests and counters."""
@@ -172,6 +169,48 @@ def test_c5_shapes_fullsize_properties(workload, min_gossips):
     assert st["events_removed"] == len(crashed) * n_alive
     assert np.all(row[crashed] == 0) and np.all(row[alive] != 0)
     d2, _, st2, _, _, _ = run()
+    assert d1 == d2
+    assert {k: st[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")} == \
+           {k: st2[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")}
+
+
+@pytest.mark.parametrize("workload", ["c4d65"])
+def test_c4_schedule_fullsize_properties(workload):
+    """C4's schedule (BASELINE configs[3]: LAN defaults, 1 % uniform loss, 0.1 % simultaneous crash)
+    dense at 65,536 members, the largest dense size one GPU holds with the lossy storm's ring
+    (DESIGN.md §6.4). Under probabilistic loss every gossip is its own ring slot (one GossipRequest
+    per gossip, each lost independently: GossipProtocolImpl.java:225-239), and false suspicions
+    re-spread by every SYNC make the storm (MembershipProtocolImpl.java:649-656). After 125 periods
+    every crashed member is gone from every alive view, no alive member was removed (each false
+    suspicion was refuted), no buffer overflowed, and a second handle reaches the same digests."""
+    w = bench.WORKLOADS[workload]
+    n = w["n"]
+
+    def run():
+        c = bench.make_cluster(workload, 0, seed=1)
+        c.step(3)
+        crashed = bench.inject_faults(c, workload, 3, 1)
+        c.step(10)
+        mid = c.stats()
+        c.step(115)
+        out = (c.digest(), mid, c.stats(), c.presence(), crashed)
+        c.close()
+        return out
+
+    d1, mid, st, (pres, last), crashed = run()
+    alive = np.ones(n, dtype=bool)
+    alive[crashed] = False
+    n_alive = int(alive.sum())
+    assert len(crashed) == round(n * w["crash"])
+    assert st["overflow"] == 0
+    assert mid["live_gossip_slots"] > 50_000 and mid["live_gossip_slots"] == mid["live_gossip_records"]
+    assert st["fd_suspect_events"] > 10 * len(crashed)  # false suspicions under 1 % loss
+    assert st["refutations"] > 0
+    assert st["not_converged"] == 0
+    assert np.all(pres[crashed] == 0)
+    assert np.all(pres[alive] == n_alive - 1) and np.all(last[alive] == 0)
+    assert st["events_removed"] == len(crashed) * n_alive
+    d2, _, st2, _, _ = run()
     assert d1 == d2
     assert {k: st[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")} == \
            {k: st2[k] for k in ("gossips_created", "gossip_first_receipts", "gossip_sends", "events_removed")}
