@@ -18,6 +18,10 @@
 
 using namespace swim;
 
+#ifndef SWIM_LOSSY_DICT
+#define SWIM_LOSSY_DICT 0
+#endif
+
 namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
@@ -529,7 +533,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
-          if (P.batched)  // batch slots in the ring: expand their records
+          if (P.batched || (SWIM_LOSSY_DICT && h->dict_on))  // batch slots in the ring: expand their records
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES),
                                h->apply_lds_b, s, P);
           else
@@ -661,7 +665,7 @@ int check_overflow(swim_handle* h) {
   HIPC(h, hipMemcpyAsync(&why, &h->base.ctl->ov_detail, 4, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   if (ov) {
-    char buf[320];
+    char buf[512];
     std::snprintf(buf, sizeof buf,
                   "simulator buffer overflow mask 0x%x (1 events, 2 gossip slots, 4 sync staging, 8 apply spill list, "
                   "16 sync bucket, 32 invariant, 64 infectedFrom bookkeeping, 128 N x K columns, 256 infection-round "

@@ -3341,12 +3341,15 @@ __global__ void __launch_bounds__(1024) k_due(KP P) {
 //      not once per cell (the previous sweep: one 128-B line per 4-B cell).
 // Removals are counted per observer (one cnt_delta update) and per column (one presence /
 // last-removal / column-minimum update per workgroup and column). MembershipEvents (REMOVED with
-// the removed record) are allocated per wave and row: one atomic per store instruction.
+// the removed record) are allocated per workgroup and tile: a block scan of the rows' fired counts
+// and one atomic on the ring's counter (an atomic per wave and row serialised ~10^6 times per launch
+// on that one word: 4.7 ms per C3 firing launch instead of ~0.5).
 constexpr uint32_t SW_COLS = 64;
 __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_col[SW_COLS], s_rem[SW_COLS], s_min[SW_COLS];
   __shared__ unsigned long long s_fire[256];
+  __shared__ uint32_t s_eoff[256], s_scan[4], s_ebase;
   Tally T;
   uint32_t fired = 0;
   const uint32_t n = P.ctl->due_count, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -3417,6 +3420,11 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
       }
       if (fm) atomicSub(&P.cnt_delta[i], (int32_t)__popcll(fm));
       s_fire[tid] = fm;
+      if (P.ecap) {  // the tile's events: row offsets by a block scan, one ring allocation
+        uint32_t tot;
+        s_eoff[tid] = block_excl_scan1024((uint32_t)__popcll(fm), &tot, s_scan);
+        if (tid == 0) s_ebase = tot ? atomicAdd(&P.ctl->event_count, tot) : 0u;
+      }
     }
     __syncthreads();
     // pass 2: the fired cells, row by row, lane q on due column q
@@ -3431,11 +3439,8 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
       uint32_t r0 = 0u;
       if (f && P.ecap) r0 = *cellp;  // the removed record, for the REMOVED event
       if (f) *cellp = SWIM_ABSENT;
-      if (P.ecap) {  // one ring allocation per wave and row
-        const unsigned long long b = __ballot(f);
-        uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(&P.ctl->event_count, (uint32_t)__popcll(b));
-        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+      if (P.ecap) {
+        const uint32_t at = s_ebase + s_eoff[t] + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
         if (f) {
           if (at >= P.ecap) {
             atomicOr(&P.ctl->overflow, OV_EVENTS);
