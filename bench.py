@@ -219,7 +219,7 @@ def preset_config(preset):
     return {"lan": ClusterConfig.defaultLanConfig, "local": ClusterConfig.defaultLocalConfig}[preset]()
 
 
-def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batching=True):
+def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batching=True, **extra):
     """One cluster of the workload: on this GPU alone, or (sharded) this rank's observer rows of
     a cluster spread over the torch.distributed world."""
     from swimhip import ShardedSwimCluster, SwimCluster
@@ -234,6 +234,7 @@ def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batchi
     gcap = w["gcap"] if batching else max(w["gcap"], w.get("gcap_unbatched", 1 << 20))
     if w.get("rcap"):
         kw["record_capacity"] = w["rcap"]
+    kw.update(extra)
     c = cls(cfg, w["n"], seed=seed, gossip_capacity=gcap, device=device, gossip_batching=batching,
             event_capacity=event_capacity, sync_capacity=w.get("scap", 0), **kw)
     if w["loss"]:
@@ -343,6 +344,8 @@ def main():
                     help="untimed periods after the timed region to measure periods-to-DEAD (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="no MembershipEvent ring (the round-3 bench handle)")
+    ap.add_argument("--infection-round-bits", type=int, default=0, choices=[0, 4, 8],
+                    help="per (member, slot) infection rounds: 0 = the library's choice (DESIGN.md §4.4)")
     ap.add_argument("--unbatched", action="store_true", help="one ring slot per gossip (A/B of DESIGN.md §3.12)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -376,8 +379,9 @@ def main():
     n_crash = w["crash_n"] if "crash_n" in w else int(round(n * w["crash"]))
     ecap = 0 if args.no_events else 1 << max(16, min(29, (max(1, n_crash) * (n // world) - 1).bit_length()))
     ecap = min(ecap, w.get("ecap", ecap))
+    extra = {"infection_round_bits": args.infection_round_bits} if args.infection_round_bits else {}
     c = make_cluster(args.workload, local, args.seed, event_capacity=ecap, sharded=world > 1,
-                     batching=not args.unbatched)
+                     batching=not args.unbatched, **extra)
     hbm_used = hbm_used_gib(local)
     log(f"created {args.workload}: N={n}, event ring {ecap}, HBM used {hbm_used} GiB")
     c.step(args.warmup)

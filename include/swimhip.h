@@ -182,6 +182,9 @@ typedef struct swim_stats {
                                  metadata differs from the stored one (MembershipProtocolImpl.java:589-610) */
   uint64_t apply_pairs;       /* receiver pairs k_gossip_apply processed two to a workgroup; 0 in the oracle */
   uint64_t commit_radix;      /* commit phases sorted by the chip-wide radix sort; 0 in the oracle      */
+  uint64_t escape_entries;    /* 4-bit infection rounds: live escape-table entries after the last period's
+                                 sweep; 0 in the oracle and on 8-bit handles */
+  uint64_t escape_capacity;   /* the escape table's entries (0 on 8-bit handles)                      */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;

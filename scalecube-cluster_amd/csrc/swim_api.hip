@@ -635,8 +635,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         break;
       case PC_END: {
         if (W > 1 && (rc = commit_end(h, P, x))) return rc;
-        if (P.hd4)  // escape entries of swept / rewritten slots become tombstones
+        if (P.hd4) {  // escape entries of swept / rewritten slots become tombstones
+          memset_ctl_u32(h, offsetof(Ctl, hx_live));
           timed(h, 7, "k_hx_sweep", [&] { hipLaunchKernelGGL(k_hx_sweep, dim3(1024), dim3(256), 0, s, P); });
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(h, SWIM_EHIP, std::string("kernel launch: ") + hipGetErrorString(e));
         if (h->base.njoin) {  // the joins of this period are complete
@@ -848,7 +850,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     uint8_t* g8 = nullptr;
     ALLOC(g8, h->GC);
     P.gc8 = g8;
-    const uint32_t hxcap = pow2ceil(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1ull << 20, NL * 64ull)));
+    // 256 entries per local row, 2^20 .. 2^27 (8 B each: <= 1 GiB)
+    const uint32_t hxcap = pow2ceil(std::min<uint64_t>(1ull << 27, std::max<uint64_t>(1ull << 20, NL * 256ull)));
     ALLOC(P.hx, hxcap);
     P.hxmask = hxcap - 1u;
   }
@@ -1679,6 +1682,8 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->events_updated = stats[ST_UPDATED];
   out->apply_pairs = stats[ST_APPLY_PAIRS];
   out->commit_radix = stats[ST_COMMIT_RADIX];
+  out->escape_entries = ctl.hx_live;
+  out->escape_capacity = h->base.hd4 ? (uint64_t)h->base.hxmask + 1u : 0u;
   {  // gossips in the live slots: the record ring from the oldest live slot's first record
     uint32_t c_lo = ctl.ccount;
     if (ctl.gcount != ctl.glo && ctl.gcount - ctl.glo <= h->GC) {

@@ -111,7 +111,7 @@ struct Ctl {
   uint32_t w_beg;       // unwrapped index of the live range's first bitmap word this round
   uint32_t n_alist;     // receivers with first receipts this round (k_gossip_pull)
   uint32_t n_inov;      // entries of in_ov this round
-  uint32_t pad[1];
+  uint32_t hx_live;     // hd4: escape entries left by the last k_hx_sweep (a gauge)
   uint32_t bl_hist[32]; // alive members per bit_length(others + 1) (spread/sweep bounds)
   // infectedFrom bookkeeping: monotone counters of the record pools, and the
   // pools' fill at the start of each round (mod 256), so an allocation can check that it does

@@ -3036,6 +3036,7 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_
 // hd4 handles, once a period: escape entries whose slot the row no longer holds with nibble 15
 // (swept, or rewritten with a small offset) become tombstones, so the table holds only live escapes
 __global__ void k_hx_sweep(KP P) {
+  uint32_t live = 0;
   for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h <= P.hxmask; h += gridDim.x * blockDim.x) {
     const unsigned long long v = P.hx[h];
     if (v == HX_EMPTY || v == HX_TOMB) continue;
@@ -3044,8 +3045,15 @@ __global__ void k_hx_sweep(KP P) {
     const uint32_t sl = (uint32_t)(key % P.GC);
     const bool held = (P.hb[row * (P.GC >> 5) + (sl >> 5)] >> (sl & 31u)) & 1u;
     const uint32_t nib = (P.hd[row * (P.GC / 2u) + (sl >> 1)] >> (4u * (sl & 1u))) & 0xFu;
-    if (!held || nib != 15u) P.hx[h] = HX_TOMB;
+    if (!held || nib != 15u)
+      P.hx[h] = HX_TOMB;
+    else
+      ++live;
   }
+  // the live entries (the table's load: SWIM_EOVERFLOW mask 256 once an insert probes 64 slots)
+  uint32_t wl;
+  (void)wave_excl_scan(live, &wl);
+  if ((threadIdx.x & 63u) == 0u && wl) atomicAdd(&P.ctl->hx_live, wl);
 }
 
 // ---------------------------------------------------------------------------------------

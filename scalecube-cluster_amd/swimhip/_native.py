@@ -119,6 +119,8 @@ STAT_FIELDS = [
     "events_updated",
     "apply_pairs",
     "commit_radix",
+    "escape_entries",
+    "escape_capacity",
 ]
 
 

@@ -42,7 +42,7 @@ for p in range(warmup + periods):
     s = c.stats()
     row = {"period": p, "created": s["gossips_created"] - prev, "live": s["live_gossip_records"],
            "received": s["gossip_first_receipts"], "sends": s["gossip_sends"],
-           "slots": s["live_gossip_slots"], "fd_suspect": s["fd_suspect_events"], "removed": s["events_removed"],
+           "slots": s["live_gossip_slots"], "escapes": s["escape_entries"], "fd_suspect": s["fd_suspect_events"], "removed": s["events_removed"],
            "dt": round(time.time() - t1, 3)}
     prev = s["gossips_created"]
     rows.append(row)
