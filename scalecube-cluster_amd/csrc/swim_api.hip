@@ -855,8 +855,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.hx, hxcap);
     P.hxmask = hxcap - 1u;
   }
-  ALLOC(P.mmin, NL * (h->GC / 32));
-  ALLOC(P.mmax, NL * (h->GC / 32));
+  ALLOC(P.mm, NL * (h->GC / 32));
   ALLOC(P.colmin, P.W);
   if (P.nxk) {
     ALLOC(P.colmap, N);

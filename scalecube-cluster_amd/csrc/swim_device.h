@@ -185,8 +185,9 @@ struct KP {
   uint32_t* colmin;
   uint32_t* inbox;
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
-  uint8_t* mmin;  // [N][GC/32] oldest / newest infection round (mod 2^8) the member holds in the
-  uint8_t* mmax;  //            word (valid while it holds any): most MIXED words resolve per member
+  uint16_t* mm;   // [N][GC/32] oldest (low byte) / newest (high byte) infection round (mod 2^8) the
+                  // member holds in the word (valid while it holds any): most MIXED words resolve per
+                  // member. One u16 per (member, word): a receipt word touches one line for both
   uint8_t* hd;   // [N][GC] infection round mod 2^8, valid where the hb bit is set (exact: an
                  // alive member's held entry is at most sweep+1 <= sweepmax rounds old, < 2^8).
                  // hd4 handles: [N][GC/2], per slot a 4-bit offset of the round from the slot's
@@ -345,6 +346,14 @@ struct KP {
 
 __device__ __forceinline__ size_t lrow(const KP& P, uint32_t m) { return (size_t)(m - P.row0); }
 __device__ __forceinline__ bool is_local(const KP& P, uint32_t m) { return m - P.row0 < P.nloc; }
+// a receipt of word `mi` at infection round `round`: the newest round the member holds in the word,
+// and (first holding: `first`) the oldest too — one u16 store, else the high byte alone
+__device__ __forceinline__ void mm_received(const KP& P, size_t mi, bool first, uint32_t round) {
+  if (first)
+    P.mm[mi] = (uint16_t)((round & 0xFFu) * 0x101u);
+  else
+    reinterpret_cast<uint8_t*>(P.mm)[2u * mi + 1u] = (uint8_t)round;
+}
 
 // the cell of subject j in a row (dense: j itself; N x K: its column or NONE while untracked)
 __device__ __forceinline__ uint32_t col_of(const KP& P, uint32_t j) { return P.nxk ? P.colmap[j] : j; }

@@ -322,8 +322,7 @@ __device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t c0
     const uint32_t old = atomicOr(&P.hb[lrow(P, origin) * W32 + (s >> 5)], 1u << (s & 31u));
     if (!(old & (1u << (s & 31u)))) atomicAdd(&P.held[origin], 1u);
     // newest/oldest infection round the origin holds in the word (same value for the batch)
-    P.mmax[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
-    if (old == 0u) P.mmin[lrow(P, origin) * W32 + (s >> 5)] = (uint8_t)P.create_round;
+    mm_received(P, lrow(P, origin) * W32 + (s >> 5), old == 0u, P.create_round);
   }
 }
 
@@ -1416,8 +1415,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
     const uint32_t spread = spread_rounds(P, others);
     uint32_t* hbr = P.hb + lrow(P, m) * W32;
     uint32_t* wbr = P.wb + lrow(P, m) * W32;
-    uint8_t* mminr = P.mmin + lrow(P, m) * W32;
-    const uint8_t* mmaxr = P.mmax + lrow(P, m) * W32;
+    uint16_t* mmr = P.mm + lrow(P, m) * W32;
     const bool lack_ok = (n_act + 31u) / 32u <= P.nsumw;  // the list fits the bitmap (as nsum)
     // SEL_BATCH aligned quads of list entries per lane per step: one 16-B list load and (for a
     // quad of consecutive aligned words, the padded layout of k_gossip_prep) one 16-B holdings
@@ -1485,7 +1483,8 @@ __device__ __forceinline__ void select_body(const KP& P) {
           uint32_t wcm = wc, scm = sc;
           if (wcm == WC_MIXED || scm == WC_MIXED) {
             // this member's own age range in the word: [r - newest, r - oldest] (mod 2^8)
-            const uint32_t amin = (r - mmaxr[ws]) & 0xFFu, amax = (r - mminr[ws]) & 0xFFu;
+            const uint32_t mmv = mmr[ws];
+            const uint32_t amin = (r - (mmv >> 8)) & 0xFFu, amax = (r - mmv) & 0xFFu;
             if (wcm == WC_MIXED) wcm = amin > spread ? WC_NONE : (amax <= spread ? WC_ALL : WC_MIXED);
             if (scm == WC_MIXED) scm = amax <= sweep ? WC_NONE : (amin > sweep ? WC_ALL : WC_MIXED);
           }
@@ -1605,7 +1604,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
             oldest_kept = max(oldest_kept, max(max(a & 0xFFu, (a >> 8) & 0xFFu), max((a >> 16) & 0xFFu, a >> 24)));
           }
         }
-        if (clear && (held & ~clear)) mminr[ws] = (uint8_t)(r - oldest_kept);
+        if (clear && (held & ~clear)) reinterpret_cast<uint8_t*>(mmr)[2u * ws] = (uint8_t)(r - oldest_kept);  // oldest
         if (clear) {
           hbr[ws] = word & ~clear;
           nclear += (uint32_t)__popc(clear);
@@ -2463,8 +2462,7 @@ __device__ __forceinline__ void apply_body(const KP& P) {
       if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
       const size_t mi = lrow(P, p) * W32 + ws;
       P.hb[mi] = prior | bits;  // onGossipReq: the receiver now holds them
-      P.mmax[mi] = (uint8_t)(r + 1u);
-      if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);  // the word held nothing before
+      mm_received(P, mi, prior == 0u, r + 1u);  // (prior == 0: the word held nothing before)
       hd_receive<HD4>(P, lrow(P, p), ws, bits, prior, v0, v1, r + 1u);
       // records ascend within a run, so the run's highest receipt carries its lattice max
       rs |= 1u;
@@ -2679,8 +2677,7 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
   if (P.wlast[ws] < r + 1u) atomicMax(&P.wlast[ws], r + 1u);
   const size_t mi = lrow(P, p) * W32 + ws;
   P.hb[mi] = prior | bits;
-  P.mmax[mi] = (uint8_t)(r + 1u);
-  if (prior == 0u) P.mmin[mi] = (uint8_t)(r + 1u);
+  mm_received(P, mi, prior == 0u, r + 1u);
   hd_receive<HD4>(P, lrow(P, p), ws, bits, prior, v0, v1, r + 1u);
 }
 

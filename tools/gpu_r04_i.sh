@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4, session I: the one-gossip-slot storm (C4's 1 % loss) through the dictionary apply — parity
 # file on that build, then C4's schedule at 65,536 with each build; the product's parity file (the
-# sweep's events now allocated per workgroup tile) and C3's converge window with the event ring.
+# sweep's events now allocated per workgroup tile, age bounds as one u16 per word) and C3 (base build vs
+# this tree; its converge window with the event ring).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_i
@@ -17,5 +18,8 @@ done
 timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 \
    --timeout-method thread > $out/pytest_parity.log 2>&1
 rc=$?; echo "pytest product rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+SWIMHIP_LIB=$PWD/variants_ab/libswimhip_base.so timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+   --converge 0 > $out/bench_c3_base.json 2> $out/bench_c3_base.err
+rc=$?; echo "c3 base rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $out/bench_c3.json 2> $out/bench_c3.err
 rc=$?; echo "c3 rc=$rc" >> $out/status.log; exit $rc
