@@ -479,7 +479,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong",  # the one cluster of the workload, its observers split over the GPUs
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (converged start, Philox-chosen crash set, seeded)",
