@@ -56,12 +56,14 @@ WORKLOADS = {
                     n=65536, preset="lan", loss=0.0, crash=0.10, part=0, gcap=1 << 17, scap=8192),
     "c2": dict(desc="C2: 4,096 members, dense N x N views, LAN defaults, 5% uniform loss, 1% crash",
                n=4096, preset="lan", loss=5.0, crash=0.01, part=0, gcap=1 << 18),
-    # BASELINE configs[4] as stated, on one GPU with 4-bit infection rounds (auto above 96 GiB of
-    # 8-bit ones: 2^18 slots x 2^20 members x 0.5 B = 128 GiB)
+    # BASELINE configs[4] as stated: the 8-GPU node's (its SYNC re-spread storm
+    # outgrows the 2^18-slot ring one GPU can hold for 2^20 members; ~4e5 live batch slots by the
+    # storm's measured growth). Per GPU at 2^17 rows: 2^20 slots of 4-bit infection rounds (auto),
+    # holdings, windows, receipts and age bounds = 120 GiB
     "c5": dict(desc="C5: 1,048,576 members, N x K tracked-subject views (K = 256), LAN defaults, 256 simultaneous "
                     "crashes (concurrent churn), suspicion-timeout sweep",
-               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256,
-               rcap=1 << 23),
+               n=1 << 20, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 20, tracked=256,
+               rcap=1 << 24),
     # C5's full size with the churn one GPU holds at that size (tests/test_gpu_fullsize.py)
     "c5g": dict(desc="C5 geometry at 1,048,576 members: N x K tracked-subject views (K = 256), LAN defaults, 8 "
                      "simultaneous crashes, suspicion-timeout sweep",
