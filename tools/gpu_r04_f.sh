@@ -18,5 +18,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/conv/
     python3 bench.py $args > $out/conv_write.json 2> $out/conv_write.err \
  && python3 tools/pmc_converge.py $out/conv 20 5 > $out/pmc_converge_c3.json
 rc=$?; echo "conv rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u tools/c4_alloc_probe.py 8 c5 > $out/c5_alloc.json 2> $out/c5_alloc.err
+rc=$?; echo "c5 alloc rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python -u bench.py --steps 60 --warmup 5 --workload c3half8k --no-cpu-baseline > $out/bench_c3half8k.json 2> $out/bench_c3half8k.err
 rc=$?; echo "half rc=$rc" >> $out/status.log; exit $rc
