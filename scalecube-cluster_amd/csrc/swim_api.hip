@@ -18,9 +18,6 @@
 
 using namespace swim;
 
-// k_sync_first's grid: 8 workgroups of 256 threads per CU, each streaming (member, chunk) items
-constexpr uint32_t SYNC_FIRST_BLOCKS = 2048;
-
 #ifndef SWIM_LOSSY_DICT
 #define SWIM_LOSSY_DICT 0
 #endif
@@ -65,7 +62,6 @@ struct swim_handle {
   // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
   uint32_t apply_blocks = 1, apply_blocks_b = 1;
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
-  bool sync_chunked = false;  // dense rows: SYNC merges take the chunked first pass (k_sync_first)
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
@@ -609,14 +605,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         });
         if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         if (P.njoin) hipLaunchKernelGGL(k_join_scatter, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
-        timed(h, 4, "k_sync_merge", [&] {
-          if (h->sync_chunked) {
-            memset_ctl_u32(h, offsetof(Ctl, n_syl));
-            hipLaunchKernelGGL(k_sync_list, dim3(blocks_for(nloc, 256)), dim3(256), 0, s, P, 0u);
-            hipLaunchKernelGGL(k_sync_first, dim3(SYNC_FIRST_BLOCKS), dim3(256), 0, s, P, 0u);
-          }
-          hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P);
-        });
+        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
         if (W > 1) {  // SYNC_ACK tables back to the requesters' shards, in the order received
@@ -638,14 +627,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 5, "k_sync_ack", [&] {
-          if (h->sync_chunked) {
-            memset_ctl_u32(h, offsetof(Ctl, n_syl));
-            hipLaunchKernelGGL(k_sync_list, dim3(blocks_for(nloc, 256)), dim3(256), 0, s, P, 1u);
-            hipLaunchKernelGGL(k_sync_first, dim3(SYNC_FIRST_BLOCKS), dim3(256), 0, s, P, 1u);
-          }
-          hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P);
-        });
+        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
@@ -980,14 +962,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
-  // dense rows: the chunked first pass of the SYNC / SYNC_ACK merges (k_sync_first)
-  h->sync_chunked = !P.nxk && (P.W & 3u) == 0u;
-  P.syl = nullptr;
-  P.schk = nullptr;
-  if (h->sync_chunked) {
-    ALLOC(P.syl, P.nloc);
-    ALLOC(P.schk, (size_t)P.nloc * ((P.W + 4095u) / 4096u));
-  }
   {  // infectedFrom bookkeeping: in-history rings, delivery records, pruned pairs
     const uint64_t f = (uint64_t)c.gossip_fanout, W32 = h->GC / 32;
     // deliveries recorded per round: those whose receiver may select the sender within the

@@ -128,7 +128,6 @@ struct Ctl {
   // handed out (high-water mark), free blocks on the stack, blocks the last claim took off it, and
   // the unwrapped end of the newest record that got no dictionary entry
   uint32_t c_prev, d_hw, d_nfree, d_taken, d_none_last;
-  uint32_t n_syl;        // members listed in syl for this SYNC / SYNC_ACK phase's chunked first pass
   uint32_t rs_rec[256], rs_body[256];
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
@@ -279,8 +278,6 @@ struct KP {
   uint32_t* recv_off;   // [N+1]
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
-  uint32_t* syl;        // [nloc] local members with SYNC (SYNC_ACK) payloads to merge this phase
-  uint8_t* schk;        // [nloc][chunks] per 4,096-cell chunk of a row: did any payload override a cell
   uint4* stg;         // [stg_cap] gossips created since the last commit: origin, subject, record, id hash
   uint32_t stg_cap;
   // cross-shard exchange (world > 1)

@@ -3694,174 +3694,12 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tot
   return base + x - v;
 }
 
-// ---- SYNC merges of dense rows in two launches (round 4) ----
-// A receiver's merges run in bucket order, each SYNC_ACK payload being its row right after that
-// merge, and new gossips take sequence numbers in cell order: one workgroup per receiver (k_sync_merge).
-// But ~2,200 receivers per period (N / syncInterval) on 256 CUs is one wave of workgroups and a
-// tail: the merges change no cell in the common case, so a first launch streams every (receiver,
-// 4,096-cell chunk) pair as its own work item, over all of the receiver's payloads at once (the row
-// chunk is read once): a chunk that no payload overrides is final — its SYNC_ACK payloads are the row
-// chunk, written here — and only flagged chunks are merged in order by k_sync_merge / k_sync_ack.
-// Per cell the merges are independent (updateMembership of subject c touches cell c, its deadline
-// and the counts), so an unflagged chunk is unchanged by every merge before and after it.
-constexpr uint32_t SY_CH = 4096;  // cells per chunk (16 KiB of a row)
-__device__ __forceinline__ uint32_t sy_chunks(const KP& P) { return (ncells(P) + SY_CH - 1u) / SY_CH; }
-
-// receiver j's bucket entry b (4 * sender + kind): the SYNC payload, where its SYNC_ACK payload goes
-// (null: a joiner's SYNC to a seed whose ack it will not take), and the request's attempt id
-__device__ __forceinline__ void sync_req_io(const KP& P, uint32_t j, uint32_t b, const uint32_t*& src, uint32_t*& ack,
-                                            uint32_t& attempt, bool header) {
-  const uint32_t from = b >> 2, kind = b & 3u;
-  const uint32_t q = 2u * from + (kind & 1u);  // request index of a periodic / FD-triggered SYNC
-  if (kind == 2u) {  // a joiner's initial SYNC; only the seed it will take the SYNC_ACK of keeps one
-    const uint32_t slot = P.jslot[from];
-    src = P.stage_sync + (size_t)slot * P.W;
-    ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
-    attempt = 0x80000000u | from;
-    return;
-  }
-  attempt = q;
-  if (is_local(P, from)) {
-    const uint32_t slot = P.req_stage[q];
-    src = P.stage_sync + (size_t)slot * P.W;
-    ack = P.stage_ack + (size_t)slot * P.W;
-  } else {  // request from another shard: payload in the received record, ack into the same
-    const size_t g = (size_t)P.rs_ref[q] * (P.W + 2u);  // position of the send buffer
-    src = P.xrecv + g + 2;
-    ack = P.xsend + g + 2;
-    if (header) {
-      P.xsend[g] = q;
-      P.xsend[g + 1] = j;
-    }
-  }
-}
-
-// requester i's SYNC_ACK payloads (onSyncAck, MPI:343-349) in (responder, kind) order: kind 0 / 1 =
-// the ack of request 2i + kind, kind 2 = the initial SYNC's first ack; returns how many
-__device__ __forceinline__ uint32_t sync_acks_of(const KP& P, uint32_t i, uint32_t* kd, uint32_t* to) {
-  uint32_t n = 0;
-  for (uint32_t k = 0; k < 2; ++k) {
-    const uint32_t qq = 2 * i + k;
-    if (P.req_stage[qq] == NONE) continue;
-    const uint32_t t = P.req_to[qq];
-    if (!delivered(P, K_SYNC_ACK, t, i, k, P.tick)) continue;
-    kd[n] = k;
-    to[n] = t;
-    ++n;
-  }
-  if (P.njoin && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap) {  // checked in k_join_select
-    kd[n] = 2u;
-    to[n] = P.jwin[i];
-    ++n;
-  }
-  for (uint32_t a = 1; a < n; ++a)  // (responder, kind) order
-    for (uint32_t b = a; b > 0 && (to[b] < to[b - 1] || (to[b] == to[b - 1] && kd[b] < kd[b - 1])); --b) {
-      uint32_t x = kd[b];
-      kd[b] = kd[b - 1];
-      kd[b - 1] = x;
-      x = to[b];
-      to[b] = to[b - 1];
-      to[b - 1] = x;
-    }
-  return n;
-}
-
-// the SYNC_ACK payload requester i merges for (kd, to)
-__device__ __forceinline__ const uint32_t* sync_ack_src(const KP& P, uint32_t i, uint32_t kd, uint32_t to,
-                                                        uint32_t* attempt, uint32_t* reason) {
-  *reason = SWIM_R_SYNC;
-  if (kd == 2u) {  // syncMembership(onStart = true): reason INITIAL_SYNC (MPI:463-473)
-    *attempt = 0x80000000u | to;
-    *reason = SWIM_R_INITIAL_SYNC;
-    return P.stage_ack + (size_t)P.jslot[i] * P.W;
-  }
-  const uint32_t qq = 2 * i + kd, slot = P.req_stage[qq];
-  *attempt = (to << 1) | kd;
-  return slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.W + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
-}
-
-// the phase's members with payloads to merge: receivers with SYNCs (acks = 0) or requesters with
-// SYNC_ACKs (acks = 1), listed in any order (each is merged on its own)
-__global__ void k_sync_list(KP P, uint32_t acks) {
-  SWIM_GUARD(P);
-  const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= P.nloc) return;
-  const uint32_t j = P.row0 + li;
-  uint32_t kd[3], to[3];
-  if (acks ? sync_acks_of(P, j, kd, to) != 0u : P.recv_count[j] != 0u) P.syl[atomicAdd(&P.ctl->n_syl, 1u)] = j;
-}
-
-// The first pass: work item = (listed member, chunk); 16 cells per thread as four 16-B quads of the
-// row chunk, then of each payload; flag the chunk if any payload overrides a cell, else (SYNC) write
-// the chunk into every SYNC_ACK payload. Remote requests get their send-record header here.
-__global__ void __launch_bounds__(256) k_sync_first(KP P, uint32_t acks) {
-  SWIM_GUARD(P);
-  const uint32_t nch = sy_chunks(P), nc = ncells(P), n_items = P.ctl->n_syl * nch;
-  for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const uint32_t j = P.syl[it / nch], ch = it % nch, c0 = ch * SY_CH;
-    const uint32_t* row = P.view + lrow(P, j) * P.W;
-    uint4 v4[4];
-#pragma unroll
-    for (uint32_t u = 0; u < 4u; ++u) {
-      const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
-      v4[u] = c < nc ? *reinterpret_cast<const uint4*>(row + c) : make_uint4(0u, 0u, 0u, 0u);
-    }
-    uint32_t nreq, off = 0;
-    uint32_t kd[3], to[3];
-    if (acks) {
-      nreq = sync_acks_of(P, j, kd, to);
-    } else {
-      nreq = min(P.recv_count[j], (uint32_t)BUCKET_MAX);  // (k_sync_merge raises OV_BUCKET beyond)
-      off = P.recv_off[j];
-    }
-    bool ov = false;
-    for (uint32_t k = 0; k < nreq; ++k) {
-      const uint32_t* src;
-      if (acks) {
-        uint32_t attempt, reason;
-        src = sync_ack_src(P, j, kd[k], to[k], &attempt, &reason);
-      } else {
-        uint32_t* ack;
-        uint32_t attempt;
-        sync_req_io(P, j, P.bucket[off + k], src, ack, attempt, ch == 0u && threadIdx.x == 0u);
-      }
-      uint4 s4[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4u; ++u) {
-        const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
-        s4[u] = c < nc ? *reinterpret_cast<const uint4*>(src + c) : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < 4u; ++u)
-        ov |= (s4[u].x && is_overrides(s4[u].x, v4[u].x)) || (s4[u].y && is_overrides(s4[u].y, v4[u].y)) ||
-              (s4[u].z && is_overrides(s4[u].z, v4[u].z)) || (s4[u].w && is_overrides(s4[u].w, v4[u].w));
-    }
-    const bool flagged = __syncthreads_or(ov) != 0;
-    if (!flagged && !acks) {
-      for (uint32_t k = 0; k < nreq; ++k) {
-        const uint32_t* src;
-        uint32_t* ack;
-        uint32_t attempt;
-        sync_req_io(P, j, P.bucket[off + k], src, ack, attempt, false);
-        if (!ack) continue;
-#pragma unroll
-        for (uint32_t u = 0; u < 4u; ++u) {
-          const uint32_t c = c0 + 1024u * u + 4u * threadIdx.x;
-          if (c < nc) *reinterpret_cast<uint4*>(ack + c) = v4[u];
-        }
-      }
-    }
-    if (threadIdx.x == 0) P.schk[lrow(P, j) * nch + ch] = flagged ? 1u : 0u;
-    if (!acks) add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? nreq * min(SY_CH, nc - c0) : 0u);
-  }
-}
-
 // Merge one table into row `obs` (syncMembership, MembershipProtocolImpl.java:463-473),
 // cells in parallel, gossip sequence numbers assigned in cell order by a block scan.
 // `ack_out` (may be null) receives the row after the merge (onSync's SYNC_ACK payload).
 __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint32_t* src, uint32_t* ack_out,
                                           uint32_t attempt, uint32_t reason, uint32_t snap, uint32_t& seq, Tally& T,
-                                          uint32_t& created, uint32_t* lds4, const uint8_t* chk = nullptr) {
+                                          uint32_t& created, uint32_t* lds4) {
   uint32_t* row = P.view + lrow(P, obs) * P.W;
   // Dense rows: cell = subject, 4 cells per thread (16-B loads) when rows are 16-B aligned.
   // N x K rows: one column per thread, walked in subject order (colorder) so gossip sequence
@@ -3871,7 +3709,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
   const uint32_t nc = ncells(P);
   const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
   __shared__ uint32_t s_chk[32];  // 1,024-cell chunks with an overridden cell (rows of <= 2^20 cells)
-  if (per == 4u && !chk) {
+  if (per == 4u) {
     // Most merges change nothing (a converged or converging cluster): first a barrier-free stream
     // over both rows, four 16-B steps per thread in flight, writing the SYNC_ACK payload as if no
     // cell were overridden; only the 1,024-cell chunks with an overriding cell take the ordered pass
@@ -3904,11 +3742,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
     if (!__syncthreads_or(any)) return;
   }
   for (uint32_t c0 = 0; c0 < nc; c0 += 256u * per) {
-    if (chk) {  // k_sync_first flagged the 4,096-cell chunks an incoming record overrides (uniform)
-      if (!chk[c0 / SY_CH]) continue;
-    } else if (per == 4u && !((s_chk[c0 >> 15] >> ((c0 >> 10) & 31u)) & 1u)) {
-      continue;  // (uniform)
-    }
+    if (per == 4u && !((s_chk[c0 >> 15] >> ((c0 >> 10) & 31u)) & 1u)) continue;  // (uniform)
     const uint32_t c = c0 + per * threadIdx.x;
     uint32_t recs[4], cells[4], nrec = 0;
     if (c < nc) {
@@ -3967,15 +3801,6 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
     cntj = BUCKET_MAX;
   }
   const uint32_t off = P.recv_off[j];
-  // dense rows: k_sync_first flagged the chunks an incoming record overrides and wrote the rest's
-  // SYNC_ACK payloads; nothing flagged, nothing to do
-  const bool chunked = !P.nxk && (P.W & 3u) == 0u;
-  const uint8_t* chk = chunked ? P.schk + lrow(P, j) * sy_chunks(P) : nullptr;
-  if (chunked) {
-    bool any = false;
-    for (uint32_t c = threadIdx.x; c < sy_chunks(P); c += blockDim.x) any |= chk[c] != 0u;
-    if (!__syncthreads_or(any)) return;
-  }
   for (uint32_t k = threadIdx.x; k < cntj; k += blockDim.x) s_list[k] = P.bucket[off + k];
   __syncthreads();
   if (threadIdx.x == 0) {  // insertion sort: bucket entry 4 * sender + kind
@@ -3995,14 +3820,34 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
   uint32_t seq = P.gseq[j];
   const uint32_t snap = P.cnt[j];
   for (uint32_t k = 0; k < cntj; ++k) {
+    const uint32_t b = s_list[k], from = b >> 2, kind = b & 3u;
+    const uint32_t q = 2u * from + (kind & 1u);  // request index of a periodic / FD-triggered SYNC
     const uint32_t* src;
     uint32_t* ack;
-    uint32_t attempt;
-    sync_req_io(P, j, s_list[k], src, ack, attempt, threadIdx.x == 0u);
-    merge_row(P, j, src, ack, attempt, SWIM_R_SYNC, snap, seq, T, created, s_lds4, chk);
+    if (kind == 2u) {  // a joiner's initial SYNC; only the seed it will take the SYNC_ACK of keeps one
+      const uint32_t slot = P.jslot[from];
+      src = P.stage_sync + (size_t)slot * P.W;
+      ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
+      merge_row(P, j, src, ack, 0x80000000u | from, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
+      continue;
+    }
+    if (is_local(P, from)) {
+      const uint32_t slot = P.req_stage[q];
+      src = P.stage_sync + (size_t)slot * P.W;
+      ack = P.stage_ack + (size_t)slot * P.W;
+    } else {  // request from another shard: payload in the received record, ack into the same
+      const size_t g = (size_t)P.rs_ref[q] * (P.W + 2u);  // position of the send buffer
+      src = P.xrecv + g + 2;
+      ack = P.xsend + g + 2;
+      if (threadIdx.x == 0) {
+        P.xsend[g] = q;
+        P.xsend[g + 1] = j;
+      }
+    }
+    merge_row(P, j, src, ack, q, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
-  add_stat(P, ST_MERGE_CELLS, (threadIdx.x == 0 && !chunked) ? cntj * ncells(P) : 0u);
+  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * ncells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -4013,29 +3858,52 @@ __global__ void __launch_bounds__(256) k_sync_ack(KP P) {
   __shared__ uint32_t s_lds4[4];
   const uint32_t i = P.row0 + blockIdx.x;
   if (i >= P.row0 + P.nloc) return;
-  uint32_t kd[3], to[3];  // kind 0 / 1: request 2i + kind; kind 2: the initial SYNC's first ack
-  const uint32_t n = sync_acks_of(P, i, kd, to);
-  if (n == 0) return;
-  add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
-  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * ncells(P) : 0u);
-  // dense rows: k_sync_first flagged the chunks an ack overrides; nothing flagged, nothing to do
-  const bool chunked = !P.nxk && (P.W & 3u) == 0u;
-  const uint8_t* chk = chunked ? P.schk + lrow(P, i) * sy_chunks(P) : nullptr;
-  if (chunked) {
-    bool any = false;
-    for (uint32_t c = threadIdx.x; c < sy_chunks(P); c += blockDim.x) any |= chk[c] != 0u;
-    if (!__syncthreads_or(any)) return;
+  uint32_t kd[3], to[3], n = 0;  // kind 0 / 1: request 2i + kind; kind 2: the initial SYNC's first ack
+  for (uint32_t k = 0; k < 2; ++k) {
+    const uint32_t qq = 2 * i + k;
+    if (P.req_stage[qq] == NONE) continue;
+    const uint32_t t = P.req_to[qq];
+    if (!delivered(P, K_SYNC_ACK, t, i, k, P.tick)) continue;
+    kd[n] = k;
+    to[n] = t;
+    ++n;
   }
+  if (P.njoin && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap) {  // checked in k_join_select
+    kd[n] = 2u;
+    to[n] = P.jwin[i];
+    ++n;
+  }
+  if (n == 0) return;
+  for (uint32_t a = 1; a < n; ++a)  // (responder, kind) order
+    for (uint32_t b = a; b > 0 && (to[b] < to[b - 1] || (to[b] == to[b - 1] && kd[b] < kd[b - 1])); --b) {
+      uint32_t x = kd[b];
+      kd[b] = kd[b - 1];
+      kd[b - 1] = x;
+      x = to[b];
+      to[b] = to[b - 1];
+      to[b - 1] = x;
+    }
   Tally T;
   uint32_t created = 0;
   uint32_t seq = P.gseq[i];
   const uint32_t snap = P.cnt[i];
   for (uint32_t k = 0; k < n; ++k) {
-    uint32_t attempt, reason;
-    const uint32_t* src = sync_ack_src(P, i, kd[k], to[k], &attempt, &reason);
-    merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4, chk);
+    const uint32_t* src;
+    uint32_t attempt, reason = SWIM_R_SYNC;
+    if (kd[k] == 2u) {  // syncMembership(onStart = true): reason INITIAL_SYNC (MPI:463-473)
+      src = P.stage_ack + (size_t)P.jslot[i] * P.W;
+      attempt = 0x80000000u | to[k];
+      reason = SWIM_R_INITIAL_SYNC;
+    } else {
+      const uint32_t qq = 2 * i + kd[k], slot = P.req_stage[qq];
+      attempt = (to[k] << 1) | kd[k];
+      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.W + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
+    }
+    merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
+  add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
+  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * ncells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
