@@ -18,10 +18,6 @@
 
 using namespace swim;
 
-#ifndef SWIM_LOSSY_DICT
-#define SWIM_LOSSY_DICT 0
-#endif
-
 namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
@@ -533,7 +529,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
-          if (P.batched || (SWIM_LOSSY_DICT && h->dict_on))  // batch slots in the ring: expand their records
+          // with the record dictionary (gossip batching on, the default) the batched apply runs whether
+          // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject
+          // runs it takes as run tops (C4's lossy storm: apply 373 -> 104 ms per 20 periods, §6.4)
+          if (P.batched || h->dict_on)
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES),
                                h->apply_lds_b, s, P);
           else

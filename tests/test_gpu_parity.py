@@ -18,14 +18,14 @@ def test_scenario_parity(name):
     scenarios.run_pair(name, SwimCluster, OracleCluster)
 
 
-# Gossip batches: lossless scenarios run batched by default; the same scenarios
-# with one ring slot per gossip must match the oracle too (the round-2 layout, kept for lossy links)
-LOSSLESS = ["c1_local32_crash", "local128_partition_heal", "test64_long_partition_rejoin", "local48_links",
-            "local32_leave2", "local24_inbound_blocks", "local40_restart_join"]
+# Gossip batches: lossless scenarios run batched by default; every scenario with one
+# ring slot per gossip and the LDS-hash apply (gossip_batching off) must match the oracle too
 
 
-@pytest.mark.parametrize("name", LOSSLESS)
+@pytest.mark.parametrize("name", list(scenarios.SCENARIOS))
 def test_scenario_parity_unbatched(name):
+    """Handles without the record dictionary (gossip_batching off): one gossip per ring slot and the
+    LDS-hash apply (k_gossip_apply), lossless and lossy scenarios alike."""
     def make(cfg, n, seed, **kw):
         return SwimCluster(cfg, n, seed, gossip_batching=False, **kw)
 
@@ -218,11 +218,15 @@ sys.path[:0] = {paths!r}
 import scenarios
 from oracle_py import OracleCluster
 from swimhip import SwimCluster
-a, b = scenarios.run_pair("lan288_restart_join_loss5", SwimCluster, OracleCluster)
+# k_gossip_apply (the LDS-hash apply) runs on handles without the record dictionary (gossip_batching
+# off); with it, one-gossip slots go through k_gossip_apply_b too
+def unbatched(cfg, n, seed, **kw):
+    return SwimCluster(cfg, n, seed, gossip_batching=False, **kw)
+a, b = scenarios.run_pair("lan288_restart_join_loss5", unbatched, OracleCluster)
 spills = a.stats()["apply_spills"]
-# a lossy run (one gossip per slot: k_gossip_apply) with more receivers than workgroups and few
-# gossips in flight: small receipt sets, which k_gossip_apply pairs
-a2, b2 = scenarios.run_pair("lan1024_loss5_crash10", SwimCluster, OracleCluster, full_tables=False)
+# a lossy run (one gossip per slot) with more receivers than workgroups and few gossips in flight:
+# small receipt sets, which k_gossip_apply pairs
+a2, b2 = scenarios.run_pair("lan1024_loss5_crash10", unbatched, OracleCluster, full_tables=False)
 spills += a2.stats()["apply_spills"]
 import bench
 from swimhip import ClusterConfig

@@ -2,7 +2,8 @@
 # Round 4, session I: the one-gossip-slot storm (C4's 1 % loss) through the dictionary apply — parity
 # file on that build, then C4's schedule at 65,536 with each build; the product's parity file (the
 # sweep's events now allocated per workgroup tile, age bounds as one u16 per word) and C3 (base build vs
-# this tree; its converge window with the event ring).
+# this tree; its converge window with the event ring); the fault-free steady state (SYNC-bound), base vs this
+# tree (the chunked SYNC first pass).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_i
@@ -22,4 +23,10 @@ SWIMHIP_LIB=$PWD/variants_ab/libswimhip_base.so timeout -k 10 300 python -u benc
    --converge 0 > $out/bench_c3_base.json 2> $out/bench_c3_base.err
 rc=$?; echo "c3 base rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $out/bench_c3.json 2> $out/bench_c3.err
-rc=$?; echo "c3 rc=$rc" >> $out/status.log; exit $rc
+rc=$?; echo "c3 rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+for v in base product; do
+  lib=$PWD/variants_ab/libswimhip_base.so; [ $v = product ] && lib=$PWD/scalecube-cluster_amd/swimhip/libswimhip.so
+  SWIMHIP_LIB=$lib timeout -k 10 200 python -u bench.py --steps 60 --warmup 5 --workload steady65k --no-cpu-baseline \
+     > $out/bench_steady_$v.json 2> $out/bench_steady_$v.err
+  rc=$?; echo "steady $v rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+done

@@ -5,8 +5,7 @@ k_sync_merge / k_sync_ack are averaged over the periods after the timed window (
 window of bench.py's converge_kernels_frac); k_susp_sweep over the periods whose suspicion deadlines
 fired (the window of bench.py's sweep_roofline: the dispatches that moved more than 1 MiB).
 FETCH_SIZE is doubled per MI355X_MICROARCH.md's gfx950 note for 16-B streaming reads (the merges);
-the sweep's widths are reported both ways. Dense handles
-(round 4) fold each phase's k_sync_list / k_sync_first dispatches into its class. usage:
+the sweep's widths are reported both ways. usage:
 pmc_converge.py <dir> S W"""
 import collections
 import csv
@@ -16,9 +15,6 @@ import os
 import sys
 
 KERNELS = ("k_sync_merge", "k_sync_ack", "k_susp_sweep")
-# dense rows (round 4): each SYNC class is k_sync_list + k_sync_first + the ordered kernel, the first
-# two dispatched twice per period (the SYNC phase, then the SYNC_ACK phase)
-FIRST = ("k_sync_list", "k_sync_first")
 
 
 def load(path, counter):
@@ -28,28 +24,14 @@ def load(path, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row["Kernel_Name"].split("(")[0].replace("swim::", "")
-            if name in KERNELS or name in FIRST:
+            if name in KERNELS:
                 v[name].append((int(row["Dispatch_Id"]), float(row["Counter_Value"]) * 1024.0))
     return {k: [x for _, x in sorted(xs)] for k, xs in v.items()}
 
 
-def fold_first(v):
-    """k_sync_merge / k_sync_ack per period + that phase's k_sync_list and k_sync_first dispatch."""
-    for name, phase in (("k_sync_merge", 0), ("k_sync_ack", 1)):
-        if name not in v:
-            continue
-        for f in FIRST:
-            xs = v.get(f, [])
-            for i in range(len(v[name])):
-                if 2 * i + phase < len(xs):
-                    v[name][i] += xs[2 * i + phase]
-    return v
-
-
 def main(d, steps, warmup):
     s, w = int(steps), int(warmup)
-    fe = fold_first(load(os.path.join(d, "fetch"), "FETCH_SIZE"))
-    wr = fold_first(load(os.path.join(d, "write"), "WRITE_SIZE"))
+    fe, wr = load(os.path.join(d, "fetch"), "FETCH_SIZE"), load(os.path.join(d, "write"), "WRITE_SIZE")
     out = {"window": {"converge_from_period": s + w, "sweep": "dispatches that moved > 1 MiB"}}
     for k in KERNELS:
         f, wv = fe.get(k, []), wr.get(k, [])
