@@ -524,6 +524,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 1, "k_gossip_pull", [&] {
           if (P.dq)
             hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+          else if (P.loss_mode == 1u)  // the loss draws' instance (§3.16's split, for registers)
+            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
           else
             hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
         });

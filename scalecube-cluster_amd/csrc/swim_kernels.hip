@@ -2087,7 +2087,15 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 #endif
 // DQ: this handle has delayed-message rings. The delay paths get an instance of
 // their own, so the common one keeps its registers (4 waves per SIMD instead of 3).
-template <bool DQ>
+#ifndef SWIM_PULL_LOSS_ILP
+#define SWIM_PULL_LOSS_ILP 4
+#endif
+constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
+
+// DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
+// probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
+// common instance keeps the one-at-a-time loop and 4 waves per SIMD).
+template <bool DQ, bool LOSS>
 __device__ __forceinline__ void pull_body(const KP& P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
@@ -2262,7 +2270,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
                     dq_push(P, p, mv[j], wsv[i] * 32u + b, P.round + dr);
                 }
                 cand &= ~hw[i] & ~u[i] & ~prev[i];
-              } else if (cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+              } else if (!LOSS && cand && P.loss_mode == 1u) {  // (the host launches the LOSS instance then)
                 uint32_t need = cand;
                 cand = 0u;
                 while (need) {
@@ -2270,6 +2278,24 @@ __device__ __forceinline__ void pull_body(const KP& P) {
                   need &= need - 1u;
                   if (draw1(P.seed, K_GOSSIP, mv[j], p, P.g_hash[wsv[i] * 32u + b], P.tick) >= P.loss_thr)
                     cand |= 1u << b;
+                }
+              } else if (LOSS && cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
+                // four candidates at a time: their id-hash loads in flight together, then their draws
+                // (one dependent hash load per candidate was the lossy storm's pull chain)
+                uint32_t need = cand;
+                cand = 0u;
+                while (need) {
+                  uint32_t bb[PULL_LOSS_ILP], hh[PULL_LOSS_ILP];
+#pragma unroll
+                  for (uint32_t k = 0; k < PULL_LOSS_ILP; ++k) {
+                    bb[k] = need ? (uint32_t)__builtin_ctz(need) : 32u;
+                    need &= need - 1u;
+                  }
+#pragma unroll
+                  for (uint32_t k = 0; k < PULL_LOSS_ILP; ++k) hh[k] = bb[k] < 32u ? P.g_hash[wsv[i] * 32u + bb[k]] : 0u;
+#pragma unroll
+                  for (uint32_t k = 0; k < PULL_LOSS_ILP; ++k)
+                    if (bb[k] < 32u && draw1(P.seed, K_GOSSIP, mv[j], p, hh[k], P.tick) >= P.loss_thr) cand |= 1u << bb[k];
                 }
               }
               u[i] |= cand;
@@ -2328,8 +2354,9 @@ __device__ __forceinline__ void pull_body(const KP& P) {
   add_stat(P, ST_G_PULLW, words);
 }
 
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false>(P); }
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_loss(KP P) { pull_body<false, true>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true, true>(P); }
 
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
