@@ -159,7 +159,9 @@ def kernel_bytes(name, d, rounds_per_period=5):
 
 
 # kernel class (swim_kernel_time index names) -> the kernels rocprof sees under it
-KERNEL_NAMES = {"k_gossip_apply": ["k_gossip_apply", "k_gossip_apply_b"], "k_gossip_pull": ["k_gossip_pull", "k_gossip_pull_loss", "k_gossip_pull_dq"],
+KERNEL_NAMES = {"k_gossip_apply": ["k_gossip_apply", "k_gossip_apply_b", "k_gossip_apply_h4", "k_gossip_apply_b_h4"],
+                "k_gossip_select": ["k_gossip_select", "k_gossip_select_h4"],
+                "k_gossip_pull": ["k_gossip_pull", "k_gossip_pull_loss", "k_gossip_pull_dq"],
                 "k_gossip_pairwin": ["k_gossip_pairfill", "k_gossip_pairprune", "k_gossip_pairdelay"]}
 
 
