@@ -2088,7 +2088,7 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 // DQ: this handle has delayed-message rings. The delay paths get an instance of
 // their own, so the common one keeps its registers (4 waves per SIMD instead of 3).
 #ifndef SWIM_PULL_LOSS_ILP
-#define SWIM_PULL_LOSS_ILP 4
+#define SWIM_PULL_LOSS_ILP 2
 #endif
 constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
 
@@ -2280,7 +2280,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
                     cand |= 1u << b;
                 }
               } else if (LOSS && cand && P.loss_mode == 1u) {  // NetworkEmulator.evaluateLoss per message
-                // four candidates at a time: their id-hash loads in flight together, then their draws
+                // two candidates at a time: their id-hash loads in flight together, then their draws
                 // (one dependent hash load per candidate was the lossy storm's pull chain)
                 uint32_t need = cand;
                 cand = 0u;
