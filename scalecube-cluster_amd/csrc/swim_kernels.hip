@@ -2734,6 +2734,12 @@ constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flig
 #define SWIM_AW_QILP 2
 #endif
 constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
+#ifndef SWIM_AW_LONG
+#define SWIM_AW_LONG 64
+#endif
+// record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
+// are flattened into one stream of 16-B quads across the wave
+constexpr uint32_t AW_LONG = SWIM_AW_LONG;
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
@@ -2877,7 +2883,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         }
 #endif
         // long ranges (batches): the whole wave walks each, 16-B quads of entry ids per lane
-        unsigned long long big = __ballot(len >= 64u);
+        unsigned long long big = __ballot(len >= AW_LONG);
         while (big) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
@@ -2906,7 +2912,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
         // flattened across the lanes, one quad per lane per load (one owner search per quad)
         {
-          const bool sh = len != 0u && len < 64u;
+          const bool sh = len != 0u && len < AW_LONG;
           const uint32_t nq = sh ? ((cr.x & 3u) + len + 3u) >> 2 : 0u;
           uint32_t qtot;
           const uint32_t qoff = wave_excl_scan(nq, &qtot);
