@@ -1915,6 +1915,11 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
 }
 
+#ifndef SWIM_REC_ILP
+#define SWIM_REC_ILP 1
+#endif
+constexpr uint32_t REC_ILP = SWIM_REC_ILP;  // k_gossip_record's loss / delay draws per step of a lane
+
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
 // position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull).
 // (Drawing lazily at pruning time instead was measured slower: a record is pruned against
@@ -1932,15 +1937,26 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
     v = own_window(P, sreg, k, w_beg, lo, hi);
   if (v && (P.loss_mode == 1u || P.delay_on)) {  // this round's deliveries only: not lost, not delayed
     const uint32_t W32 = P.GC >> 5, wi = w_beg + (ea & ACT_OFF_MASK);
+    const uint32_t* gh = P.g_hash + (wi & (W32 - 1u)) * 32u;
     uint32_t need = v;
     v = 0u;
-    while (need) {
-      const uint32_t b = (uint32_t)__builtin_ctz(need);
-      need &= need - 1u;
-      const u32x4 d = draw4(P.seed, K_GOSSIP, sid, p, P.g_hash[(wi & (W32 - 1u)) * 32u + b], P.tick);
-      if (P.loss_mode == 1u && d.x < P.loss_thr) continue;
-      if (P.delay_on && delay_of_draw(P, d.y) >= P.gint) continue;
-      v |= 1u << b;
+    while (need) {  // REC_ILP messages per step: their id-hash loads in flight together
+      uint32_t bb[REC_ILP], hh[REC_ILP];
+#pragma unroll
+      for (uint32_t k = 0; k < REC_ILP; ++k) {
+        bb[k] = need ? (uint32_t)__builtin_ctz(need) : 32u;
+        need &= need - 1u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < REC_ILP; ++k) hh[k] = bb[k] < 32u ? gh[bb[k]] : 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < REC_ILP; ++k) {
+        if (bb[k] >= 32u) continue;
+        const u32x4 d = draw4(P.seed, K_GOSSIP, sid, p, hh[k], P.tick);
+        if (P.loss_mode == 1u && d.x < P.loss_thr) continue;
+        if (P.delay_on && delay_of_draw(P, d.y) >= P.gint) continue;
+        v |= 1u << bb[k];
+      }
     }
   }
   return v;
