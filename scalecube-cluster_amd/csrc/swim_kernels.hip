@@ -2751,7 +2751,7 @@ constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flig
 #endif
 constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
 #ifndef SWIM_AW_LONG
-#define SWIM_AW_LONG 64
+#define SWIM_AW_LONG 256
 #endif
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
