@@ -1916,7 +1916,7 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
 }
 
 #ifndef SWIM_REC_ILP
-#define SWIM_REC_ILP 1
+#define SWIM_REC_ILP 2
 #endif
 constexpr uint32_t REC_ILP = SWIM_REC_ILP;  // k_gossip_record's loss / delay draws per step of a lane
 
