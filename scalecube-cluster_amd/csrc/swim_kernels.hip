@@ -2107,6 +2107,10 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 #define SWIM_PULL_LOSS_ILP 2
 #endif
 constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
+#ifndef SWIM_PULL_SILP
+#define SWIM_PULL_SILP 2
+#endif
+constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2231,10 +2235,10 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           prev[2] = p4.z;
           prev[3] = p4.w;
         }
-        for (uint32_t q0 = 0; q0 < cdeg; q0 += 2u) {
-          uint32_t wv[2][4], mv[2];
+        for (uint32_t q0 = 0; q0 < cdeg; q0 += PULL_SILP) {
+          uint32_t wv[PULL_SILP][4], mv[PULL_SILP];
 #pragma unroll
-          for (uint32_t j = 0; j < 2u; ++j) {  // the window loads of 2 senders, issued together
+          for (uint32_t j = 0; j < PULL_SILP; ++j) {  // the window loads of PULL_SILP senders, issued together
             const bool has = q0 + j < cdeg;
             const uint32_t en = has ? snd[q0 + j] : 0u;
             mv[j] = has ? s_sid[threadIdx.x >> 6][q0 + j] : 0u;
@@ -2265,7 +2269,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
             }
           }
 #pragma unroll
-          for (uint32_t j = 0; j < 2u; ++j)
+          for (uint32_t j = 0; j < PULL_SILP; ++j)
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) {
               const uint32_t win = wv[j][i];
