@@ -1373,6 +1373,39 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 #define SEL_ME(j_) s_me[w][j_][lane]
 #endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
+#ifndef SWIM_SEL_FLAT
+#define SWIM_SEL_FLAT 0
+#endif
+#if SWIM_SEL_FLAT && !SWIM_SEL_MW_WORD
+#error "SWIM_SEL_FLAT reads each MIXED entry's holdings word from s_mw"
+#endif
+
+// The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
+// the lanes' exclusive offsets, non-decreasing; every lane calls it, each with its own q).
+__device__ __forceinline__ uint32_t wave_owner(uint32_t off, uint32_t q) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 32; step > 0; step >>= 1) {
+    const uint32_t o = __shfl(off, (int)(lo + step), 64);
+    if (o <= q) lo += step;
+  }
+  return lo;
+}
+
+// position of the k-th (0-based) set bit of m, k < popcount(m)
+__device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 16; w > 0; w >>= 1) {
+    const uint32_t c = (uint32_t)__popc(m & ((1u << w) - 1u));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
 
 template <bool HD4>
 __device__ __forceinline__ void select_body(const KP& P) {
@@ -1380,6 +1413,9 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
+#if SWIM_SEL_FLAT
+  __shared__ uint32_t s_lk[4][64];  // the flattened MIXED pass's lack bits, by owner lane
+#endif
 #if SWIM_SEL_MW_WORD
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
 #else
@@ -1518,13 +1554,89 @@ __device__ __forceinline__ void select_body(const KP& P) {
         }
         }
       }
-      // entries one at a time from the mask, the infection rounds (32 B) of the next
-      // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
       auto hd_ld = [&](uint32_t e_, uint4& a_, uint4& b_) {
         const uint32_t wi_ = w_beg + (e_ & ACT_OFF_MASK), ws_ = wi_ & (W32 - 1u);
         // (hd4: escapes of the held live slots only; the holdings word is cache-resident)
         hd_load32<HD4>(P, lrow(P, m), ws_, a_, b_, HD4 ? hbr[ws_] & range_mask(wi_ << 5, lo, hi) : 0xFFFFFFFFu);
       };
+      // a MIXED entry (list entry e, holdings word, list position k) from its 32 infection rounds:
+      // sweep, window, age bounds, wb; true when the member lacks a live gossip of the word
+      auto finish_mixed = [&](uint32_t e, uint32_t word, uint32_t k, uint4 d0, uint4 d1) -> bool {
+        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
+        const uint32_t wc = (e >> 26) & 3u;
+        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t held = word & range_mask(wi << 5, lo, hi);
+        // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
+        ++hdw;
+        const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        // four ages per dword at once (byte-wise r - round, then 16-bit-lane threshold tests)
+        uint32_t over_sweep = 0, over_spread = 0;
+        uint32_t ages[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8u; ++q) {
+          const uint32_t a = bytes_sub(r, d32[q]);
+          ages[q] = a;
+          over_sweep |= bytes_gt(a, sweep) << (4u * q);
+          over_spread |= bytes_gt(a, spread) << (4u * q);
+        }
+        const uint32_t clear = held & over_sweep;  // sweepGossips
+        const uint32_t win = held & ~over_spread;
+        const bool lack = wc != WC_NONE && (held & ~clear) != range_mask(wi << 5, lo, hi);
+        uint32_t oldest_kept = 0;
+        const uint32_t kept = held & ~clear;
+        if (clear && kept) {
+#pragma unroll
+          for (uint32_t q = 0; q < 8u; ++q) {
+            const uint32_t a = ages[q] & nibble_bytes((kept >> (4u * q)) & 0xFu);
+            oldest_kept = max(oldest_kept, max(max(a & 0xFFu, (a >> 8) & 0xFFu), max((a >> 16) & 0xFFu, a >> 24)));
+          }
+        }
+        if (clear && (held & ~clear)) reinterpret_cast<uint8_t*>(mmr)[2u * ws] = (uint8_t)(r - oldest_kept);  // oldest
+        if (clear) {
+          hbr[ws] = word & ~clear;
+          nclear += (uint32_t)__popc(clear);
+          if (P.leaving[m]) leave_swept(P, m, ws, clear);
+        }
+        if (wc != WC_NONE) {
+          if (wc == WC_MIXED) {
+            ++winw;
+            wbr[DBG_IDX(k, W32, "select wbr")] = win;
+          }
+          win_l |= win != 0u;
+          winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
+        }
+        return lack;
+      };
+#if SWIM_SEL_FLAT
+      {  // the wave's MIXED entries flattened, one per lane per step: a lane's own entries cluster
+         // where the list holds the storm's newest words, and walked per lane the wave waited for
+         // the lane with the most (their list entry and holdings word are in s_mw, LDS)
+        s_lk[w][lane] = 0u;
+        uint32_t tot;
+        const uint32_t off = wave_excl_scan((uint32_t)__popc(mixm), &tot);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
+          const uint32_t q = q0 + lane;
+          const uint32_t o = wave_owner(off, q);
+          const uint32_t mo = __shfl(mixm, (int)o, 64), oo = __shfl(off, (int)o, 64);
+          if (q < tot) {
+            const uint32_t j = kth_set_bit(mo, q - oo);
+            const uint2 mw = s_mw[w][j][o];
+            uint4 d0, d1;
+            hd_ld(mw.x, d0, d1);
+            if (finish_mixed(mw.x, mw.y, k0 + 256u * (j >> 2) + 4u * o + (j & 3u), d0, d1))
+              atomicOr(&s_lk[w][o], 1u << j);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        lackm |= s_lk[w][lane];
+        mixm = 0u;
+      }
+#else
+      // entries one at a time from the mask, the infection rounds (32 B) of the next
+      // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
       uint32_t jn = 0, en = 0;
       uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
 #if SWIM_SEL_AHEAD >= 2
@@ -1570,55 +1682,14 @@ __device__ __forceinline__ void select_body(const KP& P) {
           hd_ld(en, n0, n1);
         }
 #endif
-        const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
-        const uint32_t wc = (e >> 26) & 3u;
-        const uint32_t ws = wi & (W32 - 1u);
 #if SWIM_SEL_MW_WORD
         const uint32_t word = s_mw[w][j][lane].y;
 #else
-        const uint32_t word = hbr[ws];  // cache-resident: read in the pass above
+        const uint32_t word = hbr[(w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u)];  // cache-resident: read in the pass above
 #endif
-        const uint32_t held = word & range_mask(wi << 5, lo, hi);
-        // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
-        ++hdw;
-        const uint32_t d32[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-        // four ages per dword at once (byte-wise r - round, then 16-bit-lane threshold tests)
-        uint32_t over_sweep = 0, over_spread = 0;
-        uint32_t ages[8];
-#pragma unroll
-        for (uint32_t q = 0; q < 8u; ++q) {
-          const uint32_t a = bytes_sub(r, d32[q]);
-          ages[q] = a;
-          over_sweep |= bytes_gt(a, sweep) << (4u * q);
-          over_spread |= bytes_gt(a, spread) << (4u * q);
-        }
-        const uint32_t clear = held & over_sweep;  // sweepGossips
-        const uint32_t win = held & ~over_spread;
-        if (wc != WC_NONE && (held & ~clear) != range_mask(wi << 5, lo, hi)) lackm |= 1u << j;
-        uint32_t oldest_kept = 0;
-        const uint32_t kept = held & ~clear;
-        if (clear && kept) {
-#pragma unroll
-          for (uint32_t q = 0; q < 8u; ++q) {
-            const uint32_t a = ages[q] & nibble_bytes((kept >> (4u * q)) & 0xFu);
-            oldest_kept = max(oldest_kept, max(max(a & 0xFFu, (a >> 8) & 0xFFu), max((a >> 16) & 0xFFu, a >> 24)));
-          }
-        }
-        if (clear && (held & ~clear)) reinterpret_cast<uint8_t*>(mmr)[2u * ws] = (uint8_t)(r - oldest_kept);  // oldest
-        if (clear) {
-          hbr[ws] = word & ~clear;
-          nclear += (uint32_t)__popc(clear);
-          if (P.leaving[m]) leave_swept(P, m, ws, clear);
-        }
-        if (wc != WC_NONE) {
-          if (wc == WC_MIXED) {
-            ++winw;
-            wbr[DBG_IDX(k, W32, "select wbr")] = win;
-          }
-          win_l |= win != 0u;
-          winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
-        }
+        if (finish_mixed(e, word, k, d0, d1)) lackm |= 1u << j;
       }
+#endif  // SWIM_SEL_FLAT
       if (lack_ok) {  // positions k0 + 256 jq + 4 lane + i: eight lanes fill one bitmap word
 #pragma unroll
         for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
@@ -2672,33 +2743,6 @@ __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply(KP P) { apply_bo
 __global__ void __launch_bounds__(APPLY_THREADS) k_gossip_apply_h4(KP P) { apply_body<true>(P); }
 
 // ---- batch slots: k_gossip_apply for rings that hold gossip batches ----
-// The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
-// the lanes' exclusive offsets, non-decreasing; every lane calls it, each with its own q).
-__device__ __forceinline__ uint32_t wave_owner(uint32_t off, uint32_t q) {
-  uint32_t lo = 0;
-#pragma unroll
-  for (uint32_t step = 32; step > 0; step >>= 1) {
-    const uint32_t o = __shfl(off, (int)(lo + step), 64);
-    if (o <= q) lo += step;
-  }
-  return lo;
-}
-
-// position of the k-th (0-based) set bit of m, k < popcount(m)
-__device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t w = 16; w > 0; w >>= 1) {
-    const uint32_t c = (uint32_t)__popc(m & ((1u << w) - 1u));
-    if (k >= c) {
-      k -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
-}
-
 // the highest received slot of every subject run (runw: run starts; a batch slot is a run of
 // its own): the slot whose records carry the run's lattice max
 __device__ __forceinline__ uint32_t run_tops(uint32_t bits, uint32_t rs) {
