@@ -1374,7 +1374,7 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 #endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 #ifndef SWIM_SEL_FLAT
-#define SWIM_SEL_FLAT 0
+#define SWIM_SEL_FLAT 1
 #endif
 #if SWIM_SEL_FLAT && !SWIM_SEL_MW_WORD
 #error "SWIM_SEL_FLAT reads each MIXED entry's holdings word from s_mw"
