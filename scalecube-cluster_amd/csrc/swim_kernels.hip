@@ -2972,7 +2972,8 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       tq = wall_clock64();
 #endif
       const uint32_t e = kv != NONE ? P.act[kv] : 0u;
-      const uint32_t bits = (kv != NONE && ((e >> 26) & 3u) != WC_NONE) ? nbr[kv] : 0u;
+      const uint32_t b0 = kv != NONE ? nbr[kv] : 0u;  // issued beside the list entry, not after it
+      const uint32_t bits = ((e >> 26) & 3u) != WC_NONE ? b0 : 0u;
       const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
       uint32_t rm = 0u;
       if (bits) {
