@@ -2182,13 +2182,6 @@ constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step o
 #define SWIM_PULL_SILP 2
 #endif
 constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
-#ifndef SWIM_PULL_FLAT
-#define SWIM_PULL_FLAT 0
-#endif
-#ifndef SWIM_PULL_FSEG
-#define SWIM_PULL_FSEG 4
-#endif
-constexpr uint32_t PF_SEG = SWIM_PULL_FSEG;  // flattened pull: lane-steps of the list classified per segment
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2200,10 +2193,6 @@ __device__ __forceinline__ void pull_body(const KP& P) {
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
-#if SWIM_PULL_FLAT
-  __shared__ uint32_t s_fk[DQ ? 1 : 4][DQ ? 1 : 64 * PF_SEG];  // list positions of the quads with something to do
-  __shared__ uint4 s_fh[DQ ? 1 : 4][DQ ? 1 : 64 * PF_SEG];     // ... and the receiver's holdings of them
-#endif
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
@@ -2282,14 +2271,15 @@ __device__ __forceinline__ void pull_body(const KP& P) {
       // come in 16-B loads; other quads fall back to per-word loads. classify: which of the quad's
       // words can still bring the receiver something (todo); deliver: the senders' windows, the
       // loss draws, the receipts.
-      auto classify = [&](uint32_t kq, const uint4& a, uint4 h4, bool count, uint32_t (&wcv)[4], uint32_t (&wsv)[4],
-                          uint32_t (&live)[4], uint32_t (&hw)[4], uint32_t& todo, uint32_t& anyall, uint32_t& anymix,
-                          bool& quad, uint32_t& ws0, bool load_h) {
+      auto classify = [&](uint32_t kq, const uint4& a, uint32_t (&wcv)[4], uint32_t (&wsv)[4], uint32_t (&live)[4],
+                          uint32_t (&hw)[4], uint32_t& todo, uint32_t& anyall, uint32_t& anymix, bool& quad,
+                          uint32_t& ws0) {
         const uint32_t ea[4] = {a.x, a.y, a.z, a.w};
         const uint32_t o0 = a.x & ACT_OFF_MASK;
         ws0 = (w_beg + o0) & (W32 - 1u);
         quad = kq + 3u < n_act && (ws0 & 3u) == 0u && (a.w & ACT_OFF_MASK) == o0 + 3u;
-        if (quad && load_h) h4 = *reinterpret_cast<const uint4*>(hbr + ws0);
+        uint4 h4 = make_uint4(0u, 0u, 0u, 0u);
+        if (quad) h4 = *reinterpret_cast<const uint4*>(hbr + ws0);
         const uint32_t ha[4] = {h4.x, h4.y, h4.z, h4.w};
         todo = 0;
         anyall = 0;
@@ -2301,9 +2291,9 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           const uint32_t wi = w_beg + (ea[i] & ACT_OFF_MASK);
           wsv[i] = wi & (W32 - 1u);
           live[i] = range_mask(wi << 5, lo, hi);
-          hw[i] = (quad || !load_h) ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
+          hw[i] = quad ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
           if (wcv[i] == WC_NONE) continue;
-          if (count) ++words;
+          ++words;
           if (!(DQ && P.delay_on) && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
           todo |= 1u << i;
           anyall |= wcv[i] == WC_ALL ? 1u : 0u;
@@ -2417,52 +2407,6 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           }
         if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
       };
-#if SWIM_PULL_FLAT
-      if (!DQ) {
-        // the quads with something to do, flattened across the wave (one per lane per step): the
-        // receiver's own select pass leaves a few per lane-step of the list, and walked lane by lane
-        // most of the wave idled beside the lane with the most
-        for (uint32_t base = 0; base < n_act; base += 256u * PF_SEG) {
-          uint32_t nq = 0;  // (wave-uniform)
-#pragma unroll 1
-          for (uint32_t t = 0; t < PF_SEG; ++t) {
-            const uint32_t kq = base + 256u * t + 4u * lane;
-            uint32_t todo = 0, anyall, anymix, ws0;
-            uint32_t wcv[4], wsv[4], live[4], hw[4];
-            bool quad;
-            if (kq < n_act && !(lackr && !((lackr[kq >> 5] >> (kq & 31u)) & 0xFu))) {
-              const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
-              classify(kq, a, make_uint4(0u, 0u, 0u, 0u), true, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0, true);
-            }
-            const unsigned long long bt = __ballot(todo != 0u);
-            if (todo) {
-              const uint32_t pos = nq + (uint32_t)__popcll(bt & ((1ull << lane) - 1ull));
-              s_fk[threadIdx.x >> 6][pos] = kq;
-              s_fh[threadIdx.x >> 6][pos] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-            }
-            nq += (uint32_t)__popcll(bt);
-          }
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-          for (uint32_t e0 = 0; e0 < nq; e0 += 64u) {
-            const uint32_t e = e0 + lane;
-            uint32_t todo = 0, anyall = 0, anymix = 0, ws0 = 0, kq = 0;
-            uint32_t wcv[4] = {WC_NONE, WC_NONE, WC_NONE, WC_NONE}, wsv[4] = {0u, 0u, 0u, 0u},
-                     live[4] = {0u, 0u, 0u, 0u}, hw[4] = {0u, 0u, 0u, 0u};
-            bool quad = false;
-            if (e < nq) {
-              kq = s_fk[threadIdx.x >> 6][e];
-              const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
-              classify(kq, a, s_fh[threadIdx.x >> 6][e], false, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0,
-                       false);
-            }
-            // (every lane runs the sender loop: the lanes without an entry load and deliver nothing)
-            deliver(kq, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
-          }
-          __builtin_amdgcn_wave_barrier();  // s_fk / s_fh are rewritten by the next segment
-        }
-      } else
-#endif
       for (uint32_t kq = 4u * lane; kq < n_act; kq += 256u) {
         // the receiver's own select pass marked the sent words it lacks something in: skip the
         // rest without reading the list or the holdings (most of them once a storm has spread;
@@ -2472,7 +2416,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
         uint32_t todo, anyall, anymix, ws0;
         uint32_t wcv[4], wsv[4], live[4], hw[4];
         bool quad;
-        classify(kq, a, make_uint4(0u, 0u, 0u, 0u), true, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0, true);
+        classify(kq, a, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
         if (!todo) continue;
         deliver(kq, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
       }
