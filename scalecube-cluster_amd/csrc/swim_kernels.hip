@@ -1355,11 +1355,14 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 // in the active list. A word's infection rounds (64 B) are read only when its class is MIXED;
 // ALL/NONE words are decided by the class. A member with a non-empty window registers with each
 // chosen peer (in_cnt), so delivery can run receiver-side (k_gossip_pull).
+// one list quad per lane per step at 6 waves per SIMD (80 VGPRs, 44 B of scratch): with the MIXED
+// entries flattened across the wave, more waves in flight beat more loads per wave (C3 select 63.9
+// -> 55.3 ms per 20 periods, C4's schedule 94.9 -> 87.9)
 #ifndef SWIM_SEL_BATCH
-#define SWIM_SEL_BATCH 2
+#define SWIM_SEL_BATCH 1
 #endif
 #ifndef SWIM_SEL_WAVES
-#define SWIM_SEL_WAVES 8
+#define SWIM_SEL_WAVES 6
 #endif
 #ifndef SWIM_SEL_AHEAD
 #define SWIM_SEL_AHEAD 1
