@@ -2467,7 +2467,12 @@ __device__ __forceinline__ void pull_body(const KP& P) {
 }
 
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_loss(KP P) { pull_body<false, true>(P); }
+// the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
+// per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
+#ifndef SWIM_PULL_LOSS_WAVES
+#define SWIM_PULL_LOSS_WAVES 6
+#endif
+__global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) { pull_body<false, true>(P); }
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true, true>(P); }
 
 #ifndef SWIM_APPLY_HLOG
