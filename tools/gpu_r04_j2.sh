@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4, session J2: the -m gpu suite and smoke() on the tree after the A/B rounds (select at 6 waves, flattened MIXED pass, 256-record ranges, lossy pull at 6 waves).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/r04_j2
+mkdir -p $out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+   > $out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc" >> $out/status.log; exit $rc
