@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session A: -m gpu suite on the tree, then the C4 storm at 131,072 (N x K, largest one GPU holds)
 # and the C4 shard allocation at the 2^21-slot ring the storm measurements call for.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_a
 mkdir -p $out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session B: -m gpu suite, then bench lines: C3 (driver window), C4's schedule at the sizes one
 # GPU holds (65,536 dense, 131,072 N x K).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_b
 mkdir -p $out

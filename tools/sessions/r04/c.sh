@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4, session C: -m gpu suite (hd4 parity, sharded lifecycle, wire bridge, scan KAT), C3 bench line.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_c
 mkdir -p $out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C4 storm probe at 16k / 32k / 65k members (1 % loss, 0.1 % crash), one GPU, dense.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_c4probe
 mkdir -p $out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session D: FETCH/WRITE calibration on known access patterns; C5 as stated (2^20 members,
 # N x K K = 256, 256 crashes; 4-bit infection rounds); C4's storm at 131,072 members over 45 periods.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_d
 mkdir -p $out

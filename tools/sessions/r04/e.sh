@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4, session E: -m gpu suite, then (tools/gpu_r04_d.sh) calibration, C5 as stated, C4 storm at 131k.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_e
 mkdir -p $out

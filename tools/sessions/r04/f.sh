@@ -2,7 +2,7 @@
 # Round 4, session F (run after J): the final tree's profiles — rocprofv3 kernel stats of the driver's bench command,
 # PMC FETCH/WRITE over its timed window (tools/gpu_pmc.sh), PMC over the converge window (merge / sweep),
 # and the half/half partition heal at 8,192 members.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_f
 mkdir -p $out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session G: the wire test at 48 N x K columns; C5 as stated — its storm per period (live
 # slots, live records) with a 2^23 record ring, then the bench line; rank 0's C4 shard at 2^22 slots.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_g
 mkdir -p $out

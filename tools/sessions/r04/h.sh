@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session H: C4's schedule at 65,536 dense (full-size property test); the driver's bench
 # command with the MembershipEvent ring; C5's storm (256 crashes) at 2^19 members on a 2^18 ring.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_h
 mkdir -p $out

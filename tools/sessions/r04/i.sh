@@ -4,7 +4,7 @@
 # sweep's events now allocated per workgroup tile, age bounds as one u16 per word) and C3 (base build vs
 # this tree; its converge window with the event ring); the fault-free steady state (SYNC-bound), base vs this
 # tree (the chunked SYNC first pass).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_i
 mkdir -p $out

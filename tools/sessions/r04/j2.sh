@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4, session J: the final tree's -m gpu suite and smoke().
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# Round 4, session J2: the -m gpu suite and smoke() on the tree after the A/B rounds (select at 6 waves, flattened MIXED pass, 256-record ranges, lossy pull at 6 waves).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
-out=gpurun_out/r04_j
+out=gpurun_out/r04_j2
 mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
    > $out/pytest_gpu.log 2>&1

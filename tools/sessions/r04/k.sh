@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session K: bench lines of the other configs on the final tree (dictionary apply for
 # one-gossip slots, event rings): C2, C4's schedule (65,536 dense; 131,072 N x K), C5's shapes.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_k
 mkdir -p $out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session L: the lossy pull's loss draws with their id-hash loads in flight (k_gossip_pull_loss):
 # the parity file on this tree, then C4's schedule at 65,536 with the previous build and 2 / 4 draws per step.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_l
 mkdir -p $out

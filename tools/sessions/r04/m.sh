@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session M: C4's schedule on the final tree — 65,536 dense with 8-bit and with 4-bit
 # infection rounds (what the 8-GPU shards use); the driver's own command (C3, CPU baseline included).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_m
 mkdir -p $out

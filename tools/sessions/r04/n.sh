@@ -2,7 +2,7 @@
 # Round 4, session N: the batched apply's record ranges — walked one range at a time by the whole wave
 # from 64 records up (the product), from 256 up, or never (every range flattened into the quad stream):
 # the parity file through the all-flattened build, then C3's 20/5 window with each.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_n
 mkdir -p $out

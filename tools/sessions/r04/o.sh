@@ -2,7 +2,7 @@
 # Round 4, session O: k_gossip_record's loss draws (delivery records of GossipState.infectedFrom) with
 # 1 (product), 2 or 4 id-hash loads in flight per lane: the parity file through the 4-wide build, then
 # C4's schedule at 65,536 with each.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_o
 mkdir -p $out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session P: the batched apply's long-range threshold around session N's best (256), and 4
 # instead of 2 quads in flight per lane in the flattened stream, on C3's 20/5 window.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_p
 mkdir -p $out

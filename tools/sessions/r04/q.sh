@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4, session Q: k_gossip_pull with 1, 2 (product), 3 or 4 senders' window loads in flight per lane
 # (3 also forced to 4 waves per SIMD), on C3's 20/5 window.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_q
 mkdir -p $out

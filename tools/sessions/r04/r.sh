@@ -3,7 +3,7 @@
 # flattened across the wave instead of walked per lane: the parity file through the product (the
 # per-entry code moved into a lambda) and through the flattened build, then C3 and C4's schedule
 # with each.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_r
 mkdir -p $out

@@ -3,7 +3,7 @@
 # (one per lane per step) instead of walked lane by lane: the parity file through the product (the
 # quad code split into classify / deliver) and through the flattened build, then C3 and C4's
 # schedule with each (flattened at 3 waves/SIMD, and forced to 4).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_s
 mkdir -p $out

@@ -2,7 +2,7 @@
 # Round 4, session V (final tree): rocprofv3 kernel stats of the driver's bench command, PMC FETCH /
 # WRITE over its timed window, the driver's command itself (CPU baseline included), and the half/half
 # partition heal at 16,384 members.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04_v
 mkdir -p $out
