@@ -1364,24 +1364,7 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 #ifndef SWIM_SEL_WAVES
 #define SWIM_SEL_WAVES 6
 #endif
-#ifndef SWIM_SEL_AHEAD
-#define SWIM_SEL_AHEAD 1
-#endif
-#ifndef SWIM_SEL_MW_WORD
-#define SWIM_SEL_MW_WORD 1
-#endif
-#if SWIM_SEL_MW_WORD
-#define SEL_ME(j_) s_mw[w][j_][lane].x
-#else
-#define SEL_ME(j_) s_me[w][j_][lane]
-#endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
-#ifndef SWIM_SEL_FLAT
-#define SWIM_SEL_FLAT 1
-#endif
-#if SWIM_SEL_FLAT && !SWIM_SEL_MW_WORD
-#error "SWIM_SEL_FLAT reads each MIXED entry's holdings word from s_mw"
-#endif
 
 // The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
 // the lanes' exclusive offsets, non-decreasing; every lane calls it, each with its own q).
@@ -1416,14 +1399,8 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
-#if SWIM_SEL_FLAT
-  __shared__ uint32_t s_lk[4][64];  // the flattened MIXED pass's lack bits, by owner lane
-#endif
-#if SWIM_SEL_MW_WORD
+  __shared__ uint32_t s_lk[4][64];  // the MIXED pass's lack bits, by owner lane
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
-#else
-  __shared__ uint32_t s_me[4][4 * SEL_BATCH][64];  // list entries of this step's MIXED entries
-#endif
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t m = P.row0 + blockIdx.x * 4u + w;
@@ -1529,11 +1506,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
           }
           if (wcm == WC_MIXED || scm == WC_MIXED) {
             mixm |= 1u << j;
-#if SWIM_SEL_MW_WORD
             s_mw[w][j][lane] = make_uint2(e, word);  // for the pass below: no list or holdings re-read
-#else
-            s_me[w][j][lane] = e;  // for the pass below: no list re-read
-#endif
             continue;
           }
           if (wcm == WC_ALL) win = held;
@@ -1610,10 +1583,10 @@ __device__ __forceinline__ void select_body(const KP& P) {
         }
         return lack;
       };
-#if SWIM_SEL_FLAT
       {  // the wave's MIXED entries flattened, one per lane per step: a lane's own entries cluster
          // where the list holds the storm's newest words, and walked per lane the wave waited for
-         // the lane with the most (their list entry and holdings word are in s_mw, LDS)
+         // the lane with the most (their list entry and holdings word are in s_mw, LDS; C3 select
+         // 67.0 -> 64.0 ms per 20 periods)
         s_lk[w][lane] = 0u;
         uint32_t tot;
         const uint32_t off = wave_excl_scan((uint32_t)__popc(mixm), &tot);
@@ -1635,64 +1608,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         lackm |= s_lk[w][lane];
-        mixm = 0u;
       }
-#else
-      // entries one at a time from the mask, the infection rounds (32 B) of the next
-      // SWIM_SEL_AHEAD entries loaded before the current one is evaluated
-      uint32_t jn = 0, en = 0;
-      uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
-#if SWIM_SEL_AHEAD >= 2
-      uint32_t jm = 0, em = 0;
-      uint4 m0 = n0, m1 = n0;
-      uint32_t rest = mixm;  // entries not yet loaded
-#endif
-      if (mixm) {
-        jn = (uint32_t)__builtin_ctz(mixm);
-        en = SEL_ME(jn);
-        hd_ld(en, n0, n1);
-#if SWIM_SEL_AHEAD >= 2
-        rest &= rest - 1u;
-        if (rest) {
-          jm = (uint32_t)__builtin_ctz(rest);
-          em = SEL_ME(jm);
-          hd_ld(em, m0, m1);
-          rest &= rest - 1u;
-        }
-#endif
-      }
-      while (mixm) {
-        const uint32_t j = jn;
-        mixm &= mixm - 1u;
-        const uint32_t k = k0 + 256u * (j >> 2) + 4u * lane + (j & 3u);
-        const uint32_t e = en;
-        const uint4 d0 = n0, d1 = n1;
-#if SWIM_SEL_AHEAD >= 2
-        jn = jm;
-        en = em;
-        n0 = m0;
-        n1 = m1;
-        if (rest) {
-          jm = (uint32_t)__builtin_ctz(rest);
-          em = SEL_ME(jm);
-          hd_ld(em, m0, m1);
-          rest &= rest - 1u;
-        }
-#else
-        if (mixm) {
-          jn = (uint32_t)__builtin_ctz(mixm);
-          en = SEL_ME(jn);
-          hd_ld(en, n0, n1);
-        }
-#endif
-#if SWIM_SEL_MW_WORD
-        const uint32_t word = s_mw[w][j][lane].y;
-#else
-        const uint32_t word = hbr[(w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u)];  // cache-resident: read in the pass above
-#endif
-        if (finish_mixed(e, word, k, d0, d1)) lackm |= 1u << j;
-      }
-#endif  // SWIM_SEL_FLAT
       if (lack_ok) {  // positions k0 + 256 jq + 4 lane + i: eight lanes fill one bitmap word
 #pragma unroll
         for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
