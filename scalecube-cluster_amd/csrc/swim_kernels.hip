@@ -3026,10 +3026,10 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       bool cvalid = false;
       if (tot) issue(0u, cr0, cr1, csubj, cm, cvalid);
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
-        uint4 nr0 = make_uint4(0u, 0u, 0u, 0u), nr1 = nr0;
-        uint32_t nsubj = 0u, nm = 0u;
-        bool nvalid = false;
-        if (q0 + 64u < tot) issue(q0 + 64u, nr0, nr1, nsubj, nm, nvalid);  // (uniform)
+        uint4 nx_r0 = make_uint4(0u, 0u, 0u, 0u), nx_r1 = nx_r0;
+        uint32_t nx_subj = 0u, nx_m = 0u;
+        bool nx_valid = false;
+        if (q0 + 64u < tot) issue(q0 + 64u, nx_r0, nx_r1, nx_subj, nx_m, nx_valid);  // (uniform)
         if (cvalid) {
           const uint4 r0 = cr0, r1 = cr1;
           const uint32_t subj = csubj, m = cm;
@@ -3047,11 +3047,11 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
               ++nsubj;
           }
         }
-        cr0 = nr0;
-        cr1 = nr1;
-        csubj = nsubj;
-        cm = nm;
-        cvalid = nvalid;
+        cr0 = nx_r0;  // (nx_: the prefetched step; nsubj is the merged-subject counter)
+        cr1 = nx_r1;
+        csubj = nx_subj;
+        cm = nx_m;
+        cvalid = nx_valid;
       }
 #else
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
