@@ -2746,9 +2746,6 @@ constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flig
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
 constexpr uint32_t AW_LONG = SWIM_AW_LONG;
-#ifndef SWIM_AW_MPIPE
-#define SWIM_AW_MPIPE 0
-#endif
 constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
@@ -3002,58 +2999,6 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
       uint32_t tot;
       const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
-#if SWIM_AW_MPIPE
-      // the next step's entry records, subjects and way masks are loaded before this step's table
-      // cells are read (one dependent round trip per step instead of two)
-      auto issue = [&](uint32_t q0, uint4& r0, uint4& r1, uint32_t& subj, uint32_t& m, bool& valid) {
-        const uint32_t q = q0 + lane;
-        const uint32_t o = wave_owner(off, q);
-        const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
-        valid = q < tot;
-        if (valid) {
-          const uint32_t b = kth_set_bit(bo, q - oo);
-          const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
-          const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
-          const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
-          r0 = dr[0];
-          r1 = dr[1];
-          subj = P.d_subj[base / DICT_WAYS];
-          m = (s_bm[t] >> (8u * j)) & 0xFFu;
-        }
-      };
-      uint4 cr0 = make_uint4(0u, 0u, 0u, 0u), cr1 = cr0;
-      uint32_t csubj = 0u, cm = 0u;
-      bool cvalid = false;
-      if (tot) issue(0u, cr0, cr1, csubj, cm, cvalid);
-      for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
-        uint4 nx_r0 = make_uint4(0u, 0u, 0u, 0u), nx_r1 = nx_r0;
-        uint32_t nx_subj = 0u, nx_m = 0u;
-        bool nx_valid = false;
-        if (q0 + 64u < tot) issue(q0 + 64u, nx_r0, nx_r1, nx_subj, nx_m, nx_valid);  // (uniform)
-        if (cvalid) {
-          const uint4 r0 = cr0, r1 = cr1;
-          const uint32_t subj = csubj, m = cm;
-          uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
-                              max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
-          best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
-                               max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
-          if (via_inbox) {
-            spill(subj, best);
-          } else {
-            const uint32_t c = cell_get(P, p, subj);
-            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
-              apply(subj, best);
-            else
-              ++nsubj;
-          }
-        }
-        cr0 = nx_r0;  // (nx_: the prefetched step; nsubj is the merged-subject counter)
-        cr1 = nx_r1;
-        csubj = nx_subj;
-        cm = nx_m;
-        cvalid = nx_valid;
-      }
-#else
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
         const uint32_t o = wave_owner(off, q);
@@ -3081,7 +3026,6 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           }
         }
       }
-#endif
       wsync();  // every lane has read its blocks' bits
 #pragma unroll
       for (uint32_t u = 0; u < 8u; ++u)
