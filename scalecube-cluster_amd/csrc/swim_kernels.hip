@@ -3828,7 +3828,10 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 
 // onSync (MembershipProtocolImpl.java:352-373) at receiver j = blockIdx, requests in
 // (sender, kind) order; each SYNC_ACK payload is j's table right after that request's merge.
-__global__ void __launch_bounds__(256) k_sync_merge(KP P) {
+#ifndef SWIM_SYNC_WAVES
+#define SWIM_SYNC_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
@@ -3893,7 +3896,7 @@ __global__ void __launch_bounds__(256) k_sync_merge(KP P) {
 }
 
 // onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
-__global__ void __launch_bounds__(256) k_sync_ack(KP P) {
+__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
   const uint32_t i = P.row0 + blockIdx.x;
