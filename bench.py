@@ -71,10 +71,12 @@ WORKLOADS = {
     "c5s": dict(desc="C5 geometry at 262,144 members: N x K tracked-subject views (K = 256), LAN defaults, 256 "
                      "simultaneous crashes",
                 n=1 << 18, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
-    # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows
+    # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows.
+    # Ring: 5 * 2^20 slots (a non-power-of-two ring, ids mod GC), 1.25x the ~4.2e6 live one-gossip slots
+    # C4's storm law predicts
     "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
                     "0.1% simultaneous crash",
-               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=1 << 22, scap=4096),
+               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=5 << 20, scap=4096),
     # C4's schedule on ONE GPU in N x K mode (the dense 262,144^2 view needs 8 GPUs): measures the
     # storm C4's 1 % loss and 0.1 % crash create, to size C4's ring (1 % loss: one gossip per slot)
     "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
@@ -99,7 +101,11 @@ WORKLOADS = {
     "c3half16k": dict(desc="C3 schedule with the half/half partition at 16,384 members: dense, LAN defaults, 10% "
                            "simultaneous crash + id-parity partition for 40 periods healed via SYNC",
                       n=16384, preset="lan", loss=0.0, crash=0.10, part=40, part_group=8192, gcap=1 << 18,
-                      rcap=1 << 27),
+                      rcap=1 << 27, dsub=16384),
+    "c3half32k": dict(desc="C3 schedule with the half/half partition at 32,768 members: dense, LAN defaults, 10% "
+                           "simultaneous crash + id-parity partition for 40 periods healed via SYNC",
+                      n=32768, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16384, gcap=1 << 18,
+                      rcap=1 << 29, dsub=32768),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }
@@ -238,6 +244,8 @@ def make_cluster(workload, device, seed, event_capacity=0, sharded=False, batchi
     gcap = w["gcap"] if batching else max(w["gcap"], w.get("gcap_unbatched", 1 << 20))
     if w.get("rcap"):
         kw["record_capacity"] = w["rcap"]
+    if w.get("dsub"):
+        kw["dict_subjects"] = w["dsub"]
     kw.update(extra)
     c = cls(cfg, w["n"], seed=seed, gossip_capacity=gcap, device=device, gossip_batching=batching,
             event_capacity=event_capacity, sync_capacity=w.get("scap", 0), **kw)

@@ -133,6 +133,11 @@ typedef struct swim_config {
                                rounds 15 or more after it in an escape table (exact either way; halves the
                                largest array); 0 = 4 when the 8-bit array would exceed
                                96 GiB on this handle, else 8 */
+  uint32_t dict_subjects;   /* record dictionary of the batched apply: subjects with live
+                               gossip records that each get a block of 8 entries (a power of two, 4 ..
+                               2^20; 0 = 8,192). A subject without a block merges through the spill table;
+                               each receiver in flight keeps dict_subjects bytes of entry bitmap in LDS, so
+                               larger dictionaries run fewer receivers per CU */
 } swim_config;
 
 typedef struct swim_stats {
@@ -185,6 +190,9 @@ typedef struct swim_stats {
   uint64_t escape_entries;    /* 4-bit infection rounds: live escape-table entries after the last period's
                                  sweep; 0 in the oracle and on 8-bit handles */
   uint64_t escape_capacity;   /* the escape table's entries (0 on 8-bit handles)                      */
+  uint64_t apply_skipped;     /* dictionary blocks the batched apply skipped by their merge mark: every
+                                 received record already found not to override the cell (DESIGN.md
+                                 §3.15); 0 in the oracle */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
@@ -266,6 +274,11 @@ int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag);
  * accepted ALIVE record draws with counter SWIM_DELIVER_ATTEMPT | k in that period's FD tick. A stopped
  * member receives nothing. records[k] must not be SWIM_ABSENT (a SyncData carries present records). */
 #define SWIM_DELIVER_ATTEMPT 0x80000000u
+/* reason flag (with SWIM_R_MEMBERSHIP_GOSSIP): the records are gossips with ids new to the observer
+ * (GossipProtocolImpl.onGossipReq, :171-183): each one's GossipState is put before membership handles
+ * it, so the observer forwards it in later rounds like a gossip it created (with its next gossip
+ * sequence number as the id); the host drops ids it delivered to the observer before (swimhip/wire.py) */
+#define SWIM_DELIVER_FORWARD 0x100u
 int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subjects, const uint32_t* records,
                          uint32_t n, uint32_t reason);
 /* Optional trace streams into the event ring (mask of SWIM_TRACE_*; 0 = off, the default). */

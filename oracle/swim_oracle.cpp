@@ -1316,15 +1316,22 @@ int oracle_spread(oracle_handle* h, uint32_t origin, uint32_t tag) {
 int oracle_deliver_records(oracle_handle* h, uint32_t obs, const uint32_t* subj, const uint32_t* rec, uint32_t n,
                            uint32_t reason) {
   if (!h || obs >= h->N || (n && (!subj || !rec))) return SWIM_EINVAL;
+  // SWIM_DELIVER_FORWARD: each record is a gossip new to obs; GossipProtocolImpl.onGossipReq
+  // (GossipProtocolImpl.java:171-183) puts its GossipState (obs forwards it) before membership sees it
+  const bool fwd = (reason & SWIM_DELIVER_FORWARD) != 0u;
+  reason &= ~SWIM_DELIVER_FORWARD;
   if (reason != SWIM_R_SYNC && reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC) return SWIM_EINVAL;
+  if (fwd && reason != SWIM_R_MEMBERSHIP_GOSSIP) return SWIM_EINVAL;
   for (uint32_t k = 0; k < n; ++k)
     if (subj[k] >= h->N || rec[k] == SWIM_ABSENT) return SWIM_EINVAL;
   Member& me = h->m[obs];
   if (!me.alive) return SWIM_OK;
   const uint32_t tick = tick_of(h, 0), snap = me.others;
-  for (uint32_t k = 0; k < n; ++k)
+  for (uint32_t k = 0; k < n; ++k) {
+    if (fwd) spread_gossip(h, obs, subj[k], rec[k], (int64_t)h->period * h->G);
     update_membership(h, obs, subj[k], rec[k], reason, 0, SWIM_DELIVER_ATTEMPT | k, tick, snap,
                       (int64_t)h->period * h->G);
+  }
   finish_phase(h);
   return SWIM_OK;
 }

@@ -56,7 +56,7 @@ struct swim_handle {
   uint32_t *cs_ghist = nullptr, *cs_ctr = nullptr, *cs_stat = nullptr;
   uint32_t cs_maxt = 1;
   // k_gossip_apply launch: persistent workgroups (one or two per CU) and their dynamic LDS bytes
-  uint32_t apply_blocks = 1, apply_blocks_b = 1;
+  uint32_t apply_blocks = 1, apply_blocks_b = 1, apply_waves_b = 1;
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   uint32_t CC = 0;  // record ring of the gossip batches
@@ -285,7 +285,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
     if (h->dict_on) {
       hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, DICT_SIDS / 256)), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, P.dsids / 256)), dim3(256), 0, s, P);
     }
   });
   return SWIM_OK;
@@ -535,12 +535,13 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject
           // runs it takes as run tops (C4's lossy storm: apply 373 -> 104 ms per 20 periods, §6.4)
           if (P.batched || h->dict_on)
-            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * AW_WAVES),
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b),
                                h->apply_lds_b, s, P);
           else
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
                                h->apply_lds, s, P);
         });
+        timed(h, 7, "k_spill_clear", [&] { hipLaunchKernelGGL(k_spill_clear, dim3(64), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;
@@ -697,8 +698,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     return SWIM_EINVAL;
   const uint32_t world = c.shard_world ? c.shard_world : 1u;
   if (world > SWIM_MAX_WORLD || c.shard_rank >= world || c.n_members % world) return SWIM_EINVAL;
-  // gossip ring: a power of two of at least 1024 slots (64-slot chunks, 32-slot bitmap words)
-  if (c.gossip_capacity && ((c.gossip_capacity & (c.gossip_capacity - 1)) || c.gossip_capacity < 1024u))
+  // gossip ring: a multiple of 1,024 slots (64-slot chunks, 32-slot bitmap words in aligned quads);
+  // a power of two masks ids, any other size takes them mod GC
+  if (c.gossip_capacity && (c.gossip_capacity % 1024u || c.gossip_capacity > (1u << 28))) return SWIM_EINVAL;
+  if (c.dict_subjects && ((c.dict_subjects & (c.dict_subjects - 1u)) || c.dict_subjects < 4u || c.dict_subjects > (1u << 20)))
     return SWIM_EINVAL;
   if ((c.infection_round_bits != 0u && c.infection_round_bits != 4u && c.infection_round_bits != 8u) ||
       c.gossip_batching > 1u ||
@@ -745,6 +748,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   KP& P = h->base;
   P.N = N;
   P.GC = h->GC;
+  P.gpow2 = (h->GC & (h->GC - 1)) == 0 ? 1u : 0u;
   P.gmask = h->GC - 1;
   P.G = h->G;
   P.S = h->S;
@@ -772,11 +776,15 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
     const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU
     h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
-    // the batch-slot variant: one receiver per wave, AW_WAVES waves per workgroup, each with its
-    // own entry bitmap; as many workgroups per CU as the 160 KiB of LDS (and 2,048 threads) allow
-    h->apply_lds_b = 4ull * AW_WAVES * AW_WORDS;
+    // the batch-slot variant: one receiver per wave, up to AW_WAVES waves per workgroup, each with
+    // its own entry bitmap (dict_subjects bytes); as many workgroups per CU as the 160 KiB of LDS
+    // (and 2,048 threads) allow
+    P.dsids = c.dict_subjects ? c.dict_subjects : DICT_SIDS;
+    const uint64_t wave_lds = 4ull * aw_words(P.dsids);
+    h->apply_waves_b = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(AW_WAVES, (160ull * 1024u) / wave_lds));
+    h->apply_lds_b = wave_lds * h->apply_waves_b;
     const uint32_t per_cu_b = std::max<uint32_t>(
-        1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
+        1, std::min<uint32_t>(2048 / (64 * h->apply_waves_b), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
     h->apply_blocks_b = (uint32_t)std::max(1, cus) * per_cu_b;
     for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply), reinterpret_cast<const void*>(&k_gossip_apply_h4)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
@@ -805,7 +813,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   // gossip records: batch slots keep their gossips in a ring of their own; a phase stages at most
   // as many gossips as can be live (the commit raises OV_GOSSIP beyond the ring)
   h->CC = c.record_capacity ? c.record_capacity
-                            : std::min<uint32_t>(1u << 24, std::max<uint32_t>(1u << 21, 4u * h->GC));
+                            : std::min<uint32_t>(1u << 24, std::max<uint32_t>(1u << 21, pow2ceil(4ull * h->GC)));
   P.cmask = h->CC - 1u;
   P.batch_commit = c.gossip_batching == 0 ? 1u : 0u;  // no loss set yet
   P.batched = 0u;  // set by the first batch commit (swim_api: commit_sorted)
@@ -838,7 +846,16 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (rc == SWIM_OK) rc = dalloc(h, &(ptr), (count));
   ALLOC(P.view, NN);
   ALLOC(P.dl, NN);
-  ALLOC(P.inbox, NN);
+  {  // spill table: 64 slots per local row, 2^16 .. 2^23 (16 B each: <= 128 MiB)
+    const uint32_t spc = pow2ceil(std::min<uint64_t>(1ull << 23, std::max<uint64_t>(1ull << 16, NL * 64ull)));
+    ALLOC(P.sp_key, spc);
+    ALLOC(P.sp_val, spc);
+    ALLOC(P.sp_used, spc);
+    P.spmask = spc - 1u;
+    uint32_t* nl = nullptr;
+    ALLOC(nl, N);
+    P.none_last = nl;
+  }
   ALLOC(P.hb, NL * (h->GC / 32));
   ALLOC(P.wb, NL * (h->GC / 32));
   // infection rounds: 8 bits per (member, slot), or 4-bit offsets + the escape table
@@ -898,10 +915,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (h->dict_on) {
     ALLOC(P.c_id, h->CC);
     ALLOC(P.sid_of, N);
-    ALLOC(P.d_subj, DICT_SIDS);
-    ALLOC(P.d_rec, DICT_IDS);
-    ALLOC(P.d_last, DICT_IDS);
-    ALLOC(P.d_free, DICT_SIDS);
+    ALLOC(P.d_subj, P.dsids);
+    ALLOC(P.d_rec, (size_t)P.dsids * DICT_WAYS);
+    ALLOC(P.d_last, (size_t)P.dsids * DICT_WAYS);
+    ALLOC(P.d_free, P.dsids);
+    ALLOC(P.d_gen, P.dsids);
+    ALLOC(P.dmark, NL * P.dsids);
   }
   ALLOC(P.wsum, h->GC / 32);
   ALLOC(P.scnt, h->GC);
@@ -1014,8 +1033,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.mv_head, (size_t)N, NONE);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.mv_next, (size_t)N, NONE);
   (void)hipMemsetAsync(P.joining, 0, N, s);
-  (void)hipMemsetAsync(P.dl, 0, NN * 4, s);
-  (void)hipMemsetAsync(P.inbox, 0, NN * 4, s);
+  (void)hipMemsetAsync(P.dl, 0, NN * 2, s);
+  (void)hipMemsetAsync(P.sp_key, 0, ((size_t)P.spmask + 1) * 8, s);
+  (void)hipMemsetAsync(P.sp_val, 0, ((size_t)P.spmask + 1) * 4, s);
+  (void)hipMemsetAsync(const_cast<uint32_t*>(P.none_last), 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.hb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.wb, 0, NL * (h->GC / 32) * 4, s);
   if (P.hd4) {
@@ -1059,9 +1080,11 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.ctl, 0, sizeof(Ctl), s);
   if (h->dict_on) {
     (void)hipMemsetAsync(P.sid_of, 0xFF, (size_t)N * 4, s);
-    (void)hipMemsetAsync(P.d_subj, 0xFF, (size_t)DICT_SIDS * 4, s);
-    (void)hipMemsetAsync(P.d_rec, 0, (size_t)DICT_IDS * 4, s);
-    (void)hipMemsetAsync(P.d_last, 0, (size_t)DICT_IDS * 4, s);
+    (void)hipMemsetAsync(P.d_subj, 0xFF, (size_t)P.dsids * 4, s);
+    (void)hipMemsetAsync(P.d_rec, 0, (size_t)P.dsids * DICT_WAYS * 4, s);
+    (void)hipMemsetAsync(P.d_last, 0, (size_t)P.dsids * DICT_WAYS * 4, s);
+    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.dsids, 256)), dim3(256), 0, s, P.d_gen, (size_t)P.dsids, 1u);
+    (void)hipMemsetAsync(P.dmark, 0, NL * P.dsids * 4, s);
   }
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
@@ -1205,8 +1228,21 @@ int swim_set_delay(swim_handle* h, uint32_t mean_ms) {
   if (!P.dq && P.nloc > 65536u)
     return fail(h, SWIM_EINVAL, "swim_set_delay: the delayed-message rings are sized for clusters up to 65,536 members");
   if (!P.dq) {  // per receiver: messages in flight plus the arrived ones still inside the horizon
-    uint32_t cap = 65536;  // entries per receiver, within 2 GiB of rings
-    while (cap > 4096u && (uint64_t)P.nloc * cap * 16u > (2ull << 30)) cap >>= 1;
+    // A receiver pushes up to (in-degree x window) entries per round and each stays up to dq_live
+    // rounds: a 1 s mean on LAN (200 ms rounds, dq_live ~ 136 rounds) under 2 % loss at 256 members
+    // pushes ~5e4 entries per receiver and round at its peak (every message of every window draws a
+    // delay, held gossips included), and the exponential tail keeps some entries live for ~110
+    // rounds. The ring takes the most entries per receiver (up to 2^23) that 1/16 of the free device
+    // memory allows (SWIMHIP_DQCAP: a power of two instead); one that still wraps over a live entry
+    // raises OV_IFROM (IF_DELAYQ).
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    uint32_t cap = 1u << 23;
+    while (cap > 4096u && (uint64_t)P.nloc * cap * 16u > free_b / 16u) cap >>= 1;
+    if (const char* e = std::getenv("SWIMHIP_DQCAP")) {
+      const unsigned long v = std::strtoul(e, nullptr, 10);
+      if (v >= 64u && v <= (1ul << 26) && (v & (v - 1ul)) == 0ul) cap = (uint32_t)v;
+    }
     uint4* dq = nullptr;
     uint32_t *head = nullptr, *rhead = nullptr;
     int rc = dalloc(h, &dq, (size_t)P.nloc * cap);
@@ -1429,8 +1465,11 @@ int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag) {
 int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subjects, const uint32_t* records,
                          uint32_t n, uint32_t reason) {
   if (!h || observer >= h->N || (n && (!subjects || !records))) return SWIM_EINVAL;
-  if (reason != SWIM_R_SYNC && reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC)
+  const uint32_t base_reason = reason & ~SWIM_DELIVER_FORWARD;
+  if (base_reason != SWIM_R_SYNC && base_reason != SWIM_R_MEMBERSHIP_GOSSIP && base_reason != SWIM_R_INITIAL_SYNC)
     return fail(h, SWIM_EINVAL, "swim_deliver_records: reason must be SYNC, INITIAL_SYNC or MEMBERSHIP_GOSSIP");
+  if ((reason & SWIM_DELIVER_FORWARD) && base_reason != SWIM_R_MEMBERSHIP_GOSSIP)
+    return fail(h, SWIM_EINVAL, "swim_deliver_records: SWIM_DELIVER_FORWARD goes with MEMBERSHIP_GOSSIP");
   for (uint32_t k = 0; k < n; ++k)
     if (subjects[k] >= h->N || records[k] == SWIM_ABSENT)
       return fail(h, SWIM_EINVAL, "swim_deliver_records: subject out of range or an absent record");
@@ -1449,7 +1488,8 @@ int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subj
   KP P;
   set_phase(h, P, 0);  // the coming period: its deadlines, FD tick and first gossip round
   if (P.nxk) {  // every shard requests (and so allocates) the same columns
-    hipLaunchKernelGGL(k_deliver_track, dim3(1), dim3(256), 0, s, P, h->deliver_buf, h->deliver_buf + n, n);
+    hipLaunchKernelGGL(k_deliver_track, dim3(1), dim3(256), 0, s, P, h->deliver_buf, h->deliver_buf + n, n,
+                       (reason & SWIM_DELIVER_FORWARD) ? 1u : 0u);
     track_commit(h, P);
   }
   hipLaunchKernelGGL(k_deliver, dim3(1), dim3(64), 0, s, P, observer, h->deliver_buf, h->deliver_buf + n, n, reason);
@@ -1558,30 +1598,32 @@ int swim_read_view(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n)
 
 int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32_t n) {
   if (!h || !row || observer - h->base.row0 >= h->base.nloc || n != h->N) return SWIM_EINVAL;
-  // cell-major storage: strided 2D copy of one observer column
-  if (!h->base.nxk) {
-    HIPC(h, hipMemcpy2DAsync(row, 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4, h->N,
-                             hipMemcpyDeviceToHost, h->stream));
-    HIPC(h, hipStreamSynchronize(h->stream));
-    return SWIM_OK;
+  // cell-major u16 storage: strided 2D copy of one observer column, decoded at the coming period
+  // (the absolute deadline + 1, as the oracle keeps it)
+  const uint32_t t = (uint32_t)h->period;
+  std::vector<uint32_t> subj;
+  if (h->base.nxk) {
+    int rc = tracked_columns(h, &subj);
+    if (rc) return rc;
   }
-  std::vector<uint32_t> subj, cells;
-  int rc = tracked_columns(h, &subj);
-  if (rc) return rc;
-  cells.resize(subj.size());
-  if (!subj.empty())
-    HIPC(h, hipMemcpy2DAsync(cells.data(), 4, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 4, 4,
-                             subj.size(), hipMemcpyDeviceToHost, h->stream));
+  const size_t ncol = h->base.nxk ? subj.size() : h->N;
+  std::vector<uint16_t> cells(ncol);
+  if (ncol)
+    HIPC(h, hipMemcpy2DAsync(cells.data(), 2, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 2, 2,
+                             ncol, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
   std::fill(row, row + n, 0u);
-  for (size_t c = 0; c < subj.size(); ++c) row[subj[c]] = cells[c];
+  for (size_t c = 0; c < ncol; ++c)
+    if (cells[c]) row[h->base.nxk ? subj[c] : c] = dl_dec(cells[c], t) + 1u;
   return SWIM_OK;
 }
 
 int swim_digest(swim_handle* h, uint64_t* vd, uint64_t* dd) {
   if (!h) return SWIM_EINVAL;
   HIPC(h, hipMemsetAsync(h->d_digest, 0, 16, h->stream));
-  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, h->base, h->d_digest);
+  KP Q = h->base;
+  Q.period = (uint32_t)h->period;  // deadlines decode at the coming period (dl_dec)
+  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, h->stream, Q, h->d_digest);
   unsigned long long out[2];
   HIPC(h, hipMemcpyAsync(out, h->d_digest, 16, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -1682,13 +1724,14 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->events_updated = stats[ST_UPDATED];
   out->apply_pairs = stats[ST_APPLY_PAIRS];
   out->commit_radix = stats[ST_COMMIT_RADIX];
+  out->apply_skipped = stats[ST_APPLY_SKIP];
   out->escape_entries = ctl.hx_live;
   out->escape_capacity = h->base.hd4 ? (uint64_t)h->base.hxmask + 1u : 0u;
   {  // gossips in the live slots: the record ring from the oldest live slot's first record
     uint32_t c_lo = ctl.ccount;
     if (ctl.gcount != ctl.glo && ctl.gcount - ctl.glo <= h->GC) {
       uint2 cr;
-      HIPC(h, hipMemcpy(&cr, h->base.g_cref + (ctl.glo & (h->GC - 1)), 8, hipMemcpyDeviceToHost));
+      HIPC(h, hipMemcpy(&cr, h->base.g_cref + (ctl.glo % h->GC), 8, hipMemcpyDeviceToHost));
       c_lo = cr.x;
     }
     out->live_gossip_records = ctl.ccount - c_lo;
@@ -1815,7 +1858,7 @@ int swim_debug_holdings(swim_handle* h, uint32_t member, uint32_t* out_hash, uin
   const uint32_t rnow = (uint32_t)(h->period * h->G);  // next round to run
   if (hi - lo > GC) lo = hi - GC;
   for (uint32_t id = lo; id < hi; ++id) {
-    const uint32_t s = id & (GC - 1);
+    const uint32_t s = id % GC;
     if (!((bits[s >> 5] >> (s & 31)) & 1u)) continue;
     for (uint32_t x = cref[s].x; x != cref[s].y; ++x) {  // every gossip of the slot's batch
       if (n < cap) {

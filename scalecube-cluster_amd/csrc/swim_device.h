@@ -2,9 +2,10 @@
 //
 // Data layout in HBM (dense mode, N members, GC gossip slots):
 //   view   u32[N][N]  observer-major packed records  (MembershipProtocolImpl.java:87)
-//   dl     u32[N][N]  SUBJECT-major suspicion deadlines (+1, 0 = none) so the timeout sweep
+//   dl     u16[N][N]  SUBJECT-major suspicion deadlines (dl_enc, 0 = none) so the timeout sweep
 //                     streams one subject column over all observers (MembershipProtocolImpl.java:101)
-//   inbox  u32[N][N]  observer-major lattice max of the records a gossip round delivered
+//   sp_*   spill table: lattice max per (observer, subject) of a round's records that found no LDS
+//                     slot / dictionary entry (bounded open addressing, emptied after every round)
 //   hb     u32[N][GC/32] member-major "holds gossip slot s now" bitmap
 //   hd     u8[N][GC]     infection round (mod 2^8) of each held gossip
 //                     (GossipProtocolImpl.java:49, GossipState.java:14)
@@ -56,11 +57,12 @@ enum StatIdx : int {
   ST_APPLY_RUNS,   // subject-run representatives it read from the ring and hashed
   ST_APPLY_SUBJ,   // updateMembership calls it made (one per subject per receiver)
   ST_FD_DEAD_EV,   // FailureDetectorEvent(DEAD): a DEST_GONE ack (FailureDetectorImpl.java:231-235,383)
-  ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the global inbox
+  ST_APPLY_SPILL,  // subjects k_gossip_apply merged through the spill table
   ST_APPLY_RECS,   // gossip records of batch slots k_gossip_apply_b expanded into its entry bitmap
   ST_UPDATED,      // MembershipEvent UPDATED (MembershipProtocolImpl.java:599-600)
   ST_APPLY_PAIRS,  // receiver pairs k_gossip_apply processed in two half-workgroups (SWIM_APPLY_PAIR)
   ST_COMMIT_RADIX, // commit phases sorted by the chip-wide radix sort (more than CS_SMALL gossips)
+  ST_APPLY_SKIP,   // dictionary blocks k_gossip_apply_b skipped by their merge mark (no cell read)
   ST_COUNT
 };
 
@@ -68,7 +70,7 @@ enum Overflow : uint32_t {
   OV_EVENTS = 1u,
   OV_GOSSIP = 2u,
   OV_SYNC = 4u,
-  OV_SPILL = 8u,  // a receiver spilled more subjects in one round than its LDS spill list holds
+  OV_SPILL = 8u,  // the spill table (or a receiver's LDS spill list) is out of slots
   OV_BUCKET = 16u,
   OV_BUG = 32u,  // a device-side invariant check failed (bounded loop exhausted)
   OV_IFROM = 64u,  // infectedFrom bookkeeping out of capacity or a delivery predicted never to
@@ -132,6 +134,7 @@ struct Ctl {
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
+  uint32_t sp_n;        // spill-table slots claimed this round (sp_used), reset by k_finalize
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
@@ -142,8 +145,9 @@ enum WordClass : uint32_t { WC_NONE = 0, WC_MIXED = 1, WC_ALL = 2 };
 struct KP {
   // sizes / config
   uint32_t N, GC, gmask, G, S, f, kreq, rm, mult, n_seeds, time_left_pos;
+  uint32_t gpow2;  // GC is a power of two (gmask = GC - 1); else ids map to slots mod GC (gmod)
   // observer-row shard of this handle: members [row0, row0 + nloc) live here;
-  // view/inbox/hb/wb/nb/hd rows and dl columns are indexed by the local row m - row0
+  // view/hb/wb/nb/hd rows and dl columns are indexed by the local row m - row0
   uint32_t row0, nloc, rank, world;
   // view geometry: a row holds W cells; dense W = N (cell = subject), N x K mode (nxk = 1) W = K
   // (cell = the subject's column, colmap); an untracked subject reads as BASELINE everywhere
@@ -181,9 +185,19 @@ struct KP {
   uint32_t* jwin;     // [N] the seed member whose SYNC_ACK the joiner merges (first round trip), or NONE
   // state
   uint32_t* view;
-  uint32_t* dl;  // [W cells][nloc observers] suspicion deadline + 1 (0 = none), subject-major
+  uint16_t* dl;  // [W cells][nloc observers] suspicion deadline (dl_enc; 0 = none), subject-major
   uint32_t* colmin;
-  uint32_t* inbox;
+  // Spill table of the gossip apply (replaces a dense [nloc][W] inbox): the lattice
+  // max per (local row, cell) of the round's records that found no LDS slot / dictionary entry. Open
+  // addressing on key = row * W + cell + 1; a key is claimed by CAS and never freed inside the round
+  // (probe chains never break), the claimed slots are listed in sp_used and emptied after the round's
+  // apply (k_spill_clear). A key that finds no slot within SP_PROBE raises OV_SPILL.
+  unsigned long long* sp_key;  // [spmask + 1]
+  uint32_t* sp_val;            // [spmask + 1]
+  uint32_t* sp_used;           // [spmask + 1] slots claimed this round (Ctl::sp_n of them)
+  uint32_t spmask;
+  const uint32_t* none_last;   // [N] per subject: unwrapped end of its newest record without a
+                               // dictionary entry (k_dict_entries); such a subject merges via the spill table
   uint32_t* hb;  // [N][GC/32] holds-now bitmap (set on receipt, cleared by the owner's sweep)
   uint16_t* mm;   // [N][GC/32] oldest (low byte) / newest (high byte) infection round (mod 2^8) the
                   // member holds in the word (valid while it holds any): most MIXED words resolve per
@@ -243,11 +257,19 @@ struct KP {
   // is an entry of its subject's block of DICT_WAYS entries; c_id names each ring record's entry,
   // so a receiver ORs one bit per received record into an LDS bitmap and merges per block.
   uint32_t* sid_of;   // [N] subject -> its block, NONE
-  uint32_t* d_subj;   // [DICT_SIDS] block -> subject, NONE while free
-  uint32_t* d_rec;    // [DICT_IDS] packed record of each entry, 0 = empty (no record packs to 0)
-  uint32_t* d_last;   // [DICT_IDS] unwrapped index + 1 of the newest ring record naming the entry
-  uint32_t* d_free;   // [DICT_SIDS] stack of free blocks
+  uint32_t dsids;     // subject blocks (swim_config.dict_subjects; DICT_SIDS by default)
+  uint32_t* d_subj;   // [dsids] block -> subject, NONE while free
+  uint32_t* d_rec;    // [dsids * DICT_WAYS] packed record of each entry, 0 = empty (no record packs to 0)
+  uint32_t* d_last;   // [dsids * DICT_WAYS] unwrapped index + 1 of the newest ring record naming the entry
+  uint32_t* d_free;   // [dsids] stack of free blocks
   uint32_t* c_id;     // [CC] entry of each record-ring record; ID_USER, or ID_NONE (slow path)
+  // Merge marks of the batched apply: per (local row, block) the entries whose
+  // records the receiver already found not to override its (present) cell, tagged with the block's
+  // generation: mark = gen24 << 8 | way mask. A block's generation moves whenever one of its entries
+  // is emptied or the block is freed (k_dict_free), and a removal of the cell clears the mark
+  // (mark_clear), so a valid mark's entries are <= the cell: cells only grow while present.
+  uint32_t* dmark;    // [nloc][dsids] or nullptr (no dictionary)
+  uint32_t* d_gen;    // [dsids] generation of each block (low 24 bits never 0)
   uint2* g_sr;        // [GC] (subject, packed record) of each slot's first gossip (the gossip itself
                       // for a one-gossip slot)
   uint32_t* runw;     // [GC/32] bit s: slot s starts a run of one subject (a commit sorts its gossips
@@ -373,7 +395,7 @@ constexpr uint32_t NONE_U32 = NONE;
 #ifndef SWIM_DICT_SIDS
 #define SWIM_DICT_SIDS 8192
 #endif
-constexpr uint32_t DICT_SIDS = SWIM_DICT_SIDS;   // subject blocks
+constexpr uint32_t DICT_SIDS = SWIM_DICT_SIDS;   // subject blocks by default (swim_config.dict_subjects)
 constexpr uint32_t DICT_WAYS = 8;                // distinct live records per subject
 constexpr uint32_t DICT_IDS = DICT_SIDS * DICT_WAYS;
 constexpr uint32_t DICT_WORDS = DICT_IDS / 32u;  // a receiver's entry bitmap
@@ -381,18 +403,26 @@ constexpr uint32_t ID_USER = 0xFFFFFFFEu;        // c_id of a user gossip (subje
 constexpr uint32_t ID_NONE = NONE;               // c_id of a record that found no entry
 constexpr uint32_t DICT_LOCK = 0xFFFFFFFEu;      // sid_of while k_dict_claim allocates the block
 // sid_of of a subject whose claim found no block: DICT_NOBLK | (the commit's first record index &
-// DICT_TAG_MASK); a later commit may claim again (k_dict_claim). Never a block id (< 2^16).
+// DICT_TAG_MASK); a later commit may claim again (k_dict_claim). Never a block id (< 2^20).
 constexpr uint32_t DICT_NOBLK = 0x80000000u;
 constexpr uint32_t DICT_TAG_MASK = 0x3FFFFFFFu;
 static_assert(DICT_SIDS >= 4 && (DICT_SIDS & (DICT_SIDS - 1)) == 0 && DICT_SIDS <= (1u << 16),
               "SWIM_DICT_SIDS: a power of two in 4 .. 65536");
 
 
+// Ring slot of gossip id `id` and ring word of unwrapped word index `wi`. A power-of-two ring masks;
+// any other multiple of 1,024 slots (C4's 5 * 2^20: DESIGN.md §4.2) takes the remainder, and its ids
+// must not wrap 2^32 (k_commit raises OV_GOSSIP before they do)
+__device__ __forceinline__ uint32_t gmod(const KP& P, uint32_t id) { return P.gpow2 ? (id & P.gmask) : id % P.GC; }
+__device__ __forceinline__ uint32_t wmod(const KP& P, uint32_t wi) {
+  return P.gpow2 ? (wi & ((P.GC >> 5) - 1u)) : wi % (P.GC >> 5);
+}
+
 // the unwrapped index of the live record ring's first record: the oldest possibly-live slot's
 // first one (the ring's end when no slot is live)
 __device__ __forceinline__ uint32_t live_rec_lo(const KP& P) {
   const uint32_t glo = P.ctl->glo, g0 = P.ctl->gcount;
-  return (g0 != glo && g0 - glo <= P.GC) ? P.g_cref[glo & P.gmask].x : P.ctl->ccount;
+  return (g0 != glo && g0 - glo <= P.GC) ? P.g_cref[gmod(P, glo)].x : P.ctl->ccount;
 }
 
 // the member whose transport receives a message sent to member x (TransportImpl sends to
@@ -770,6 +800,57 @@ __device__ __forceinline__ bool fetch_ok(const KP& P, uint32_t obs, uint32_t sub
          msg_delay(P, K_MREQ, obs, subj, attempt, P.tick) + msg_delay(P, K_MRESP, subj, obs, attempt, P.tick) < P.mto;
 }
 
+// the spill table (KP::sp_key): the record's lattice max into (receiver p, cell c); returns the slot,
+// *first = this call claimed the key (its caller lists the slot for the round's merge)
+constexpr uint32_t SP_PROBE = 128;
+__device__ __forceinline__ uint32_t spill_put(const KP& P, uint32_t p, uint32_t c, uint32_t rec, bool* first) {
+  const unsigned long long key = (unsigned long long)lrow(P, p) * P.W + c + 1ull;
+  uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & P.spmask;
+  *first = false;
+  for (uint32_t q = 0; q < SP_PROBE; ++q, h = (h + 1u) & P.spmask) {
+    unsigned long long k = P.sp_key[h];
+    if (k == 0ull) {
+      k = atomicCAS(&P.sp_key[h], 0ull, key);
+      if (k == 0ull) {
+        atomicMax(&P.sp_val[h], rec);
+        *first = true;
+        P.sp_used[atomicAdd(&P.ctl->sp_n, 1u) & P.spmask] = h;  // (<= one claim per slot: never wraps)
+        return h;
+      }
+    }
+    if (k == key) {
+      atomicMax(&P.sp_val[h], rec);
+      return h;
+    }
+  }
+  atomicOr(&P.ctl->overflow, OV_SPILL);
+  return NONE_U32;
+}
+// the cell of a spill-table slot's key
+__device__ __forceinline__ uint32_t spill_cell(const KP& P, uint32_t h) {
+  return (uint32_t)((P.sp_key[h] - 1ull) % P.W);
+}
+
+// Suspicion deadlines are u16 cells: 0x8000 | (deadline mod 2^15), 0 = none. A
+// stored deadline is never more than the suspicion timeout (mult * bit_length(N) <= 5 * 21 periods)
+// ahead of the current period, nor behind it (the sweep fires or drops every due one), so the absolute
+// period is the one within +-2^14 of any period of the run it is decoded at.
+__host__ __device__ __forceinline__ uint16_t dl_enc(uint32_t dl) { return (uint16_t)(0x8000u | (dl & 0x7FFFu)); }
+__host__ __device__ __forceinline__ uint32_t dl_dec(uint32_t e, uint32_t t) {
+  int32_t diff = (int32_t)(((e & 0x7FFFu) - t) & 0x7FFFu);
+  if (diff >= 0x4000) diff -= 0x8000;
+  return t + (uint32_t)diff;
+}
+
+// A removed cell (present -> absent) drops the batched apply's merge mark of its subject's block:
+// records that did not override the present cell may override what the cell becomes next
+__device__ __forceinline__ void mark_clear(const KP& P, uint32_t obs, uint32_t subj) {
+  if (!P.dmark) return;
+  const uint32_t sid = P.sid_of[subj];
+  if (sid < P.dsids) P.dmark[lrow(P, obs) * P.dsids + sid] = 0u;
+}
+constexpr uint32_t GEN_MASK = 0xFFFFFFu;  // generation bits a merge mark keeps
+
 // MembershipProtocolImpl.updateMembership (MembershipProtocolImpl.java:481-547) and callees
 // (onSelfMemberDetected :549-569, onDeadMemberDetected :571-587, onAliveMemberDetected
 // :589-610, schedule/cancelSuspicionTimeoutTask :612-635, spreadMembershipGossipUnlessGossiped
@@ -797,10 +878,11 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.refut++;
     return r2;
   }
-  uint32_t* dlp = P.dl + (size_t)col * P.nloc + lrow(P, obs);  // subject-major: a due column streams
+  uint16_t* dlp = P.dl + (size_t)col * P.nloc + lrow(P, obs);  // subject-major: a due column streams
   if (r1 == SWIM_DEAD) {
     *dlp = 0u;
     *cellp = SWIM_ABSENT;
+    mark_clear(P, obs, subj);
     atomicSub(&P.cnt_delta[obs], 1);
     atomicSub(&P.pres[subj], 1u);
     atomicMax(&P.last_removed[subj], P.period + 1u);
@@ -814,7 +896,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
     T.accepted++;
     if (*dlp == 0u) {
       const uint32_t dl = P.period + susp_periods(P, others_snap);
-      *dlp = dl + 1u;
+      *dlp = dl_enc(dl);
       // every observer scheduling in a round computes the same deadline: read first, so the hot
       // column minimum takes one atomic per round instead of one per observer
       if (P.colmin[col] > dl) atomicMin(&P.colmin[col], dl);

@@ -37,7 +37,18 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// the spill-table slots the round's apply claimed become empty again (k_finalize then resets the count)
+__global__ void k_spill_clear(KP P) {
+  const uint32_t n = min(P.ctl->sp_n, P.spmask + 1u);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const uint32_t hs = P.sp_used[t];
+    P.sp_key[hs] = 0ull;
+    P.sp_val[hs] = 0u;
+  }
+}
+
 __global__ void k_finalize(KP P) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) P.ctl->sp_n = 0u;  // (k_spill_clear ran before, if at all)
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.row0 + P.nloc) {
@@ -124,13 +135,21 @@ __global__ void k_spread(KP P, uint32_t origin, uint32_t tag) {  // one wave; la
 // :407-414), accepted SYNC records spread (MPI:649-656). One wave; lane 0 does the work in order.
 // N x K: an untracked subject's BASELINE record is a no-op (equal records never override); the
 // host requested columns for every other record's subject beforehand (k_deliver_track).
+// SWIM_DELIVER_FORWARD: each record is a gossip new to obs (onGossipReq, GossipProtocolImpl.java:171-183):
+// its GossipState is put first (the observer forwards it from the coming round on), then membership.
 __global__ void k_deliver(KP P, uint32_t obs, const uint32_t* subj, const uint32_t* rec, uint32_t n, uint32_t reason) {
   Tally T;
   uint32_t created = 0;
+  const bool fwd = (reason & SWIM_DELIVER_FORWARD) != 0u;
+  reason &= ~SWIM_DELIVER_FORWARD;
   if (threadIdx.x == 0 && P.alive[obs] && is_local(P, obs)) {
     const uint32_t snap = P.cnt[obs];
     for (uint32_t k = 0; k < n; ++k) {
       const uint32_t j = subj[k], r1 = rec[k];
+      if (fwd) {
+        emit_gossip(P, obs, j, r1, P.gseq[obs]++);
+        ++created;
+      }
       if (P.nxk && P.colmap[j] == NONE && r1 == BASELINE) continue;
       const uint32_t r = apply_record(P, obs, j, r1, reason, SWIM_DELIVER_ATTEMPT | k, snap, T);
       if (r) {
@@ -144,10 +163,11 @@ __global__ void k_deliver(KP P, uint32_t obs, const uint32_t* subj, const uint32
 }
 
 __device__ __forceinline__ void track_request(const KP& P, uint32_t j);
-// N x K: columns for the delivered records' subjects that leave the baseline
-__global__ void k_deliver_track(KP P, const uint32_t* subj, const uint32_t* rec, uint32_t n) {
+// N x K: columns for the delivered records' subjects that leave the baseline (forwarded gossips: every
+// subject, since the members they reach merge the record through their tables)
+__global__ void k_deliver_track(KP P, const uint32_t* subj, const uint32_t* rec, uint32_t n, uint32_t all) {
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
-    if (rec[k] != BASELINE) track_request(P, subj[k]);
+    if (all || rec[k] != BASELINE) track_request(P, subj[k]);
 }
 
 // swim_update_metadata: MetadataStoreImpl.updateMetadata (a new version of the member's metadata)
@@ -193,6 +213,8 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
     if (P.meta_view) P.meta_view[lrow(P, x) * P.W + c] = 0u;
   }
   for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) P.ih_rhead[lrow(P, x) * 256u + t] = 0u;
+  if (P.dmark)  // a fresh table: no merge marks
+    for (uint32_t t = threadIdx.x; t < P.dsids; t += blockDim.x) P.dmark[lrow(P, x) * P.dsids + t] = 0u;
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;
     P.cnt_delta[x] = 0;
@@ -288,7 +310,7 @@ __device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t c0
   P.c_sr[x & P.cmask] = make_uint2(subject, record);
   P.c_hash[x & P.cmask] = hash;
   const uint32_t id = g0 + ci;
-  const uint32_t s = id & P.gmask;
+  const uint32_t s = gmod(P, id);
   uint32_t* cref = reinterpret_cast<uint32_t*>(P.g_cref);
   // the DEAD record of a member about itself is only ever its leave gossip (MPI:203-212)
   if (subject == origin && record == SWIM_DEAD && P.leaving[origin]) P.leave_slot[origin] = s;
@@ -296,13 +318,14 @@ __device__ __forceinline__ void commit_one(const KP& P, uint32_t g0, uint32_t c0
     cref[2u * s + 1u] = x + 1u;
     // the live records start at the oldest live slot's first one: they must fit the record ring
     const uint32_t glo = P.ctl->glo;
-    const uint32_t c_lo = (g0 != glo && g0 - glo <= P.GC) ? cref[2u * (glo & P.gmask)] : c0;
+    const uint32_t c_lo = (g0 != glo && g0 - glo <= P.GC) ? cref[2u * (gmod(P, glo))] : c0;
     if (x + 1u - c_lo > P.cmask + 1u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
   }
   if (!open) return;
   // the live id range must stay below GC - 64 slots so bitmap words never alias across the
   // ring wrap, and the slot's previous gossip must be dead everywhere (glo passed it)
   if (id - P.ctl->glo >= P.GC - 64u) atomicOr(&P.ctl->overflow, OV_GOSSIP);
+  if (!P.gpow2 && id >= 0xFFFFFFFFu - P.GC) atomicOr(&P.ctl->overflow, OV_GOSSIP);  // ids mod GC would jump
   cref[2u * s] = x;
   P.g_sr[s] = make_uint2(subject, record);
   P.g_hash[s] = hash;
@@ -637,7 +660,7 @@ __global__ void k_multi_live(KP P, uint32_t* out) {
   const uint32_t lo = P.ctl->glo, hi = P.ctl->gcount;
   const uint32_t n = hi - lo > P.GC ? P.GC : hi - lo;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint2 r = P.g_cref[(lo + i) & P.gmask];
+    const uint2 r = P.g_cref[gmod(P, lo + i)];
     if (r.y - r.x > 1u) atomicOr(out, 1u);
   }
 }
@@ -651,12 +674,12 @@ __global__ void k_commit_wsum(KP P, uint32_t all) {
   const uint32_t* cref = reinterpret_cast<const uint32_t*>(P.g_cref);
   for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += gridDim.x * blockDim.x) {
     uint32_t sum = 0;
-    const uint32_t ws = w & ((P.GC >> 5) - 1u);
+    const uint32_t ws = wmod(P, w);
     for (uint32_t b = 0; b < 32u; ++b) {
       const uint32_t id = (w << 5) + b;
       uint32_t c = 0;
       if ((int32_t)(g1 - id) > 0) {  // created (the word's slots from earlier commits count)
-        const uint32_t s = id & P.gmask;
+        const uint32_t s = gmod(P, id);
         c = cref[2u * s + 1u] - cref[2u * s];
       }
       sum += c;
@@ -682,15 +705,15 @@ __global__ void k_dict_claim(KP P) {
     if (subj >= P.N) continue;
     const uint32_t cur = P.sid_of[subj];
     // a block, a claim in progress, or a claim of this commit that found none
-    if (cur < DICT_SIDS || cur == DICT_LOCK || cur == tag) continue;
+    if (cur < P.dsids || cur == DICT_LOCK || cur == tag) continue;
     if (atomicCAS(&P.sid_of[subj], cur, DICT_LOCK) != cur) continue;  // NONE or an older commit's tag
     const uint32_t k = atomicAdd(&P.ctl->d_taken, 1u);
     uint32_t sid = NONE;
     if (k < nfree) {
       sid = P.d_free[nfree - 1u - k];
-    } else {  // (one claim per subject and commit: k_dict_entries clamps the mark back to DICT_SIDS)
+    } else {  // (one claim per subject and commit: k_dict_entries clamps the mark back to dsids)
       const uint32_t hw = atomicAdd(&P.ctl->d_hw, 1u);
-      if (hw < DICT_SIDS) sid = hw;
+      if (hw < P.dsids) sid = hw;
     }
     if (sid != NONE) P.d_subj[sid] = subj;
     P.sid_of[subj] = sid != NONE ? sid : tag;
@@ -705,7 +728,7 @@ __global__ void k_dict_entries(KP P) {
     const uint32_t t = P.ctl->d_taken, f = P.ctl->d_nfree;
     P.ctl->d_nfree = f - min(t, f);
     P.ctl->d_taken = 0u;
-    if (P.ctl->d_hw > DICT_SIDS) P.ctl->d_hw = DICT_SIDS;  // failed claims of the last commit
+    if (P.ctl->d_hw > P.dsids) P.ctl->d_hw = P.dsids;  // failed claims of the last commit
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t x = c0 + i;
@@ -715,7 +738,7 @@ __global__ void k_dict_entries(KP P) {
       id = ID_USER;
     } else {
       const uint32_t sid = P.sid_of[sr.x];
-      if (sid < DICT_SIDS) {
+      if (sid < P.dsids) {
         for (uint32_t k = 0; k < DICT_WAYS; ++k) {
           uint32_t* e = &P.d_rec[sid * DICT_WAYS + k];
           uint32_t v = *e;
@@ -728,28 +751,40 @@ __global__ void k_dict_entries(KP P) {
       }
     }
     P.c_id[x & P.cmask] = id;
-    if (id < DICT_IDS)
+    if (id < P.dsids * DICT_WAYS)
       atomicMax(&P.d_last[id], x + 1u);
-    else if (id == ID_NONE)
+    else if (id == ID_NONE) {
       atomicMax(&P.ctl->d_none_last, x + 1u);
+      atomicMax(const_cast<uint32_t*>(&P.none_last[sr.x]), x + 1u);
+    }
   }
 }
 
 // Entries no live record names are emptied; a block left empty goes back on the stack (its
 // subject gets a block again with its next record).
 __global__ void k_dict_free(KP P) {
-  const uint32_t hw = min(P.ctl->d_hw, DICT_SIDS), c_lo = live_rec_lo(P);
+  const uint32_t hw = min(P.ctl->d_hw, P.dsids), c_lo = live_rec_lo(P);
   for (uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x; sid < hw; sid += gridDim.x * blockDim.x) {
     const uint32_t subj = P.d_subj[sid];
     if (subj == NONE) continue;
-    bool live = false;
+    bool live = false, emptied = false;
     for (uint32_t k = 0; k < DICT_WAYS; ++k) {
       const uint32_t id = sid * DICT_WAYS + k;
       if (P.d_rec[id] == 0u) continue;
-      if ((int32_t)(P.d_last[id] - c_lo) > 0)
+      if ((int32_t)(P.d_last[id] - c_lo) > 0) {
         live = true;
-      else
+      } else {
         P.d_rec[id] = 0u;
+        emptied = true;
+      }
+    }
+    if (emptied && P.dmark) {  // an entry may take another record: the block's merge marks lapse
+      uint32_t g = P.d_gen[sid] + 1u;
+      if ((g & GEN_MASK) == 0u) {  // the marks' 24 generation bits wrap: no stale mark may match
+        ++g;
+        for (uint32_t r = 0; r < P.nloc; ++r) P.dmark[(size_t)r * P.dsids + sid] = 0u;
+      }
+      P.d_gen[sid] = g;
     }
     if (!live) {
       P.d_subj[sid] = NONE;
@@ -1235,7 +1270,7 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     const uint32_t hi0 = c->gcount, lo0 = c->glo;
     const uint32_t lo1 = hi0 - lo0 > P.GC ? hi0 - P.GC : lo0;
     for (uint32_t wi = (lo1 >> 5) + threadIdx.x; wi < ((hi0 + 31u) >> 5); wi += blockDim.x)
-      if (P.wlast[wi & ((P.GC >> 5) - 1u)] + P.sweepmax >= P.round) {
+      if (P.wlast[wmod(P, wi)] + P.sweepmax >= P.round) {
         atomicMin(&s_first, wi);
         break;  // later words of this thread are larger
       }
@@ -1301,9 +1336,9 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
       const uint32_t wi = wq + j;
       uint32_t wc = WC_NONE, sc = WC_NONE;
       if (wi >= w_lo && wi < w_end) {
-        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t ws = wmod(P, wi);
         const uint32_t id0 = (wi << 5) > lo ? (wi << 5) : lo;
-        const int32_t inf_lo = (int32_t)P.g_create[id0 & P.gmask];
+        const int32_t inf_lo = (int32_t)P.g_create[gmod(P, id0)];
         const int32_t inf_hi = (int32_t)P.wlast[ws];
         const int32_t amin = r - inf_hi, amax = r - inf_lo;  // holders' ages lie in [amin, amax]
         wc = amin > spread_hi ? WC_NONE : (amax <= spread_lo ? WC_ALL : WC_MIXED);
@@ -1320,14 +1355,14 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
         *reinterpret_cast<uint4*>(P.act + base + off) = make_uint4(e[0], e[1], e[2], e[3]);
 #pragma unroll
         for (uint32_t j = 0; j < 4u; ++j)  // word -> list position, for infectedFrom records
-          P.actpos[(wq + j) & (W32 - 1u)] = make_uint2(P.round, base + off + j);
+          P.actpos[wmod(P, wq + j)] = make_uint2(P.round, base + off + j);
       }
     } else {
       uint32_t o = base + off;
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j)
         if ((onm >> j) & 1u) {
-          P.actpos[(wq + j) & (W32 - 1u)] = make_uint2(P.round, o);
+          P.actpos[wmod(P, wq + j)] = make_uint2(P.round, o);
           P.act[o++] = e[j];
         }
     }
@@ -1453,7 +1488,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
         const uint32_t kq = k0 + 256u * j + 4u * lane;
         const uint32_t o0 = ev[4 * j] & ACT_OFF_MASK;
-        const uint32_t ws0 = (w_beg + o0) & (W32 - 1u);
+        const uint32_t ws0 = wmod(P, w_beg + o0);
         const bool quad = kq + 3u < n_act && (ws0 & 3u) == 0u && (ev[4 * j + 3] & ACT_OFF_MASK) == o0 + 3u;
         if (quad) {
           const uint4 h = *reinterpret_cast<const uint4*>(hbr + ws0);
@@ -1464,7 +1499,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         } else {
 #pragma unroll
           for (uint32_t i = 0; i < 4u; ++i)
-            wv[4 * j + i] = kq + i < n_act ? hbr[(w_beg + (ev[4 * j + i] & ACT_OFF_MASK)) & (W32 - 1u)] : 0u;
+            wv[4 * j + i] = kq + i < n_act ? hbr[wmod(P, w_beg + (ev[4 * j + i] & ACT_OFF_MASK))] : 0u;
         }
       }
       uint32_t mixm = 0;  // entries whose infection rounds must be read
@@ -1491,7 +1526,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         const uint32_t e = eq[i], word = hq[i];
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u, sc = (e >> 28) & 3u;
-        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t ws = wmod(P, wi);
         const uint32_t live = k < n_act ? range_mask(wi << 5, lo, hi) : 0u;
         const uint32_t held = word & live;
         uint32_t clear = 0, win = 0;
@@ -1531,7 +1566,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         }
       }
       auto hd_ld = [&](uint32_t e_, uint4& a_, uint4& b_) {
-        const uint32_t wi_ = w_beg + (e_ & ACT_OFF_MASK), ws_ = wi_ & (W32 - 1u);
+        const uint32_t wi_ = w_beg + (e_ & ACT_OFF_MASK), ws_ = wmod(P, wi_);
         // (hd4: escapes of the held live slots only; the holdings word is cache-resident)
         hd_load32<HD4>(P, lrow(P, m), ws_, a_, b_, HD4 ? hbr[ws_] & range_mask(wi_ << 5, lo, hi) : 0xFFFFFFFFu);
       };
@@ -1540,7 +1575,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
       auto finish_mixed = [&](uint32_t e, uint32_t word, uint32_t k, uint4 d0, uint4 d1) -> bool {
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u;
-        const uint32_t ws = wi & (W32 - 1u);
+        const uint32_t ws = wmod(P, wi);
         const uint32_t held = word & range_mask(wi << 5, lo, hi);
         // age = r - infectionPeriod, exact mod 2^8 (every held entry received before round r)
         ++hdw;
@@ -1802,7 +1837,7 @@ __device__ __forceinline__ uint32_t own_window(const KP& P, uint32_t m, uint32_t
   if (wc == WC_NONE) return 0u;
   const uint32_t W32 = P.GC >> 5;
   const uint32_t wi = w_beg + (ea & ACT_OFF_MASK);
-  if (wc == WC_ALL) return P.hb[lrow(P, m) * W32 + (wi & (W32 - 1u))] & range_mask(wi << 5, lo, hi);
+  if (wc == WC_ALL) return P.hb[lrow(P, m) * W32 + (wmod(P, wi))] & range_mask(wi << 5, lo, hi);
   return P.wb[lrow(P, m) * W32 + k];
 }
 
@@ -1831,7 +1866,6 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
-  const uint32_t W32 = P.GC >> 5;
   const uint32_t nch = (P.astride + PCHUNK - 1u) / PCHUNK;  // chunks of the longest record
   uint32_t removed_alive = 0;
   for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * MAXREC * nch; u += gridDim.x * 4u) {
@@ -1851,12 +1885,12 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       if (!bits) continue;
       const uint32_t wi = wbt + (act_t[q] & ACT_OFF_MASK);
       if (wi < w_beg) continue;  // every holder has swept the word
-      const uint2 ap = P.actpos[wi & (W32 - 1u)];  // listed this round, as this very word?
+      const uint2 ap = P.actpos[wmod(P, wi)];  // listed this round, as this very word?
       if (ap.x != P.round || ap.y >= n_act) continue;
       const uint32_t ea = P.act[ap.y];
       if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
-      const uint32_t supp = bits & state_since(P, sp.x, wi & (W32 - 1u), t, bits);
-      if (supp) removed += slot_gossips(P, wi & (W32 - 1u), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
+      const uint32_t supp = bits & state_since(P, sp.x, wmod(P, wi), t, bits);
+      if (supp) removed += slot_gossips(P, wmod(P, wi), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
       removed_alive += removed;
@@ -1877,7 +1911,6 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->sp_cnt < P.spcap ? P.ctl->sp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, r = P.round;
-  const uint32_t W32 = P.GC >> 5;
   uint32_t removed_alive = 0;
   for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
     if (!P.sp_dq[i]) continue;  // (uniform per wave)
@@ -1889,11 +1922,11 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
     for (uint32_t j = q0 + lane; j < q1; j += 64u) {
       const uint4 e = dq[j & (P.dqcap - 1u)];  // {peer that sent it, ring slot, arrival round, flags}
       if (e.x != sp.y || !(e.w & DQ_ARRIVED) || e.z >= r || e.z + P.hzn < r) continue;
-      const uint32_t ws = (e.y >> 5) & (W32 - 1u);
+      const uint32_t ws = wmod(P, e.y >> 5);
       const uint2 ap = P.actpos[ws];  // listed this round, as this very word?
       if (ap.x != r || ap.y >= n_act) continue;
       const uint32_t ea = P.act[ap.y];
-      if (((w_beg + (ea & ACT_OFF_MASK)) & (W32 - 1u)) != ws || ((ea >> 26) & 3u) == WC_NONE) continue;
+      if ((wmod(P, w_beg + (ea & ACT_OFF_MASK))) != ws || ((ea >> 26) & 3u) == WC_NONE) continue;
       const uint32_t supp = (1u << (e.y & 31u)) & state_since(P, sp.x, ws, e.z, 1u << (e.y & 31u));
       if (supp) removed += slot_gossips(P, ws, atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
@@ -1926,8 +1959,8 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
   else
     v = own_window(P, sreg, k, w_beg, lo, hi);
   if (v && (P.loss_mode == 1u || P.delay_on)) {  // this round's deliveries only: not lost, not delayed
-    const uint32_t W32 = P.GC >> 5, wi = w_beg + (ea & ACT_OFF_MASK);
-    const uint32_t* gh = P.g_hash + (wi & (W32 - 1u)) * 32u;
+    const uint32_t wi = w_beg + (ea & ACT_OFF_MASK);
+    const uint32_t* gh = P.g_hash + (wmod(P, wi)) * 32u;
     uint32_t need = v;
     v = 0u;
     while (need) {  // REC_ILP messages per step: their id-hash loads in flight together
@@ -2195,7 +2228,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
                           uint32_t& ws0) {
         const uint32_t ea[4] = {a.x, a.y, a.z, a.w};
         const uint32_t o0 = a.x & ACT_OFF_MASK;
-        ws0 = (w_beg + o0) & (W32 - 1u);
+        ws0 = wmod(P, w_beg + o0);
         quad = kq + 3u < n_act && (ws0 & 3u) == 0u && (a.w & ACT_OFF_MASK) == o0 + 3u;
         uint4 h4 = make_uint4(0u, 0u, 0u, 0u);
         if (quad) h4 = *reinterpret_cast<const uint4*>(hbr + ws0);
@@ -2208,7 +2241,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           const bool in = kq + i < n_act;
           wcv[i] = in ? (ea[i] >> 26) & 3u : WC_NONE;
           const uint32_t wi = w_beg + (ea[i] & ACT_OFF_MASK);
-          wsv[i] = wi & (W32 - 1u);
+          wsv[i] = wmod(P, wi);
           live[i] = range_mask(wi << 5, lo, hi);
           hw[i] = quad ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
           if (wcv[i] == WC_NONE) continue;
@@ -2351,7 +2384,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
         const uint4 e = dq[j & (P.dqcap - 1u)];
         if (e.z != P.round || (e.w & DQ_ARRIVED)) continue;
         dq[j & (P.dqcap - 1u)].w = e.w | DQ_ARRIVED;  // counts for infectedFrom from now on (k_gossip_select)
-        const uint32_t ws = (e.y >> 5) & (W32 - 1u), bit = 1u << (e.y & 31u);
+        const uint32_t ws = wmod(P, e.y >> 5), bit = 1u << (e.y & 31u);
         if (hbr[ws] & bit) continue;  // held (after this round's sweep): no new GossipState
         const uint2 ap = P.actpos[ws];
         if (ap.x != P.round || ap.y >= n_act) {  // the slot's word is kept listed until then (wlast)
@@ -2443,7 +2476,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_part(uint32_t v, uint32_t* t
 // rounds). Ring slots of one commit are sorted by (subject, record), so one representative per
 // run of one subject carries the run's lattice max; representatives are max-reduced per subject
 // in an LDS hash sized to the receipt count. A subject that finds no slot within HPROBE probes
-// goes to the global inbox instead (consistently for the whole round) and onto an LDS list.
+// goes to the spill table instead (consistently for the whole round) and onto an LDS list.
 // Then one updateMembership per subject.
 template <bool HD4>
 __device__ __forceinline__ void apply_body(const KP& P) {
@@ -2561,10 +2594,14 @@ __device__ __forceinline__ void apply_body(const KP& P) {
             h = (h + 1u) & hm;
           }
           if (!placed) {  // slots only ever fill up, so this subject spills for the whole round
-            if (atomicMax(&P.inbox[lrow(P, p) * P.W + col_of(P, sr[j].x)], sr[j].y) == 0u) {
+            const uint32_t c = col_of(P, sr[j].x);
+            bool first = false;
+            const uint32_t hs = c == NONE ? NONE : spill_put(P, p, c, sr[j].y, &first);
+            if (c == NONE) atomicOr(&P.ctl->overflow, OV_TRACK);
+            if (first) {
               const uint32_t o = atomicAdd(&s_nspill, 1u);
               if (o < spill_cap)
-                s_spl[o] = sr[j].x;
+                s_spl[o] = hs;
               else
                 atomicOr(&P.ctl->overflow, OV_SPILL);
             }
@@ -2618,7 +2655,7 @@ __device__ __forceinline__ void apply_body(const KP& P) {
         bv[j] = (kv[j] != NONE && ((ev[j] >> 26) & 3u) != WC_NONE) ? nbr[kv[j]] : 0u;
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
-        wsv[j] = (w_beg + (ev[j] & ACT_OFF_MASK)) & (W32 - 1u);
+        wsv[j] = wmod(P, w_beg + (ev[j] & ACT_OFF_MASK));
         if (bv[j]) {
           pv[j] = P.hb[lrow(P, p) * W32 + wsv[j]];
           rv[j] = P.runw[wsv[j]];
@@ -2663,9 +2700,9 @@ __device__ __forceinline__ void apply_body(const KP& P) {
     }
     const uint32_t nsp = s_nspill < spill_cap ? s_nspill : spill_cap;
     if (nsp) __threadfence();
-    for (uint32_t t = tid; t < nsp; t += nthr) {
-      const uint32_t subj = s_spl[t];
-      apply(subj, atomicExch(&P.inbox[lrow(P, p) * P.W + col_of(P, subj)], 0u));
+    for (uint32_t t = tid; t < nsp; t += nthr) {  // the spilled subjects' slots of the spill table
+      const uint32_t hs = s_spl[t];
+      apply(subj_of(P, spill_cell(P, hs)), atomicExch(&P.sp_val[hs], 0u));
     }
     if (tid == 0) atomicAdd(&P.held[p], total);
     nspills += tid == 0 ? nsp : 0u;
@@ -2723,9 +2760,9 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 // receiver gets ~10^4..10^5 records of ~10^3..10^4 subjects per round, mostly the same few records
 // per subject again: an LDS hash of (subject, max) per receiver spent its time probing and
 // spilling there (4.4 s per 100 C3 rounds); a bit per record costs one LDS OR.
-// Records without an entry (dictionary out of blocks or ways) take the global inbox (lattice max
-// per cell; spilled subjects listed in LDS, the whole inbox row scanned when the list overflows).
-// While any such record is live, the bitmap's maxima go through the inbox as well, so a subject
+// Records without an entry (dictionary out of blocks or ways) take the spill table (lattice max
+// per cell; the claimed slots listed in LDS, the round's claimed slots scanned when the list overflows).
+// While a subject has such a record live, its bitmap maxima go through the spill table as well, so a subject
 // is merged exactly once per round.
 #ifndef SWIM_APPLY_WSPILL
 #define SWIM_APPLY_WSPILL 128
@@ -2746,7 +2783,8 @@ constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flig
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
 constexpr uint32_t AW_LONG = SWIM_AW_LONG;
-constexpr uint32_t AW_WORDS = DICT_WORDS + AW_SPILL + 4u;  // LDS words per wave
+// LDS words per wave: the entry bitmap (dsids / 4 words: DICT_WAYS bits per block), the spill list, misc
+__host__ __device__ __forceinline__ uint32_t aw_words(uint32_t dsids) { return dsids / 4u + AW_SPILL + 4u; }
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
 #ifndef SWIM_AW_MINW
@@ -2756,16 +2794,20 @@ template <bool HD4>
 __device__ __forceinline__ void apply_b_body(const KP& P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  uint32_t* s_bm = s_dyn + wv * AW_WORDS;  // entry bitmap: all-zero between receivers
-  uint32_t* s_spl = s_bm + DICT_WORDS;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  uint32_t* s_bm = s_dyn + wv * aw_words(P.dsids);  // entry bitmap: all-zero between receivers
+  uint32_t* s_spl = s_bm + P.dsids / 4u;
   uint32_t* s_misc = s_spl + AW_SPILL;  // [0] spilled subjects
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
   const uint32_t W32 = P.GC >> 5;
-  const uint32_t bw = (min(P.ctl->d_hw, DICT_SIDS) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
-  const bool via_inbox = (int32_t)(P.ctl->d_none_last - live_rec_lo(P)) > 0;  // a live record has no entry
+  const uint32_t bw = (min(P.ctl->d_hw, P.dsids) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
+  const uint32_t dids = P.dsids * DICT_WAYS;
+  // a live record has no dictionary entry: the subjects of such records merge through the spill table
+  // (their entry records too), so every subject is merged exactly once per round
+  const uint32_t c_lo = live_rec_lo(P);
+  const bool any_none = (int32_t)(P.ctl->d_none_last - c_lo) > 0;
   Tally T;
-  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrecs = 0, nrcpt = 0;
+  uint32_t created = 0, nwords = 0, nruns = 0, nsubj = 0, nspills = 0, nrecs = 0, nrcpt = 0, nskip = 0;
   auto wsync = [] {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -2794,36 +2836,37 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #define APPLYB_SUB(acc)
 #endif
   APPLYB_MARK(0);
-  for (uint32_t li = blockIdx.x * AW_WAVES + wv; li < n_list; li += gridDim.x * AW_WAVES) {
+  for (uint32_t li = blockIdx.x * nwv + wv; li < n_list; li += gridDim.x * nwv) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t nsw = (n_act + 31u) >> 5;
     const bool summ = nsw <= P.nsumw;
     const uint32_t* sumr = P.nsum + lrow(P, p) * P.nsumw;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
-    uint32_t* inrow = P.inbox + lrow(P, p) * P.W;
     if (lane == 0) s_misc[0] = 0u;
     wsync();
-    bool rowscan = false;  // the spill list overflowed: scan the whole inbox row at the end
+    bool rowscan = false;  // the spill list overflowed: the round's claimed slots are scanned at the end
     uint32_t ent = 0, rc = 0;
-    // lattice max into the receiver's inbox cell; the subject's first writer lists it
+    // lattice max into the receiver's spill-table cell; the key's claimer lists its slot
     auto spill = [&](uint32_t subj, uint32_t rec) {
       const uint32_t c = col_of(P, subj);
       if (c == NONE) {  // N x K: no column for a subject with a live gossip
         atomicOr(&P.ctl->overflow, OV_TRACK);
         return;
       }
-      if (atomicMax(&inrow[c], rec) == 0u) {
+      bool first = false;
+      const uint32_t hs = spill_put(P, p, c, rec, &first);
+      if (first) {
         const uint32_t o = atomicAdd(&s_misc[0], 1u);
         if (o < AW_SPILL)
-          s_spl[o] = subj;
+          s_spl[o] = hs;
         else
           rowscan = true;
       }
     };
     // record-ring record x of a received run top
     auto record = [&](uint32_t x, uint32_t id) {
-      if (id < DICT_IDS) {
+      if (id < dids) {
         atomicOr(&s_bm[id >> 5], 1u << (id & 31u));
         return;
       }
@@ -2842,7 +2885,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       const uint32_t e = kv != NONE ? P.act[kv] : 0u;
       const uint32_t b0 = kv != NONE ? nbr[kv] : 0u;  // issued beside the list entry, not after it
       const uint32_t bits = ((e >> 26) & 3u) != WC_NONE ? b0 : 0u;
-      const uint32_t ws = (w_beg + (e & ACT_OFF_MASK)) & (W32 - 1u);
+      const uint32_t ws = wmod(P, w_beg + (e & ACT_OFF_MASK));
       uint32_t rm = 0u;
       if (bits) {
         const uint32_t prior = P.hb[lrow(P, p) * W32 + ws];
@@ -2903,7 +2946,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
             for (uint32_t u = 0; u < AW_VILP; ++u) {
               const uint32_t d = x0 + 256u * u + 4u * lane;
               v[u] = d < span ? *reinterpret_cast<const uint4*>(P.c_id + ((a0 + d) & P.cmask))
-                              : make_uint4(DICT_IDS, DICT_IDS, DICT_IDS, DICT_IDS);
+                              : make_uint4(dids, dids, dids, dids);
             }
 #pragma unroll
             for (uint32_t u = 0; u < AW_VILP; ++u) {
@@ -2936,7 +2979,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
               bl[u] = ee < qtot ? lo : 0u;
               qb[u] = (bx[u] & ~3u) + 4u * (ee - oo);
               v[u] = ee < qtot ? *reinterpret_cast<const uint4*>(P.c_id + (qb[u] & P.cmask))
-                               : make_uint4(DICT_IDS, DICT_IDS, DICT_IDS, DICT_IDS);
+                               : make_uint4(dids, dids, dids, dids);
             }
 #pragma unroll
             for (uint32_t u = 0; u < AW_QILP; ++u) {
@@ -2975,6 +3018,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     wsync();
     APPLYB_MARK(1);
     const uint32_t snap = P.cnt[p];
+    uint32_t* mrow = P.dmark + lrow(P, p) * P.dsids;  // the receiver's merge marks
     auto apply = [&](uint32_t subj, uint32_t r1) {
       ++nsubj;
       const uint32_t rec = apply_record(P, p, subj, r1, SWIM_R_MEMBERSHIP_GOSSIP, 0u, snap, T);
@@ -3007,22 +3051,37 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           const uint32_t b = kth_set_bit(bo, q - oo);
           const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
           const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
+          const uint32_t sid = base / DICT_WAYS;
+          const uint32_t m = (s_bm[t] >> (8u * j)) & 0xFFu;
+          // the merge mark (every load of the block in flight at once): when every set entry is
+          // marked, none overrides the cell (MPI:489) and the cell is not read
+          uint32_t* mkp = mrow + sid;
+          const uint32_t mk = *mkp, g = P.d_gen[sid] & GEN_MASK;
           const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
           const uint4 r0 = dr[0], r1 = dr[1];
-          const uint32_t subj = P.d_subj[base / DICT_WAYS];
-          const uint32_t m = (s_bm[t] >> (8u * j)) & 0xFFu;
-          uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
-                              max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
-          best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
-                               max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
-          if (via_inbox) {
-            spill(subj, best);
+          const uint32_t subj = P.d_subj[sid];
+          const bool mvalid = (mk >> 8) == g;
+          if (mvalid && (m & ~mk & 0xFFu) == 0u) {
+            ++nskip;
           } else {
-            const uint32_t c = cell_get(P, p, subj);
-            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE))  // (the latter: OV_TRACK)
-              apply(subj, best);
-            else
-              ++nsubj;
+            uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
+                                max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
+            best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
+                                 max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
+            if (any_none && (int32_t)(P.none_last[subj] - c_lo) > 0) {
+              spill(subj, best);
+            } else {
+              const uint32_t c = cell_get(P, p, subj);
+              if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE)) {  // (the latter: OV_TRACK)
+                apply(subj, best);
+              } else {
+                ++nsubj;
+                // no set entry overrides the present cell: mark them (an absent cell is not
+                // marked: a record that does not override it may override a re-added one)
+                const uint32_t nm = (g << 8) | (((mvalid ? mk : 0u) | m) & 0xFFu);
+                if (c != SWIM_ABSENT && nm != mk) *mkp = nm;
+              }
+            }
           }
         }
       }
@@ -3034,16 +3093,22 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     wsync();
     APPLYB_MARK(2);
     const uint32_t nsp = min(s_misc[0], AW_SPILL);
-    if (__any(rowscan)) {  // every spilled subject: the inbox row's nonzero cells
+    if (__any(rowscan)) {  // every spilled subject: this row's keys among the round's claimed slots
       __threadfence();
-      const uint32_t nc = ncells(P);
-      for (uint32_t c = lane; c < nc; c += 64u)
-        if (inrow[c]) apply(subj_of(P, c), atomicExch(&inrow[c], 0u));
+      const uint32_t nu = min(atomicAdd(&P.ctl->sp_n, 0u), P.spmask + 1u);
+      const unsigned long long k0 = lrow(P, p) * (unsigned long long)P.W + 1ull, k1 = k0 + P.W;
+      for (uint32_t t = lane; t < nu; t += 64u) {
+        const uint32_t hs = P.sp_used[t];  // (another wave's entry may still be stale: keys filter it)
+        const unsigned long long k = P.sp_key[hs];
+        if (k < k0 || k >= k1) continue;
+        const uint32_t v = atomicExch(&P.sp_val[hs], 0u);
+        if (v) apply(subj_of(P, (uint32_t)(k - k0)), v);
+      }
     } else {
       if (nsp) __threadfence();
       for (uint32_t t = lane; t < nsp; t += 64u) {
-        const uint32_t subj = s_spl[t];
-        apply(subj, atomicExch(&inrow[col_of(P, subj)], 0u));
+        const uint32_t hs = s_spl[t];
+        apply(subj_of(P, spill_cell(P, hs)), atomicExch(&P.sp_val[hs], 0u));
       }
     }
     if (lane == 0) atomicAdd(&P.held[p], total);
@@ -3058,6 +3123,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
   add_stat(P, ST_APPLY_SPILL, nspills);
   add_stat(P, ST_APPLY_RECS, nrecs);
   add_stat(P, ST_GOSSIP_RECEIPTS, nrcpt);
+  add_stat(P, ST_APPLY_SKIP, nskip);
 #ifdef SWIM_APPLY_PROF
   if (lane == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(P.dbg_log) + 17, t_w);
@@ -3171,7 +3237,7 @@ __global__ void __launch_bounds__(256) k_gossip_need(KP P, uint32_t n_pairs, uin
           if (((e >> 26) & 3u) == WC_NONE) continue;
           const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
           const uint32_t live = range_mask(wi << 5, lo, hi);
-          if (all || (hbr[wi & (W32 - 1u)] & live) != live) bits |= 1u << b;
+          if (all || (hbr[wmod(P, wi)] & live) != live) bits |= 1u << b;
         }
       if (t < nneed) {
         P.rneed[(size_t)i * nneed + t] = bits;
@@ -3234,7 +3300,7 @@ __global__ void __launch_bounds__(256) k_gossip_pack_sparse(KP P, uint32_t n_pai
         const uint32_t k = 32u * (4u * threadIdx.x + j) + b;
         const uint32_t e = P.act[k];
         const uint32_t wc = (e >> 26) & 3u, wi = w_beg + (e & ACT_OFF_MASK);
-        out[o++] = pwr ? pwr[k] : (wc == WC_ALL ? hbr[wi & (W32 - 1u)] & range_mask(wi << 5, lo, hi) : wbr[k]);
+        out[o++] = pwr ? pwr[k] : (wc == WC_ALL ? hbr[wmod(P, wi)] & range_mask(wi << 5, lo, hi) : wbr[k]);
       }
     }
   }
@@ -3423,13 +3489,13 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
         for (uint32_t q = 0; q < 4u; ++q) {
           if (!v[q]) continue;
           const uint32_t k = k0 + q, j = s_col[k];
-          uint32_t* dp = P.dl + (size_t)j * P.nloc + li;
+          uint16_t* dp = P.dl + (size_t)j * P.nloc + li;
           if (!alive) {  // a stopped member's timers never fire: dropped
             *dp = 0u;
             continue;
           }
-          const uint32_t dl = v[q] - 1u;
-          if (dl > P.period) {  // still standing: the column's minimum (reduced per wave below)
+          const uint32_t dl = dl_dec(v[q], P.period);
+          if ((int32_t)(dl - P.period) > 0) {  // still standing: the column's minimum (reduced per wave below)
             smin[q] = dl;
             continue;
           }
@@ -3475,6 +3541,7 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
     // pass 2: the fired cells, row by row, lane q on due column q
     const uint32_t jq = lane < nc ? s_col[lane] : 0u;
     const uint32_t sq = lane < nc ? subj_of(P, jq) : 0u;
+    const uint32_t bq = (lane < nc && P.dmark) ? P.sid_of[sq] : NONE;  // merge marks (mark_clear)
     for (uint32_t t = wv; t < 256u; t += 4u) {
       const unsigned long long fm = s_fire[t];  // (the same word for every lane: a broadcast)
       if (!fm) continue;  // (uniform)
@@ -3482,8 +3549,12 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
       const bool f = (fm >> lane) & 1ull;
       uint32_t* cellp = P.view + (size_t)lr * P.W + jq;
       uint32_t r0 = 0u;
-      if (f && P.ecap) r0 = *cellp;  // the removed record, for the REMOVED event
+      if (f && P.ecap) {
+        r0 = *cellp;  // the removed record, for the REMOVED event
+        if (r0 == SWIM_ABSENT) atomicOr(&P.ctl->overflow, OV_BUG);  // a deadline without a record
+      }
       if (f) *cellp = SWIM_ABSENT;
+      if (f && bq < P.dsids) P.dmark[(size_t)lr * P.dsids + bq] = 0u;
       if (P.ecap) {
         const uint32_t at = s_ebase + s_eoff[t] + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
         if (f) {
@@ -3970,8 +4041,9 @@ __global__ void k_digest(KP P, unsigned long long* out) {
   }
   const size_t dtot = (size_t)nc * nloc;
   for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < dtot; x += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t d = P.dl[x];  // x = cell * nloc + local observer
-    if (d) {
+    const uint32_t e = P.dl[x];  // x = cell * nloc + local observer
+    if (e) {
+      const uint32_t d = dl_dec(e, P.period) + 1u;  // the oracle's deadline + 1
       const uint64_t subj = subj_of(P, (uint32_t)(x / nloc)), obs = row0 + x % nloc;
       b += fmix64((obs * N + subj) * K + d);
     }

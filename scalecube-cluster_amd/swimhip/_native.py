@@ -28,6 +28,7 @@ EV_ADDED, EV_REMOVED, EV_UPDATED = 1, 2, 3
 EV_GOSSIP, EV_FD = 8, 9  # GossipProtocol.listen() / FailureDetector.listen() streams (include/swimhip.h)
 TRACE_FD = 1
 R_FAILURE_DETECTOR_EVENT, R_MEMBERSHIP_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_SUSPICION_TIMEOUT = 0, 1, 2, 3, 4
+DELIVER_FORWARD = 0x100  # swim_deliver_records reason flag: the records are gossips new to the observer
 
 
 def pack(inc: int, code: int) -> int:
@@ -61,6 +62,7 @@ class SwimConfig(ctypes.Structure):
         ("gossip_batching", ctypes.c_uint32),
         ("record_capacity", ctypes.c_uint32),
         ("infection_round_bits", ctypes.c_uint32),
+        ("dict_subjects", ctypes.c_uint32),
     ]
 
 
@@ -121,6 +123,7 @@ STAT_FIELDS = [
     "commit_radix",
     "escape_entries",
     "escape_capacity",
+    "apply_skipped",
 ]
 
 

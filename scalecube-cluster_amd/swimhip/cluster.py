@@ -82,7 +82,7 @@ class SwimCluster:
     def __init__(self, config: ClusterConfig, n_members: int, seed: int = 0, *, event_capacity: int = 0,
                  gossip_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
                  n_initial: int = 0, gossip_batching: bool = True, record_capacity: int = 0,
-                 infection_round_bits: int = 0, _lib=None,
+                 infection_round_bits: int = 0, dict_subjects: int = 0, _lib=None,
                  _prefix: str = "swim_", _shard=(0, 1)):
         self._lib = _lib if _lib is not None else nat.load_swimhip()
         self._p = _prefix
@@ -93,12 +93,14 @@ class SwimCluster:
                                    event_capacity=event_capacity, sync_capacity=sync_capacity,
                                    tracked_subjects=tracked_subjects, device=device, shard_rank=_shard[0],
                                    shard_world=_shard[1], n_initial=n_initial, gossip_batching=gossip_batching,
-                                   record_capacity=record_capacity, infection_round_bits=infection_round_bits)
+                                   record_capacity=record_capacity, infection_round_bits=infection_round_bits,
+                                   dict_subjects=dict_subjects)
         h = ctypes.c_void_p()
         self._h = None
         self._call("create", ctypes.byref(self._cfg), ctypes.byref(h))
         self._h = h
         self._alive = np.arange(self.n) < (n_initial or self.n)
+        self.period = 0  # periods stepped (host count; swim_stats.period on the device)
 
     # -- plumbing -------------------------------------------------------------------------
     def _fn(self, name):
@@ -228,6 +230,7 @@ class SwimCluster:
     # -- stepping -------------------------------------------------------------------------
     def step(self, periods: int = 1):
         self._call("step", self._h, int(periods))
+        self.period += int(periods)
 
     # -- observation ----------------------------------------------------------------------
     def view(self, observer: int) -> np.ndarray:
@@ -328,6 +331,7 @@ class SwimCluster:
 
     def step_async(self, periods: int = 1):
         self._call("step_async", self._h, int(periods))
+        self.period += int(periods)
 
     def sync(self):
         self._call("sync", self._h)

@@ -234,7 +234,7 @@ class ClusterConfig(_Cfg):
 def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_capacity: int = 0,
                    event_capacity: int = 0, sync_capacity: int = 0, tracked_subjects: int = 0, device: int = 0,
                    shard_rank: int = 0, shard_world: int = 1, n_initial: int = 0, gossip_batching: bool = True,
-                   record_capacity: int = 0, infection_round_bits: int = 0):
+                   record_capacity: int = 0, infection_round_bits: int = 0, dict_subjects: int = 0):
     """Marshal a ClusterConfig into the C struct of include/swimhip.h. n_initial < n_members leaves
     ids [n_initial, n_members) as spare slots for joins and restarts."""
     from ._native import SwimConfig
@@ -269,4 +269,5 @@ def to_swim_config(cfg: ClusterConfig, n_members: int, seed: int = 0, *, gossip_
     c.gossip_batching = 0 if gossip_batching else 1
     c.record_capacity = record_capacity
     c.infection_round_bits = infection_round_bits
+    c.dict_subjects = dict_subjects
     return c

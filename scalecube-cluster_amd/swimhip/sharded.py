@@ -142,9 +142,37 @@ class ShardedSwimCluster(SwimCluster):
                 if self._x.op == nat.X_DONE:
                     break
                 self._exchange(status)
+            self.period += 1
 
     def step_async(self, periods: int = 1):
         self.step(periods)
+
+    # -- collective fault injection: every rank must pass the same arguments ----------------
+    def _same_args(self, name, ids):
+        """All-gather a digest of the call's arguments and fail on every rank when they differ. A
+        leave changes the layout of every later commit exchange block (a {gossips, stopped} header,
+        include/swimhip.h); ranks that disagree would read each other's blocks wrongly."""
+        ids = np.asarray(list(ids), dtype=np.uint64)
+        dig = int((ids * np.uint64(0x9E3779B97F4A7C15) + np.arange(len(ids), dtype=np.uint64)).sum()
+                  & np.uint64(0x7FFFFFFFFFFFFFFF)) if len(ids) else 0
+        rows = self._all_gather_ints([len(ids), dig])
+        if any(r != rows[0] for r in rows):
+            raise SwimError(-22, f"{name}: ranks passed different arguments {rows}")
+
+    def leave(self, ids):
+        ids = list(ids)
+        self._same_args("leave", ids)
+        super().leave(ids)
+
+    def crash(self, ids):
+        ids = list(ids)
+        self._same_args("crash", ids)
+        super().crash(ids)
+
+    def update_metadata(self, ids):
+        ids = list(ids)
+        self._same_args("update_metadata", ids)
+        super().update_metadata(ids)
 
     def sync(self):
         self._call("sync", self._h)

@@ -396,23 +396,60 @@ def decoded_records(records: List[MembershipRecord], directory: Directory):
     return subj, rec
 
 
+def _seen_ids(cluster, observer: int) -> dict:
+    """The gossip ids a simulated member holds from real nodes: GossipProtocolImpl.gossips keyed by
+    gossipId (:171-183), each until the period its sweep drops it (sweepGossips, :281-304)."""
+    seen = cluster.__dict__.setdefault("_wire_seen", {})
+    return seen.setdefault(int(observer), {})
+
+
+def _sweep_periods(cluster) -> int:
+    """Periods a received gossip stays in `gossips`: gossipPeriodsToSweep gossip rounds
+    (ClusterMath.java:99-102) at the cluster's size, rounded up to whole periods, + 1."""
+    from .cluster_math import gossipPeriodsToSweep
+
+    g = cluster.config.gossipConfig()
+    rounds_per_period = max(1, cluster.config.failureDetectorConfig().pingInterval() // g.gossipInterval())
+    sweep = gossipPeriodsToSweep(g.gossipRepeatMult(), cluster.n)
+    return -(-sweep // rounds_per_period) + 1
+
+
 def deliver(cluster, observer: int, msg: Message, directory: Directory, sync_group: str = "default") -> int:
     """Hand a real node's message to simulated member `observer` (before the next period). Returns
-    the number of records delivered. SYNC / SYNC_ACK: syncMembership with reason SYNC (accepted
-    records re-spread), a foreign sync group ignored (checkSyncGroup, MembershipProtocolImpl.java:442-448);
-    GossipRequest: each membership gossip's record with reason MEMBERSHIP_GOSSIP (onMembershipGossip,
-    :407-414). Other messages (pings, metadata, application gossips) carry no membership records."""
+    the number of records delivered.
+
+    SYNC: syncMembership with reason SYNC (accepted records re-spread), a foreign sync group ignored
+    (checkSyncGroup, MembershipProtocolImpl.java:442-448). SYNC_ACK: only one without a correlation id
+    (a reply to a periodic SYNC, onSyncAck, :343-349); onMessage drops a SYNC_ACK that carries one
+    (:331-334): it answers an initial sync the simulated member never sent to a real node.
+    GossipRequest: each membership gossip whose id the observer does not hold yet (onGossipReq,
+    GossipProtocolImpl.java:171-183; a repeat from another real peer is dropped): its GossipState is put,
+    so the observer forwards it to simulated peers in the coming rounds (SWIM_DELIVER_FORWARD), and
+    its record goes to onMembershipGossip with reason MEMBERSHIP_GOSSIP (:407-414). An id is held until
+    the observer's sweep drops it (gossipPeriodsToSweep), then a copy counts as new again. Other
+    messages (pings, metadata, application gossips) carry no membership records."""
     q, data = msg.qualifier, msg.data
     if q in (SYNC, SYNC_ACK) and isinstance(data, SyncData):
         if data.syncGroup != sync_group:
             return 0
+        if q == SYNC_ACK and msg.correlationId is not None:
+            return 0
         subj, rec = decoded_records(data.membership, directory)
         reason = nat.R_SYNC
     elif q == GOSSIP_REQ and isinstance(data, GossipRequest):
-        recs = [g.message.data for g in data.gossips
-                if g.message.qualifier == MEMBERSHIP_GOSSIP and isinstance(g.message.data, MembershipRecord)]
+        seen = _seen_ids(cluster, observer)
+        now = cluster.period
+        for gid in [g for g, until in seen.items() if until <= now]:
+            del seen[gid]
+        recs = []
+        for g in data.gossips:
+            if g.gossipId in seen:
+                continue
+            seen[g.gossipId] = now + _sweep_periods(cluster)
+            if g.message.qualifier == MEMBERSHIP_GOSSIP and isinstance(g.message.data, MembershipRecord):
+                recs.append(g.message.data)
         subj, rec = decoded_records(recs, directory)
-        reason = nat.R_MEMBERSHIP_GOSSIP
+        reason = nat.R_MEMBERSHIP_GOSSIP | nat.DELIVER_FORWARD
     else:
         return 0
     if subj:

@@ -36,7 +36,7 @@ def test_oracle_mirrors_stateful_api():
 def test_struct_sizes_match_c_layout():
     assert ctypes.sizeof(nat.SwimEvent) == 24
     assert ctypes.sizeof(nat.SwimStats) == 8 * len(nat.STAT_FIELDS)
-    assert ctypes.sizeof(nat.SwimConfig) == 104
+    assert ctypes.sizeof(nat.SwimConfig) == 112
     assert ctypes.sizeof(nat.SwimXchg) == 16 + 2 * 8 * nat.MAX_WORLD + 8
 
 

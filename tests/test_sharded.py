@@ -95,7 +95,7 @@ def test_exchange_protocol_rccl_one_rank():
     mp.spawn(_exchange_worker, args=(1, _free_port(), "nccl"), nprocs=1, join=True)
 
 
-def _parity_worker(rank, world, port, names):
+def _parity_worker(rank, world, port, names, shard_kw=None):
     import scenarios
     from swimhip import SwimCluster
 
@@ -103,7 +103,7 @@ def _parity_worker(rank, world, port, names):
     torch.cuda.set_device(0)
     try:
         for name in names:
-            scenarios.run_pair(name, lambda *a, **k: ShardedSwimCluster(*a, **k), SwimCluster)
+            scenarios.run_pair(name, lambda *a, **k: ShardedSwimCluster(*a, **k, **(shard_kw or {})), SwimCluster)
     finally:
         dist.destroy_process_group()
 
@@ -130,6 +130,19 @@ def test_shard_lifecycle_and_delays_match_unsharded(world, names):
     receiver shard asks for every window word, since every message draws its delay), metadata
     updates and user gossips. Bit-exact with the unsharded handle, period by period."""
     mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,names", [(2, ["test48_delay30_partition", "test64_long_partition_rejoin"]),
+                                         (4, ["local128_partition_heal"])])
+def test_hd4_shards_match_unsharded_hd8(world, names):
+    """4-bit infection rounds on sharded handles, which C4's and C5's node shards pick
+    by default: the escape table of rounds 15 or more after a slot's creation (members reached late
+    across a partition cut, or by a delayed message), k_hx_sweep, and the slots' creation rounds (gc8)
+    written by commits every shard makes from the exchanged batch. Sharded hd4 against the unsharded
+    8-bit handle, bit-exact every period."""
+    mp.spawn(_parity_worker, args=(world, _free_port(), names, {"infection_round_bits": 4}), nprocs=world,
+             join=True)
 
 
 def _nxk_worker(rank, world, port, names, k):

@@ -146,6 +146,48 @@ def test_sync_from_a_real_node_into_the_oracle():
     assert sum(1 for i in range(n) if c.view(i)[5] == nat.pack(1, nat.ALIVE)) == n
 
 
+def test_gossip_request_is_forwarded_once_per_id():
+    """GossipProtocolImpl.onGossipReq (:171-183) on the bridge: a real node's membership gossip with
+    a new id is put into the simulated member's gossips (forwarded to simulated peers in the coming
+    rounds, a gossip the observer created) and handed to membership once; the same id from a second
+    real peer is dropped; once the observer's sweep drops the id (gossipPeriodsToSweep) a copy counts
+    as new again."""
+    cfg = ClusterConfig.defaultLocalConfig()
+    n = 16
+    d = wire.Directory(n)
+    c = OracleCluster(cfg, n, seed=5, event_capacity=1 << 12)
+    c.step(2)
+    gossip = wire.membership_gossip_request(d, 9, 0, wire.MembershipRecord(d[7], "SUSPECT", 0))
+    before = c.stats()["gossips_created"]
+    assert wire.deliver(c, 3, gossip, d) == 1
+    assert c.stats()["gossips_created"] == before + 1  # the forwarded copy
+    assert c.view(3)[7] == nat.pack(0, nat.SUSPECT)
+    assert wire.deliver(c, 3, gossip, d) == 0  # a repeat of a held id
+    assert c.stats()["gossips_created"] == before + 1
+    c.step(1)  # the forward reaches the other simulated members (10 rounds per local period)
+    assert sum(1 for i in range(n) if c.view(i)[7] in (nat.pack(0, nat.SUSPECT), nat.pack(1, nat.ALIVE))) == n
+    c.step(wire._sweep_periods(c))
+    assert wire.deliver(c, 3, gossip, d) == 1  # swept: new again
+
+
+def test_sync_ack_with_correlation_id_is_dropped():
+    """MembershipProtocolImpl.onMessage (:331-334) ignores a SYNC_ACK carrying a correlation id (only
+    start0's initial sync consumes one); a SYNC_ACK without one is onSyncAck (:343-349)."""
+    cfg = ClusterConfig.defaultLocalConfig()
+    n = 8
+    d = wire.Directory(n)
+    c = OracleCluster(cfg, n, seed=6, event_capacity=1 << 12)
+    c.step(1)
+    recs = [wire.MembershipRecord(d[j], "SUSPECT" if j == 4 else "ALIVE", 0) for j in range(n)]
+    with_cid = wire.Message({wire.HEADER_QUALIFIER: wire.SYNC_ACK, wire.HEADER_CORRELATION_ID: "3"},
+                            wire.SyncData(recs))
+    assert wire.deliver(c, 1, with_cid, d) == 0
+    assert c.view(1)[4] == nat.pack(0, nat.ALIVE)
+    plain = wire.Message({wire.HEADER_QUALIFIER: wire.SYNC_ACK}, wire.SyncData(recs))
+    assert wire.deliver(c, 1, plain, d) == n
+    assert c.view(1)[4] == nat.pack(0, nat.SUSPECT)
+
+
 def test_membership_gossip_request_round_trip():
     d = wire.Directory(8)
     rec = wire.MembershipRecord(d[3], "SUSPECT", 2)
@@ -161,7 +203,8 @@ def test_membership_gossip_request_round_trip():
 def test_delivered_records_match_oracle(tracked):
     """swim_deliver_records on the GPU equals the oracle's: a real node's SYNC (SUSPECTs, a self
     SUSPECT that forces refutation, an ALIVE of higher incarnation, a DEAD) and a membership-gossip
-    GossipRequest delivered between periods, under 10 % loss (metadata fetches draw), then 12 periods
+    GossipRequest delivered between periods (forwarded by the receiving member, its repeat dropped),
+    under 10 % loss (metadata fetches draw), then 12 periods
     stepped: tables, deadlines, events and counters bit-exact (dense, and N x K with 48 columns: 10 % loss over 14
     periods takes ~20 of the 64 subjects off the baseline)."""
     cfg = ClusterConfig.defaultLocalConfig()
@@ -179,7 +222,8 @@ def test_delivered_records_match_oracle(tracked):
         c.step(2)
         assert wire.deliver(c, 12, sync, d) == n      # ALIVE inc 2 about 12 itself: refuted with inc 3
         assert wire.deliver(c, 3, sync, d) == n       # 3 refutes its SUSPECT
-        assert wire.deliver(c, 30, gossip, d) == 1    # MEMBERSHIP_GOSSIP: applied, not re-spread
+        assert wire.deliver(c, 30, gossip, d) == 1    # MEMBERSHIP_GOSSIP: applied and forwarded
+        assert wire.deliver(c, 30, gossip, d) == 0    # the same id again: dropped
     for _ in range(4):
         for c in (a, b):
             c.step(3)

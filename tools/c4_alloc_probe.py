@@ -22,6 +22,8 @@ w = bench.WORKLOADS[wl]
 kw = {"tracked_subjects": w["tracked"]} if w.get("tracked") else {}
 if w.get("rcap"):
     kw["record_capacity"] = w["rcap"]
+if w.get("dsub"):
+    kw["dict_subjects"] = w["dsub"]
 free0, total = torch.cuda.mem_get_info(0)
 c = SwimCluster(bench.preset_config(w["preset"]), w["n"], seed=1, gossip_capacity=w["gcap"], device=0,
                 sync_capacity=w.get("scap", 0), _shard=(0, world), **kw)
