@@ -325,6 +325,30 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev);
 /* Begin a period (when none is in flight) or resume it after the described exchange. */
 int swim_shard_step(swim_handle* h, swim_xchg* x);
 
+/* Library-driven exchanges. With a transport attached, swim_step / swim_step_async advance a sharded
+ * handle through whole periods: at each exchange the library gathers every rank's status row (error
+ * code, op, send counts: one small all-gather and one host stop, so an error any rank detects fails
+ * every rank together), then moves the data itself (an all-gather padded to the largest block, or an
+ * all-to-all-v) and resumes. The handle allocates its exchange buffers unless swim_shard_attach gave
+ * some. Either the library's own RCCL communicator over xGMI (swim_shard_comm_init: rank 0 makes a
+ * unique id with swim_rccl_unique_id and the host hands it to every rank; the collectives run on the
+ * handle's stream), or the host's collectives through a swim_transport (host_staged = 1: the library
+ * stages through host memory and calls back with host pointers, e.g. gloo; 0: device pointers on
+ * `stream`). Both calls return 0 on success; rank order everywhere. */
+typedef struct swim_transport {
+  void* ctx;
+  uint32_t host_staged;
+  /* every rank contributes `bytes` from send; recv gets world blocks of `bytes`, in rank order */
+  int (*allgather)(void* ctx, const void* send, void* recv, uint64_t bytes, void* stream);
+  /* send_bytes[q] bytes to rank q (consecutive in send, in rank order); recv_bytes[q] from rank q */
+  int (*alltoallv)(void* ctx, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes,
+                   void* stream);
+} swim_transport;
+int swim_shard_set_transport(swim_handle* h, const swim_transport* t);
+int swim_rccl_unique_id(uint8_t unique_id[128]);
+/* rank / world must equal the handle's shard_rank / shard_world */
+int swim_shard_comm_init(swim_handle* h, const uint8_t unique_id[128], uint32_t rank, uint32_t world);
+
 /* Events in canonical order (period, observer, phase, subject, type, reason, record). buf = NULL
  * with cap = 0 discards the pending events and returns their count (no copy, no sort). */
 int swim_drain_events(swim_handle* h, swim_event* buf, uint64_t cap, uint64_t* n_out);

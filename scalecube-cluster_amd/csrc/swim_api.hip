@@ -5,6 +5,7 @@
 // the replacement for ClusterImpl's per-member wiring of FailureDetectorImpl,
 // GossipProtocolImpl and MembershipProtocolImpl (core/ClusterImpl.java:170-227) for N members.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -44,6 +45,7 @@ struct swim_handle {
   uint32_t q = 0;
   // sharding
   uint32_t world = 1, rank = 0;
+  bool sharded = false;  // periods stop at exchanges: world > 1, or world 1 with a transport (a test of it)
   uint32_t n_leaving = 0;  // swim_leave calls so far (the stop check runs only once one happened)
   uint32_t n0 = 0;          // members started at create (swim_config.n_initial)
   std::vector<uint8_t> started;  // ids ever started (spare slots: until swim_join / swim_restart)
@@ -72,6 +74,12 @@ struct swim_handle {
   unsigned long long* d_digest = nullptr;
   uint32_t* d_scan = nullptr;  // k_scan_tiles sums and their exclusive scan
   std::vector<void*> allocs;
+  // library-driven exchanges (swim_shard_set_transport / swim_shard_comm_init)
+  swim_transport tr{};
+  bool has_tr = false;
+  ncclComm_t comm = nullptr;
+  uint64_t* d_status = nullptr;  // [(1 + world) * (2 + world)]: this rank's status row, then all ranks'
+  std::vector<uint8_t> hsend, hrecv;  // host staging of a host_staged transport
   std::string err;
   // timing
   bool timing = false;
@@ -120,6 +128,8 @@ int dalloc(swim_handle* h, T** p, size_t count) {
 }
 
 void free_all(swim_handle* h) {
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  h->comm = nullptr;
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
   for (auto ev : h->pool) (void)hipEventDestroy(ev);
@@ -297,7 +307,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
 // first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t bound = NONE) {
   hipStream_t s = h->stream;
-  if (h->world == 1) {
+  if (!h->sharded) {
     *rc = commit_sorted(h, P, P.stg, 0u, bound);
     return false;
   }
@@ -377,6 +387,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
 // the period, or SWIM_OK with another op when an exchange must happen first (world > 1).
 int period_resume(swim_handle* h, swim_xchg* x) {
   const uint32_t N = h->N, G = h->G, W = h->world, nloc = h->base.nloc;
+  const bool SH = h->sharded;  // exchanges happen (world > 1, or a world-1 handle with a transport)
   const uint32_t RL = h->base.W;  // cells of a SYNC row (dense N, N x K the K columns)
   const uint32_t gL = blocks_for(nloc, 256);
   hipStream_t s = h->stream;
@@ -389,7 +400,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         h->pc = PC_FD_TRACK;
         if (P.nxk) {  // N x K: columns for the subjects this FD phase changes first
           timed(h, 0, "k_fd_track", [&] { hipLaunchKernelGGL(k_fd_track, dim3(gL), dim3(256), 0, s, P); });
-          if (W > 1) {  // every shard's requests to every shard: all allocate the same columns
+          if (SH) {  // every shard's requests to every shard: all allocate the same columns
             Ctl c;
             if ((rc = read_ctl(h, &c))) return rc;
             P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
@@ -403,7 +414,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         break;
       case PC_FD_TRACK:
-        if (P.nxk && W > 1) {
+        if (P.nxk && SH) {
           uint32_t cnt[SWIM_MAX_WORLD];
           for (uint32_t q = 0; q < W; ++q) cnt[q] = (uint32_t)x->recv_counts[q];
           HIPC(h, hipMemcpyAsync(h->d_xcounts, cnt, 4ull * W, hipMemcpyHostToDevice, s));
@@ -420,7 +431,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (rc) return rc;
         break;
       case PC_FD_C:
-        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        if (SH && (rc = commit_end(h, P, x))) return rc;
         h->q = 0;
         h->pc = PC_R_MAX;
         break;
@@ -429,7 +440,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         h->pc = PC_R_SEL;
         break;
       case PC_R_SEL:
-        if (W > 1) {  // liveness + bounds over every shard arrived with the last commit
+        if (SH) {  // liveness + bounds over every shard arrived with the last commit
           P.blx = h->d_blx;
           HIPC(h, hipMemsetAsync(P.ctl->xg_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         }
@@ -442,7 +453,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (P.dq)  // rings exist once a delay was set; messages in flight arrive even after it is reset
           timed(h, 10, "k_gossip_pairdelay", [&] { hipLaunchKernelGGL(k_gossip_pairdelay, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
-        if (W > 1) {  // (1) registrations with receivers on other shards
+        if (SH) {  // (1) registrations with receivers on other shards
           Ctl c;
           if ((rc = read_ctl(h, &c))) return rc;
           if (c.n_act > 32u * 1024u) return fail(h, SWIM_EOVERFLOW, "active list too long for sharded need bitmaps");
@@ -513,7 +524,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         return SWIM_OK;
       }
       case PC_R_PULL:
-        if (W > 1) {
+        if (SH) {
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           P.nneed = h->nneed;
           if (h->n_in_pairs)
@@ -549,7 +560,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (rc) return rc;
         break;
       case PC_R_C:
-        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        if (SH && (rc = commit_end(h, P, x))) return rc;
         h->q++;
         h->pc = h->q < G ? PC_R_MAX : PC_SUSP;
         break;
@@ -569,7 +580,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (P.njoin) hipLaunchKernelGGL(k_join_select, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
         timed(h, 6, "k_sync_snapshot", [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_REQ;
-        if (W > 1) {  // tables of requesters whose receiver lives on another shard
+        if (SH) {  // tables of requesters whose receiver lives on another shard
           Ctl c;
           if ((rc = read_ctl(h, &c))) return rc;
           uint32_t n_rec = 0;
@@ -587,7 +598,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         break;
       case PC_SYNC_REQ: {
         uint32_t n_rec = 0;
-        if (W > 1) {
+        if (SH) {
           uint64_t words = 0;
           for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
           n_rec = (uint32_t)(words / (RL + 2u));
@@ -610,7 +621,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
-        if (W > 1) {  // SYNC_ACK tables back to the requesters' shards, in the order received
+        if (SH) {  // SYNC_ACK tables back to the requesters' shards, in the order received
           uint64_t back[SWIM_MAX_WORLD];
           for (uint32_t q = 0; q < W; ++q) back[q] = x->recv_counts[q];
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
@@ -622,7 +633,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
       }
       case PC_SYNC_ACK:  // phase G+3: SYNC_ACK
         set_phase(h, P, G + 3);
-        if (W > 1) {
+        if (SH) {
           uint64_t words = 0;
           for (uint32_t q = 0; q < W; ++q) words += x->recv_counts[q];
           const uint32_t n_rec = (uint32_t)(words / (RL + 2u));
@@ -636,7 +647,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (rc) return rc;
         break;
       case PC_END: {
-        if (W > 1 && (rc = commit_end(h, P, x))) return rc;
+        if (SH && (rc = commit_end(h, P, x))) return rc;
         if (P.hd4) {  // escape entries of swept / rewritten slots become tombstones
           memset_ctl_u32(h, offsetof(Ctl, hx_live));
           timed(h, 7, "k_hx_sweep", [&] { hipLaunchKernelGGL(k_hx_sweep, dim3(1024), dim3(256), 0, s, P); });
@@ -677,6 +688,161 @@ int check_overflow(swim_handle* h) {
                   "detail 0x%x (1 misprediction, 2 records per pair, 4 pruned pairs, 8 delivery records, 16 in-history)",
                   ov, why);
     return fail(h, SWIM_EOVERFLOW, buf);
+  }
+  return SWIM_OK;
+}
+
+// ---- library-driven exchanges ---------------------------------------------
+// The library-owned RCCL communicator as a transport: collectives on the handle's stream
+int rccl_allgather(void* ctx, const void* send, void* recv, uint64_t bytes, void* stream) {
+  swim_handle* h = static_cast<swim_handle*>(ctx);
+  return ncclAllGather(send, recv, bytes, ncclUint8, h->comm, static_cast<hipStream_t>(stream)) == ncclSuccess ? 0 : -1;
+}
+int rccl_alltoallv(void* ctx, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb, void* stream) {
+  swim_handle* h = static_cast<swim_handle*>(ctx);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint64_t so = 0, ro = 0;
+  if (ncclGroupStart() != ncclSuccess) return -1;
+  for (uint32_t q = 0; q < h->world; ++q) {
+    if (sb[q] && ncclSend(static_cast<const uint8_t*>(send) + so, sb[q], ncclUint8, (int)q, h->comm, s) != ncclSuccess)
+      return -1;
+    if (rb[q] && ncclRecv(static_cast<uint8_t*>(recv) + ro, rb[q], ncclUint8, (int)q, h->comm, s) != ncclSuccess)
+      return -1;
+    so += sb[q];
+    ro += rb[q];
+  }
+  return ncclGroupEnd() == ncclSuccess ? 0 : -1;
+}
+
+// One all-gather of n bytes per rank through the transport (send / recv: device buffers)
+int tr_allgather(swim_handle* h, const void* send, void* recv, uint64_t n) {
+  if (!h->tr.host_staged) {
+    if (h->tr.allgather(h->tr.ctx, send, recv, n, h->stream))
+      return fail(h, SWIM_ERCCL, "shard exchange: all-gather failed");
+    return SWIM_OK;
+  }
+  const uint64_t W = h->world;
+  if (h->hsend.size() < n) h->hsend.resize(n);
+  if (h->hrecv.size() < W * n) h->hrecv.resize(W * n);
+  HIPC(h, hipMemcpyAsync(h->hsend.data(), send, n, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (h->tr.allgather(h->tr.ctx, h->hsend.data(), h->hrecv.data(), n, nullptr))
+    return fail(h, SWIM_ERCCL, "shard exchange: all-gather failed");
+  HIPC(h, hipMemcpyAsync(recv, h->hrecv.data(), W * n, hipMemcpyHostToDevice, h->stream));
+  return SWIM_OK;
+}
+
+int tr_alltoallv(swim_handle* h, const uint64_t* sb, const uint64_t* rb) {
+  if (!h->tr.host_staged) {
+    if (h->tr.alltoallv(h->tr.ctx, h->xsend, sb, h->xrecv, rb, h->stream))
+      return fail(h, SWIM_ERCCL, "shard exchange: all-to-all-v failed");
+    return SWIM_OK;
+  }
+  uint64_t st = 0, rt = 0;
+  for (uint32_t q = 0; q < h->world; ++q) {
+    st += sb[q];
+    rt += rb[q];
+  }
+  if (h->hsend.size() < st) h->hsend.resize(st);
+  if (h->hrecv.size() < rt) h->hrecv.resize(rt);
+  if (st) HIPC(h, hipMemcpyAsync(h->hsend.data(), h->xsend, st, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (h->tr.alltoallv(h->tr.ctx, h->hsend.data(), sb, h->hrecv.data(), rb, nullptr))
+    return fail(h, SWIM_ERCCL, "shard exchange: all-to-all-v failed");
+  if (rt) HIPC(h, hipMemcpyAsync(h->xrecv, h->hrecv.data(), rt, hipMemcpyHostToDevice, h->stream));
+  return SWIM_OK;
+}
+
+// The status all-gather every exchange starts with: row = {error code, op, send words / counts}.
+// Every rank learns every rank's counts (an all-to-all-v needs them before the data moves) and
+// every error: a failure one rank detects fails all of them at the same exchange, never a hang.
+int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t>* rows) {
+  const uint32_t W = h->world, R = 2u + W;
+  std::vector<uint64_t> row(R, 0ull);
+  row[0] = (uint64_t)(int64_t)code;
+  row[1] = code ? ~0ull : x.op;
+  if (!code && x.op == SWIM_X_ALLGATHER) row[2] = x.send_words;
+  if (!code && x.op == SWIM_X_ALLTOALLV)
+    for (uint32_t q = 0; q < W; ++q) row[2 + q] = x.send_counts[q];
+  HIPC(h, hipMemcpyAsync(h->d_status, row.data(), 8ull * R, hipMemcpyHostToDevice, h->stream));
+  int rc = tr_allgather(h, h->d_status, h->d_status + R, 8ull * R);
+  if (rc) return rc;
+  rows->resize((size_t)W * R);
+  HIPC(h, hipMemcpyAsync(rows->data(), h->d_status + R, 8ull * W * R, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  return SWIM_OK;
+}
+
+// One period of a sharded handle with a transport: period_resume up to each exchange, the status
+// all-gather, the collective, resume.
+int tr_period(swim_handle* h) {
+  const uint32_t W = h->world, R = 2u + W;
+  std::vector<uint64_t> rows;
+  for (;;) {
+    swim_xchg x;
+    int rc = period_resume(h, &x);
+    if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow check joins the status
+      HIPC(h, hipStreamSynchronize(h->stream));
+      resolve_timing(h);
+      rc = check_overflow(h);
+    }
+    const std::string mine = rc ? h->err : std::string();
+    const int src = tr_status(h, rc, x, &rows);
+    if (src) return src;
+    for (uint32_t q = 0; q < W; ++q)
+      if (rows[(size_t)q * R]) {
+        if (rc) return fail(h, rc, mine);
+        return fail(h, (int)(int64_t)rows[(size_t)q * R], "shard exchange: rank " + std::to_string(q) + " failed");
+      }
+    for (uint32_t q = 1; q < W; ++q)
+      if (rows[(size_t)q * R + 1] != rows[1]) return fail(h, SWIM_EINVAL, "shard exchange: ranks out of step");
+    if (x.op == SWIM_X_DONE) return SWIM_OK;
+    if (x.op == SWIM_X_ALLGATHER) {
+      uint64_t m = 0;
+      for (uint32_t q = 0; q < W; ++q) m = std::max(m, rows[(size_t)q * R + 2]);
+      if (m * W > h->xrecv_words) return fail(h, SWIM_EOVERFLOW, "shard exchange: all-gather over the receive buffer");
+      if (m && (rc = tr_allgather(h, h->xsend, h->xrecv, 4ull * m))) return rc;
+      for (uint32_t q = 0; q < W; ++q) x.recv_counts[q] = rows[(size_t)q * R + 2];
+      x.recv_stride = m;
+    } else if (x.op == SWIM_X_ALLTOALLV) {
+      uint64_t sb[SWIM_MAX_WORLD], rb[SWIM_MAX_WORLD], vol = 0;
+      for (uint32_t r = 0; r < W; ++r) {  // every rank checks every rank's volumes: all fail together
+        uint64_t out = 0, in = 0;
+        for (uint32_t q = 0; q < W; ++q) {
+          out += rows[(size_t)r * R + 2 + q];
+          in += rows[(size_t)q * R + 2 + r];
+        }
+        if (out > h->xsend_words || in > h->xrecv_words)
+          return fail(h, SWIM_EOVERFLOW, "shard exchange over the buffer capacity on rank " + std::to_string(r));
+        vol += out;
+      }
+      for (uint32_t q = 0; q < W; ++q) {
+        sb[q] = 4ull * rows[(size_t)h->rank * R + 2 + q];
+        rb[q] = 4ull * rows[(size_t)q * R + 2 + h->rank];
+        x.recv_counts[q] = rb[q] / 4;
+      }
+      if (vol && (rc = tr_alltoallv(h, sb, rb))) return rc;
+      x.recv_stride = vol;  // the global volume: 0 lets the library skip ahead
+    } else {
+      return fail(h, SWIM_EINVAL, "shard exchange: unknown op");
+    }
+  }
+}
+
+// exchange buffers and the status rows of a handle that drives its own exchanges
+int tr_buffers(swim_handle* h) {
+  const uint32_t W = h->world, R = 2u + W;
+  int rc = SWIM_OK;
+  if (!h->d_status && (rc = dalloc(h, &h->d_status, (size_t)(1 + W) * R))) return rc;
+  if (!h->xsend) {
+    uint64_t sw = 0, rw = 0;
+    if ((rc = swim_shard_buffer_words(h, &sw, &rw))) return rc;
+    uint32_t *a = nullptr, *b = nullptr;
+    if ((rc = dalloc(h, &a, sw)) || (rc = dalloc(h, &b, rw))) return rc;
+    h->xsend = a;
+    h->xrecv = b;
+    h->xsend_words = sw;
+    h->xrecv_words = rw;
   }
   return SWIM_OK;
 }
@@ -803,6 +969,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   P.seed = c.seed;
   h->world = world;
   h->rank = c.shard_rank;
+  h->sharded = world > 1;
   P.world = world;
   P.rank = c.shard_rank;
   P.nloc = N / world;
@@ -1345,7 +1512,7 @@ int start_member(swim_handle* h, uint32_t x, uint32_t a) {
 }
 
 int join_checks(swim_handle* h, uint32_t n) {
-  if (h->world > 1 || h->base.nxk) return fail(h, SWIM_EINVAL, "join / restart: dense, unsharded handles only");
+  if (h->sharded || h->base.nxk) return fail(h, SWIM_EINVAL, "join / restart: dense, unsharded handles only");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "join / restart: a period is in flight");
   const uint64_t seeds = std::min<uint64_t>(h->cfg.n_seeds, h->N);
   if ((uint64_t)(h->base.njoin + n) * std::max<uint64_t>(1, seeds) > h->scap)
@@ -1507,9 +1674,10 @@ int swim_trace(swim_handle* h, uint32_t mask) {
 
 int swim_step_async(swim_handle* h, uint32_t periods) {
   if (!h) return SWIM_EINVAL;
-  if (h->world > 1) return fail(h, SWIM_EINVAL, "sharded handle: use swim_shard_step");
+  if (h->sharded && !h->has_tr)
+    return fail(h, SWIM_EINVAL, "sharded handle: attach a transport (swim_shard_comm_init) or use swim_shard_step");
   for (uint32_t p = 0; p < periods; ++p) {
-    int rc = step_one(h);
+    int rc = h->sharded ? tr_period(h) : step_one(h);
     if (rc) return rc;
   }
   return SWIM_OK;
@@ -1929,9 +2097,48 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev) {
   return SWIM_OK;
 }
 
+int swim_shard_set_transport(swim_handle* h, const swim_transport* t) {
+  if (!h || !t || !t->allgather || !t->alltoallv) return SWIM_EINVAL;
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_shard_set_transport: a period is in flight");
+  h->tr = *t;
+  h->has_tr = true;
+  h->sharded = true;  // (world 1: every exchange goes through the transport to this rank alone)
+  return tr_buffers(h);
+}
+
+int swim_rccl_unique_id(uint8_t unique_id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId");
+  if (!unique_id) return SWIM_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SWIM_ERCCL;
+  std::memcpy(unique_id, &id, sizeof id);
+  return SWIM_OK;
+}
+
+int swim_shard_comm_init(swim_handle* h, const uint8_t unique_id[128], uint32_t rank, uint32_t world) {
+  if (!h || !unique_id || world != h->world || rank != h->rank) return SWIM_EINVAL;
+  if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_shard_comm_init: a period is in flight");
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, SWIM_EHIP, "hipSetDevice");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof id);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  h->comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&h->comm, (int)world, id, (int)rank);
+  if (r != ncclSuccess) return fail(h, SWIM_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  swim_transport t{};
+  t.ctx = h;
+  t.host_staged = 0;
+  t.allgather = rccl_allgather;
+  t.alltoallv = rccl_alltoallv;
+  h->tr = t;
+  h->has_tr = true;
+  h->sharded = true;
+  return tr_buffers(h);
+}
+
 int swim_shard_step(swim_handle* h, swim_xchg* x) {
   if (!h || !x) return SWIM_EINVAL;
-  if (h->world > 1 && (!h->xsend || !h->xrecv)) return fail(h, SWIM_EINVAL, "swim_shard_attach first");
+  if (h->sharded && (!h->xsend || !h->xrecv)) return fail(h, SWIM_EINVAL, "swim_shard_attach first");
   int rc = period_resume(h, x);
   if (rc) return rc;
   if (x->op == SWIM_X_DONE) {  // end of period: surface overflows like swim_step

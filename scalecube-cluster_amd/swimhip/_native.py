@@ -148,6 +148,22 @@ class SwimXchg(ctypes.Structure):
     ]
 
 
+# swim_transport (include/swimhip.h): the host's collectives, called back by the library
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                ctypes.c_void_p)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p)
+
+
+class SwimTransport(ctypes.Structure):
+    _fields_ = [
+        ("ctx", ctypes.c_void_p),
+        ("host_staged", ctypes.c_uint32),
+        ("allgather", ALLGATHER_FN),
+        ("alltoallv", ALLTOALLV_FN),
+    ]
+
+
 # (name, restype, argtypes) for every entry point of include/swimhip.h
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
@@ -202,6 +218,9 @@ SWIM_ONLY = [
     ("swim_shard_buffer_words", _I, [_P, _pU64, _pU64]),
     ("swim_shard_attach", _I, [_P, _P, _P]),
     ("swim_shard_step", _I, [_P, ctypes.POINTER(SwimXchg)]),
+    ("swim_shard_set_transport", _I, [_P, ctypes.POINTER(SwimTransport)]),
+    ("swim_rccl_unique_id", _I, [_pU8]),
+    ("swim_shard_comm_init", _I, [_P, _pU8, _U32, _U32]),
 ]
 
 

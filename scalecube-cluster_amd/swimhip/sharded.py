@@ -24,7 +24,14 @@ from .cluster import MembershipEvent, SwimCluster, SwimError
 
 
 class ShardedSwimCluster(SwimCluster):
-    def __init__(self, config, n_members: int, seed: int = 0, *, group=None, device: int = 0, **kw):
+    """exchange = "library" (default): the library drives every exchange of a period itself
+    (swim_step): over its own RCCL communicator on the "nccl" backend (swim_shard_comm_init; rank 0's
+    unique id broadcast once), or through host-staged gloo callbacks (swim_shard_set_transport);
+    one status all-gather and one host stop per exchange. exchange = "host": this class runs each
+    exchange the library describes (swim_shard_step), with torch.distributed."""
+
+    def __init__(self, config, n_members: int, seed: int = 0, *, group=None, device: int = 0,
+                 exchange: str = "library", **kw):
         import torch
         import torch.distributed as dist
 
@@ -45,6 +52,62 @@ class ShardedSwimCluster(SwimCluster):
         self._call("shard_attach", self._h, ctypes.c_void_p(self._send.data_ptr()),
                    ctypes.c_void_p(self._recv.data_ptr()))
         self._x = nat.SwimXchg()
+        if exchange not in ("library", "host"):
+            raise ValueError("exchange: 'library' or 'host'")
+        self._lib_x = exchange == "library"
+        if self._lib_x:
+            self._attach_transport()
+
+    # -- library-driven exchanges ------------------------------------------------------------
+    def _attach_transport(self):
+        if not self._gloo:  # the library's own RCCL communicator over xGMI
+            uid = (ctypes.c_uint8 * 128)()
+            if self.rank == 0:
+                self._call_raw("rccl_unique_id", uid)
+            obj = [bytes(uid)]
+            self._dist.broadcast_object_list(obj, src=0, group=self._group)
+            ctypes.memmove(uid, obj[0], 128)
+            self._call("shard_comm_init", self._h, uid, self.rank, self.world)
+            return
+        torch, dist, grp, W = self._torch, self._dist, self._group, self.world
+        errors = self._cb_errors = []
+
+        def words(ptr, nbytes):  # a host buffer of the library as int32 words (sizes are multiples of 4)
+            return np.ctypeslib.as_array((ctypes.c_int32 * (nbytes // 4)).from_address(ptr)) if nbytes else \
+                np.zeros(0, dtype=np.int32)
+
+        def allgather(ctx, send, recv, nbytes, stream):
+            try:
+                src = torch.from_numpy(words(send, nbytes).copy())
+                parts = [torch.empty_like(src) for _ in range(W)]
+                dist.all_gather(parts, src, group=grp)
+                words(recv, W * nbytes)[:] = torch.cat(parts).numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001 (reported after the library returns)
+                errors.append(e)
+                return -1
+
+        def alltoallv(ctx, send, sb, recv, rb, stream):
+            try:
+                sc = [int(sb[q]) // 4 for q in range(W)]
+                rc = [int(rb[q]) // 4 for q in range(W)]
+                src = torch.from_numpy(words(send, 4 * sum(sc)).copy())
+                out = torch.empty(sum(rc), dtype=torch.int32)
+                dist.all_to_all_single(out, src, rc, sc, group=grp)
+                words(recv, 4 * sum(rc))[:] = out.numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+                return -1
+
+        self._cbs = (nat.ALLGATHER_FN(allgather), nat.ALLTOALLV_FN(alltoallv))  # kept alive with the handle
+        t = nat.SwimTransport(None, 1, self._cbs[0], self._cbs[1])
+        self._call("shard_set_transport", self._h, ctypes.byref(t))
+
+    def _call_raw(self, name, *args):
+        rc = getattr(self._lib, "swim_" + name)(*args)
+        if rc != nat.SWIM_OK:
+            raise SwimError(rc, name)
 
     # -- collectives ---------------------------------------------------------------------
     def _all_gather_ints(self, vals):
@@ -131,6 +194,15 @@ class ShardedSwimCluster(SwimCluster):
         return status
 
     def step(self, periods: int = 1):
+        if self._lib_x:
+            try:
+                self._call("step", self._h, int(periods))
+            except SwimError:
+                if getattr(self, "_cb_errors", None):
+                    raise SwimError(-6, f"host collective failed: {self._cb_errors[0]!r}")
+                raise
+            self.period += int(periods)
+            return
         for _ in range(int(periods)):
             while True:
                 err = None

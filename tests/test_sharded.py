@@ -133,6 +133,38 @@ def test_shard_lifecycle_and_delays_match_unsharded(world, names):
 
 
 @pytest.mark.gpu
+def test_host_driven_exchanges_match_unsharded():
+    """The host-driven protocol (swim_shard_step: the host performs each exchange the library
+    describes, as a Java host with its own collectives would) against the unsharded handle; every
+    other sharded test runs the library-driven exchanges (swim_step with a transport)."""
+    mp.spawn(_parity_worker, args=(2, _free_port(), ["lan256_loss5_crash3", "local32_leave2"], {"exchange": "host"}),
+             nprocs=2, join=True)
+
+
+def _rccl_library_worker(rank, world, port, names):
+    import scenarios
+    from swimhip import SwimCluster
+
+    _init(rank, world, port, "nccl")
+    try:
+        for name in names:
+            scenarios.run_pair(name, lambda *a, **k: ShardedSwimCluster(*a, **k), SwimCluster)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_library_rccl_one_rank_matches_unsharded():
+    """The library-owned RCCL communicator (swim_rccl_unique_id, swim_shard_comm_init: collectives on the
+    handle's stream, one status all-gather per exchange) on a one-rank group: the handle then runs every
+    exchange of a period through RCCL to itself (gossip-id commits with the liveness maxima, the status
+    rows). RCCL refuses two ranks on one GPU, so this is how far the library-owned path runs before a
+    multi-GPU node. Bit-exact with the unsharded handle every period."""
+    mp.spawn(_rccl_library_worker, args=(1, _free_port(), ["c1_local32_crash", "lan256_loss5_crash3", "local32_leave2"]),
+             nprocs=1, join=True)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,names", [(2, ["test48_delay30_partition", "test64_long_partition_rejoin"]),
                                          (4, ["local128_partition_heal"])])
 def test_hd4_shards_match_unsharded_hd8(world, names):
