@@ -14,4 +14,7 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --c
 rc=$?; echo "c3 rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python -u -m pytest tests/test_sharded.py tests/test_memory_plan.py -m gpu -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread \
    > $out/pytest_sharded.log 2>&1
-rc=$?; echo "sharded rc=$rc" >> $out/status.log; exit $rc
+rc=$?; echo "sharded rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_c4_rehearsal.py -m gpu -x -v -s -p no:cacheprovider --timeout 540 --timeout-method thread \
+   > $out/pytest_c4_rehearsal.log 2>&1
+rc=$?; echo "c4 rehearsal rc=$rc" >> $out/status.log; exit $rc
