@@ -65,6 +65,7 @@ struct swim_handle {
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
   uint32_t* crash_ids = nullptr;  // [N] the members one swim_crash call stops (allocated on first use)
   uint32_t* deliver_buf = nullptr;  // swim_deliver_records: subjects, then records (grown on demand)
+  uint32_t* d_rowbuf = nullptr;     // swim_read_deadlines: one decoded row (allocated on first use)
   uint32_t deliver_cap = 0;
   unsigned long long* ck[2] = {nullptr, nullptr};
   unsigned long long* cv[2] = {nullptr, nullptr};
@@ -1775,14 +1776,19 @@ int swim_read_deadlines(swim_handle* h, uint32_t observer, uint32_t* row, uint32
     if (rc) return rc;
   }
   const size_t ncol = h->base.nxk ? subj.size() : h->N;
-  std::vector<uint16_t> cells(ncol);
-  if (ncol)
-    HIPC(h, hipMemcpy2DAsync(cells.data(), 2, h->base.dl + (observer - h->base.row0), (size_t)h->base.nloc * 2, 2,
-                             ncol, hipMemcpyDeviceToHost, h->stream));
+  if (!h->d_rowbuf) {
+    int rc = dalloc(h, &h->d_rowbuf, h->N);
+    if (rc) return rc;
+  }
+  std::vector<uint32_t> cells(ncol);
+  if (ncol) {
+    hipLaunchKernelGGL(k_read_dl, dim3(blocks_for(ncol, 256)), dim3(256), 0, h->stream, h->base,
+                       observer - h->base.row0, t, h->d_rowbuf, (uint32_t)ncol);
+    HIPC(h, hipMemcpyAsync(cells.data(), h->d_rowbuf, ncol * 4, hipMemcpyDeviceToHost, h->stream));
+  }
   HIPC(h, hipStreamSynchronize(h->stream));
   std::fill(row, row + n, 0u);
-  for (size_t c = 0; c < ncol; ++c)
-    if (cells[c]) row[h->base.nxk ? subj[c] : c] = dl_dec(cells[c], t) + 1u;
+  for (size_t c = 0; c < ncol; ++c) row[h->base.nxk ? subj[c] : c] = cells[c];
   return SWIM_OK;
 }
 

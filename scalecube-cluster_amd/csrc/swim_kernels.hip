@@ -4029,6 +4029,15 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
 // ---------------------------------------------------------------------------------------
 // Order-independent digests of every (observer, subject) record and deadline, the same sums
 // for dense and N x K tables (an untracked subject contributes BASELINE in every row).
+// one observer's deadlines (column-strided u16 cells), decoded to the oracle's deadline + 1 (0 = none)
+// at period t, into a dense row: one 2-B element per row of a strided copy is the DMA engines' slow path
+__global__ void k_read_dl(KP P, uint32_t lr, uint32_t t, uint32_t* out, uint32_t ncol) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncol; c += gridDim.x * blockDim.x) {
+    const uint32_t e = P.dl[(size_t)c * P.nloc + lr];
+    out[c] = e ? dl_dec(e, t) + 1u : 0u;
+  }
+}
+
 __global__ void k_digest(KP P, unsigned long long* out) {
   const uint64_t K = 0x9E3779B97F4A7C15ull;
   const uint32_t N = P.N, nloc = P.nloc, row0 = P.row0, nc = ncells(P);
