@@ -1014,8 +1014,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (rc == SWIM_OK) rc = dalloc(h, &(ptr), (count));
   ALLOC(P.view, NN);
   ALLOC(P.dl, NN);
-  {  // spill table: 64 slots per local row, 2^16 .. 2^23 (16 B each: <= 128 MiB)
-    const uint32_t spc = pow2ceil(std::min<uint64_t>(1ull << 23, std::max<uint64_t>(1ull << 16, NL * 64ull)));
+  {  // spill table: room for every (row, cell) at load 1/2 (what the dense inbox held) up to 2^25 slots
+     // (16 B each: <= 512 MiB); a round that spills more keys than that raises OV_SPILL
+    const uint32_t spc = pow2ceil(std::min<uint64_t>(1ull << 25, std::max<uint64_t>(1ull << 16, 2ull * NN)));
     ALLOC(P.sp_key, spc);
     ALLOC(P.sp_val, spc);
     ALLOC(P.sp_used, spc);
