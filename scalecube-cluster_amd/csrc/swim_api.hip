@@ -779,8 +779,9 @@ int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t
 int tr_period(swim_handle* h) {
   const uint32_t W = h->world, R = 2u + W;
   std::vector<uint64_t> rows;
+  swim_xchg x;  // carries each exchange's receive counts into the resumed period
+  xchg_clear(&x, SWIM_X_DONE, W);
   for (;;) {
-    swim_xchg x;
     int rc = period_resume(h, &x);
     if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow check joins the status
       HIPC(h, hipStreamSynchronize(h->stream));
