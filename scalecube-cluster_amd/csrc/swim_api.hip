@@ -71,6 +71,7 @@ struct swim_handle {
   unsigned long long* cv[2] = {nullptr, nullptr};
   // sharded gossip rounds: pairs sent / received, need-bitmap width, scan scratch
   uint32_t n_out_pairs = 0, n_in_pairs = 0, nneed = 0;
+  uint32_t sync_rl = 0;  // cells of a SYNC row exchanged this period (sharded, read at the SYNC phase)
   uint32_t out_pairs[SWIM_MAX_WORLD] = {0};
   unsigned long long* d_digest = nullptr;
   uint32_t* d_scan = nullptr;  // k_scan_tiles sums and their exclusive scan
@@ -252,6 +253,10 @@ void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
 
 int check_overflow(swim_handle* h);
 
+// words after a commit exchange block's gossips: per-word liveness, bit-length bounds, and (dense
+// tmode) the touched-column bitmap
+uint64_t commit_tail(const swim_handle* h) { return h->GC / 32 + 2ull + (h->base.tmode ? h->N / 32 : 0u); }
+
 // Order the phase's gossips by (subject, record) and commit them: one k_commit launch. stg != nullptr: the local stage, counted on the device (no host round trip); otherwise
 // the n gathered gossips already in h->ck[0] / h->cv[0].
 int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, uint32_t bound = NONE) {
@@ -344,7 +349,7 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t b
   hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, hdr + 4u * n + ns);
   HIPC_RC(h, rc, hipStreamSynchronize(s));
   xchg_clear(x, SWIM_X_ALLGATHER, h->world);
-  x->send_words = hdr + 4ull * n + ns + h->GC / 32 + 2;
+  x->send_words = hdr + 4ull * n + ns + commit_tail(h);
   return true;
 }
 
@@ -352,7 +357,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   hipStream_t s = h->stream;
   const uint32_t* xr = reinterpret_cast<const uint32_t*>(h->xrecv);
   uint32_t total = 0, offs[SWIM_MAX_WORLD];
-  const uint64_t tail = h->GC / 32 + 2;  // wlast + bounds after each shard's gossips
+  const uint64_t tail = commit_tail(h);  // wlast + bounds (+ touched columns) after each shard's gossips
   for (uint32_t q = 0; q < h->world; ++q) {
     const uint32_t* blk = xr + q * x->recv_stride;
     uint32_t c = 0, ns = 0, hdr = 0;
@@ -389,7 +394,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
 int period_resume(swim_handle* h, swim_xchg* x) {
   const uint32_t N = h->N, G = h->G, W = h->world, nloc = h->base.nloc;
   const bool SH = h->sharded;  // exchanges happen (world > 1, or a world-1 handle with a transport)
-  const uint32_t RL = h->base.W;  // cells of a SYNC row (dense N, N x K the K columns)
+  uint32_t& RL = h->sync_rl;  // cells of this period's SYNC rows (dense N or touched, N x K the K columns)
   const uint32_t gL = blocks_for(nloc, 256);
   hipStream_t s = h->stream;
   KP& P = h->cur;
@@ -577,6 +582,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         HIPC(h, hipMemsetAsync(P.ctl->xs_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
         (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
         (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
+        if (P.tmode)  // the touched columns this period's SYNC payloads carry
+          timed(h, 7, "k_tlist", [&] { hipLaunchKernelGGL(k_tlist, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 7, "k_sync_select", [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
         if (P.njoin) hipLaunchKernelGGL(k_join_select, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
         timed(h, 6, "k_sync_snapshot", [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
@@ -584,6 +591,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (SH) {  // tables of requesters whose receiver lives on another shard
           Ctl c;
           if ((rc = read_ctl(h, &c))) return rc;
+          RL = (P.tmode && c.ntouched < N) ? c.ntouched : P.W;  // (the same on every shard: tbits are merged)
           uint32_t n_rec = 0;
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
           for (uint32_t q = 0; q < W; ++q) {
@@ -1045,6 +1053,12 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   }
   ALLOC(P.mm, NL * (h->GC / 32));
   ALLOC(P.colmin, P.W);
+  // touched columns (dense views without spare slots: every other column is BASELINE in every row)
+  P.tmode = (!P.nxk && h->n0 == N && N % 32u == 0u) ? 1u : 0u;
+  if (P.tmode) {
+    ALLOC(P.tbits, N / 32);
+    ALLOC(P.tlist, N);
+  }
   if (P.nxk) {
     ALLOC(P.colmap, N);
     ALLOC(P.colsubj, P.W);
@@ -1215,6 +1229,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     (void)hipMemsetAsync(P.hx, 0, ((size_t)P.hxmask + 1) * 8, s);
   }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.W, 256)), dim3(256), 0, s, P.colmin, (size_t)P.W, NONE);
+  if (P.tmode) (void)hipMemsetAsync(P.tbits, 0, (size_t)N / 8, s);
   if (P.nxk) {
     hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.colmap, (size_t)N, NONE);
     (void)hipMemsetAsync(P.track_req, 0, (size_t)N * 4, s);
@@ -2081,7 +2096,7 @@ int swim_shard_buffer_words(swim_handle* h, uint64_t* send_words, uint64_t* recv
   const uint64_t win = nloc * (uint64_t)h->base.f * (2 + W32);
   const uint64_t rows = (uint64_t)h->scap * (h->base.W + 2ull);
   // commits carry the liveness maxima too, and once members leave a header and the stopped members
-  const uint64_t stg = 4ull * h->base.stg_cap + W32 + 2 + 4 + nloc;
+  const uint64_t stg = 4ull * h->base.stg_cap + commit_tail(h) + 4 + nloc;
   // The window bounds assume every pair ships every active word; the need bitmaps ship only the
   // words a receiver lacks something in, far fewer (k_gossip_need), so both buffers are capped at
   // 2^31 words (8 GiB): C4's shards (32,768 rows of 262,144) would otherwise reserve ~90 GB for a

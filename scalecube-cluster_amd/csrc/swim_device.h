@@ -135,6 +135,7 @@ struct Ctl {
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used), reset by k_finalize
+  uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
@@ -155,6 +156,13 @@ struct KP {
   uint32_t* colmap;    // [N] subject -> column, NONE while untracked (N x K only)
   uint32_t* colsubj;   // [K] column -> subject
   uint32_t* colorder;  // [K] the allocated columns in subject order (SYNC merges walk it)
+  // Touched columns of dense views: a subject whose record some row ever changed
+  // from the converged BASELINE. Every other column holds BASELINE in every row, and equal records
+  // never override (MembershipProtocolImpl.java:489), so SYNC / SYNC_ACK payloads carry the touched
+  // columns only, in subject order (tmode: dense handles without spare slots)
+  uint32_t tmode;
+  uint32_t* tbits;     // [N / 32] touched columns (sharded: OR-merged by every commit exchange)
+  uint32_t* tlist;     // [N] the touched columns in ascending order (k_tlist, each SYNC phase)
   uint32_t* track_req;   // [N] subject listed for a column (k_fd_track / k_track_one)
   uint32_t* track_list;  // [tcap] subjects the coming FD phase changes first (k_track_alloc)
   uint32_t tcap;
@@ -470,6 +478,14 @@ __device__ __forceinline__ uint32_t ncells(const KP& P) {
   const uint32_t n = P.ctl->ncols;
   return n < P.W ? n : P.W;
 }
+
+// this period's SYNC payloads carry the touched columns only (in tlist order)
+__device__ __forceinline__ bool tlisted(const KP& P) { return P.tmode && P.ctl->ntouched < P.N; }
+// cells of a SYNC / SYNC_ACK payload row: the listed touched columns, else the row's cells in use
+// (dense N, N x K the allocated columns)
+__device__ __forceinline__ uint32_t sync_cells(const KP& P) { return tlisted(P) ? P.ctl->ntouched : ncells(P); }
+// the words of one cross-shard SYNC record: request, receiver, then the payload
+__device__ __forceinline__ size_t sync_rec_words(const KP& P) { return (tlisted(P) ? P.ctl->ntouched : P.W) + 2u; }
 
 // gossips in the slots `bits` of bitmap word ws (GossipRequest / receipt counters count gossips,
 // not slots): popcount while every slot holds one gossip, else the word's total when the mask
@@ -842,6 +858,13 @@ __host__ __device__ __forceinline__ uint32_t dl_dec(uint32_t e, uint32_t t) {
   return t + (uint32_t)diff;
 }
 
+// a dense column whose cell leaves the converged BASELINE in some row (KP::tbits)
+__device__ __forceinline__ void touch(const KP& P, uint32_t col) {
+  if (!P.tmode) return;
+  const uint32_t b = 1u << (col & 31u);
+  if (!(P.tbits[col >> 5] & b)) atomicOr(&P.tbits[col >> 5], b);
+}
+
 // A removed cell (present -> absent) drops the batched apply's merge mark of its subject's block:
 // records that did not override the present cell may override what the cell becomes next
 __device__ __forceinline__ void mark_clear(const KP& P, uint32_t obs, uint32_t subj) {
@@ -869,6 +892,7 @@ __device__ __forceinline__ uint32_t apply_record(const KP& P, uint32_t obs, uint
   // a record of another member id at the observer's own address is ignored (MPI:499-505)
   if (P.rerouted && subj != obs && P.addr[subj] == P.addr[obs]) return 0u;
   const bool spread = reason != SWIM_R_MEMBERSHIP_GOSSIP && reason != SWIM_R_INITIAL_SYNC;
+  touch(P, col);  // every accepted record below writes the cell (a refutation too)
   if (subj == obs) {
     const uint32_t inc1 = (r1 == SWIM_DEAD) ? rec_inc(r0) : rec_inc(r1);
     const uint32_t inc0 = rec_inc(r0);

@@ -111,6 +111,7 @@ __global__ void k_leave(KP P, uint32_t i) {  // one wave; lane 0 does the work
     if (col == NONE) {                   // no column left (OV_TRACK): the run has failed
       atomicOr(&P.ctl->overflow, OV_TRACK);
     } else if (is_local(P, i)) {
+      touch(P, col);
       P.view[lrow(P, i) * P.W + col] = SWIM_DEAD;
       emit_gossip(P, i, i, SWIM_DEAD, P.gseq[i]++);
       created = 1;
@@ -181,6 +182,7 @@ __global__ void k_update_meta(KP P, uint32_t i) {  // one wave; lane 0 does the 
     if (col == NONE) {
       atomicOr(&P.ctl->overflow, OV_TRACK);
     } else if (is_local(P, i)) {
+      touch(P, col);
       uint32_t* cellp = P.view + lrow(P, i) * P.W + col;
       const uint32_t r = SWIM_PACK(rec_inc(*cellp) + 1u, SWIM_ALIVE);
       *cellp = r;
@@ -3328,13 +3330,16 @@ __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
     uint32_t dst, i;
     if (!xrec_locate(P, P.ctl->xs_cnt, g, &dst, &i)) break;
     const uint32_t q = P.xs_pend[(size_t)dst * 2u * P.nloc + i];
-    uint32_t* out = P.xsend + (size_t)g * (P.W + 2u);  // a row of W cells (N x K: columns)
+    uint32_t* out = P.xsend + (size_t)g * sync_rec_words(P);  // a row of W cells (N x K: columns; tmode: touched)
     if (threadIdx.x == 0) {
       out[0] = q;
       out[1] = P.req_to[q];
     }
     const uint32_t* row = P.view + lrow(P, q >> 1) * P.W;
-    for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) out[2 + c] = row[c];
+    if (tlisted(P))
+      for (uint32_t c = threadIdx.x; c < P.ctl->ntouched; c += blockDim.x) out[2 + c] = row[P.tlist[c]];
+    else
+      for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) out[2 + c] = row[c];
   }
 }
 
@@ -3343,7 +3348,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
-    const uint32_t* rec = P.xrecv + (size_t)g * (P.W + 2u);
+    const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     P.rs_ref[rec[0]] = g;
     atomicAdd(&P.recv_count[rec[1]], 1u);
   }
@@ -3353,7 +3358,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n_rec) {
-    const uint32_t* rec = P.xrecv + (size_t)g * (P.W + 2u);
+    const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     const uint32_t to = rec[1];
     P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = 4u * (rec[0] >> 1) + (rec[0] & 1u);
   }
@@ -3363,7 +3368,7 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
 __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * (P.W + 2u)]] = g;
+  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * sync_rec_words(P)]] = g;
 }
 
 // Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
@@ -3382,6 +3387,9 @@ __global__ void k_round_max_pack(KP P, uint32_t off) {
     P.xsend[off + W32] = bhi;
     P.xsend[off + W32 + 1] = 32u - blo;  // 0 when this shard has no alive member
   }
+  if (P.tmode)  // the touched columns after the bounds (OR-merged)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (P.N >> 5); i += gridDim.x * blockDim.x)
+      P.xsend[off + W32 + 2u + i] = P.tbits[i];
 }
 
 // element-wise max over the shards' blocks (offsets in `offs`) into wlast and blx
@@ -3398,6 +3406,12 @@ __global__ void k_round_max_merge(KP P, const uint32_t* offs, uint32_t* blx) {
     else
       blx[i - W32] = v;
   }
+  if (P.tmode)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (P.N >> 5); i += gridDim.x * blockDim.x) {
+      uint32_t v = 0;
+      for (uint32_t q = 0; q < P.world; ++q) v |= P.xrecv[offs[q] + W32 + 2u + i];
+      P.tbits[i] = v;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3724,10 +3738,46 @@ __global__ void k_join_scatter(KP P) {
 }
 
 // prepareSyncDataMsg (MembershipProtocolImpl.java:457-461): payload = sender's table at phase start.
+// Dense views in tmode: the touched columns in ascending order (tlist, ntouched) for this period's
+// SYNC payloads. One workgroup, an ordered compaction: thread t takes 64 consecutive columns (two
+// bitmap words), one block scan places them.
+__global__ void __launch_bounds__(1024) k_tlist(KP P) {
+  SWIM_GUARD(P);
+  __shared__ uint32_t s_lds[16];
+  uint32_t base = 0;
+  for (uint32_t c0 = 0; c0 < P.N; c0 += 65536u) {
+    const uint32_t w = (c0 >> 5) + 2u * threadIdx.x;
+    const uint32_t nw = P.N >> 5;  // (N is a multiple of 32 in tmode: swim_create)
+    unsigned long long m = 0ull;
+    if (w < nw) m = P.tbits[w];
+    if (w + 1u < nw) m |= (unsigned long long)P.tbits[w + 1u] << 32;
+    uint32_t tot;
+    uint32_t o = base + block_excl_scan1024((uint32_t)__popcll(m), &tot, s_lds);
+    while (m) {
+      P.tlist[o++] = 32u * w + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+    }
+    base += tot;
+  }
+  // beyond a quarter of the columns a gather reads nearly every line of a row anyway: whole rows
+  // (16-B streams) this period, ntouched = N
+  if (threadIdx.x == 0) P.ctl->ntouched = 4u * base > P.N ? P.N : base;
+}
+
+
 __global__ void __launch_bounds__(256) k_sync_snapshot(KP P) {
   SWIM_GUARD(P);
   uint32_t n = P.ctl->stage_count;
   if (n > P.scap) n = P.scap;
+  if (tlisted(P)) {  // the touched columns only: a gather from the sender's row
+    const uint32_t T = P.ctl->ntouched;
+    for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+      const uint32_t* row = P.view + lrow(P, P.stage_req[k] >> 1) * P.W;
+      uint32_t* dst = P.stage_sync + (size_t)k * P.W;
+      for (uint32_t c = threadIdx.x; c < T; c += blockDim.x) dst[c] = row[P.tlist[c]];
+    }
+    return;
+  }
   const uint32_t W = ncells(P), nv = (P.W & 3u) ? 0u : W / 4u;  // a row = the first ncells cells
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t from = P.stage_req[k] >> 1;
@@ -3817,8 +3867,9 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
   // numbers come out exactly as in the dense table; untracked subjects hold BASELINE on both
   // sides, and equal records never override (MembershipProtocolImpl.java:489).
   // Cells the incoming record does not override (the common case) never enter updateMembership.
-  const uint32_t nc = ncells(P);
-  const uint32_t per = (!P.nxk && (P.W & 3u) == 0u) ? 4u : 1u;
+  const uint32_t nc = sync_cells(P);
+  const bool listed = tlisted(P);
+  const uint32_t per = (!P.nxk && !listed && (P.W & 3u) == 0u) ? 4u : 1u;
   __shared__ uint32_t s_chk[32];  // 1,024-cell chunks with an overridden cell (rows of <= 2^20 cells)
   if (per == 4u) {
     // Most merges change nothing (a converged or converging cluster): first a barrier-free stream
@@ -3864,6 +3915,10 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
         sv[0] = s4.x, sv[1] = s4.y, sv[2] = s4.z, sv[3] = s4.w;
         vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
         cv[0] = c, cv[1] = c + 1u, cv[2] = c + 2u, cv[3] = c + 3u;
+      } else if (listed) {  // the touched columns: payload position c holds column tlist[c]
+        cv[0] = P.tlist[c];
+        sv[0] = src[c];
+        vv[0] = row[cv[0]];
       } else {
         cv[0] = P.nxk ? P.colorder[c] : c;
         sv[0] = src[cv[0]];
@@ -3884,7 +3939,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
         if (per == 4u)
           *reinterpret_cast<uint4*>(ack_out + c) = make_uint4(vv[0], vv[1], vv[2], vv[3]);
         else
-          ack_out[cv[0]] = vv[0];
+          ack_out[listed ? c : cv[0]] = vv[0];
       }
     }
     if (__syncthreads_or(nrec != 0u)) {  // gossip sequence numbers in subject order
@@ -3952,7 +4007,7 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
       src = P.stage_sync + (size_t)slot * P.W;
       ack = P.stage_ack + (size_t)slot * P.W;
     } else {  // request from another shard: payload in the received record, ack into the same
-      const size_t g = (size_t)P.rs_ref[q] * (P.W + 2u);  // position of the send buffer
+      const size_t g = (size_t)P.rs_ref[q] * sync_rec_words(P);  // position of the send buffer
       src = P.xrecv + g + 2;
       ack = P.xsend + g + 2;
       if (threadIdx.x == 0) {
@@ -3963,7 +4018,7 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
     merge_row(P, j, src, ack, q, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[j] = seq;
-  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * ncells(P) : 0u);
+  add_stat(P, ST_MERGE_CELLS, threadIdx.x == 0 ? cntj * sync_cells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
@@ -4013,13 +4068,13 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
     } else {
       const uint32_t qq = 2 * i + kd[k], slot = P.req_stage[qq];
       attempt = (to[k] << 1) | kd[k];
-      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * (P.W + 2u) + 2 : P.stage_ack + (size_t)slot * P.W;
+      src = slot == REMOTE ? P.xrecv + (size_t)P.ack_ref[qq] * sync_rec_words(P) + 2 : P.stage_ack + (size_t)slot * P.W;
     }
     merge_row(P, i, src, nullptr, attempt, reason, snap, seq, T, created, s_lds4);
   }
   if (threadIdx.x == 0) P.gseq[i] = seq;
   add_stat(P, ST_ACKS_DELIVERED, threadIdx.x == 0 ? n : 0u);
-  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * ncells(P) : 0u);
+  add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * sync_cells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
 }
