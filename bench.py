@@ -139,15 +139,17 @@ def kernel_bytes(name, d, rounds_per_period=5):
         # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4).
         # One-gossip slots (k_gossip_apply): per subject run one ring record (8 B), per subject the
         # table cell and its deadline (8 B). Batch slots (k_gossip_apply_b):
-        # per run top its record range (8 B), per record its dictionary entry id (4 B), per merged
-        # subject block the entry's record, the block's subject and the table cell (12 B)
+        # per run top its record range (8 B), per record its dictionary entry id (4 B), per block with
+        # received entries its merge mark and the block's generation (8 B), and per block merged (not
+        # skipped by its mark) the entry's record, the block's subject and the table cell (12 B)
         recs = d.get("apply_records", 0)
         if recs:
-            return 93 * d["apply_words"] + 8 * d["apply_runs"] + 4 * recs + 12 * d["apply_subjects"]
+            blocks = d["apply_subjects"] + d.get("apply_skipped", 0)
+            return 93 * d["apply_words"] + 8 * d["apply_runs"] + 4 * recs + 8 * blocks + 12 * d["apply_subjects"]
         return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
-    if name == "k_susp_sweep":  # stream a deadline column; per fired cell the deadline write, the
+    if name == "k_susp_sweep":  # stream a u16 deadline column; per fired cell the deadline write, the
         # view cell read + write, and (a handle with an event ring) its 24-B REMOVED event
-        return 4 * d["sweep_cells"] + 12 * d["suspicion_timeouts"] + 24 * d.get("sweep_events", 0)
+        return 2 * d["sweep_cells"] + 10 * d["suspicion_timeouts"] + 24 * d.get("sweep_events", 0)
     if name == "k_fd":  # cursor + count + liveness + target/proxy cells + own cell r/w (~24 B/member)
         return 24 * d["fd_probes"]
     # infectedFrom bookkeeping: in-history ring entries (16 B per registration,
@@ -524,7 +526,8 @@ def main():
                                    "merge_cells", "gossip_scanned", "gossip_hd_words", "gossip_window_words",
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
                                    "infected_suppressed", "infected_pruned_pairs", "infected_records",
-                                   "apply_words", "apply_runs", "apply_subjects", "apply_records", "apply_spills")},
+                                   "apply_words", "apply_runs", "apply_subjects", "apply_records", "apply_spills",
+                                   "apply_skipped")},
         "gossip_slots": {"live_at_end": s1["live_gossip_slots"], "gossips_live_at_end": s1["live_gossip_records"]},
     }
     c.close()
