@@ -166,6 +166,11 @@ def kernel_bytes(name, d, rounds_per_period=5):
     return 0
 
 
+# the kernel classes that can dominate a period (the roofline line's candidates): only these carry HIP
+# events in the timed region by default (--timing major)
+MAJOR_CLASSES = ["k_gossip_select", "k_gossip_pull", "k_gossip_apply", "k_susp_sweep", "k_sync_merge", "k_sync_ack",
+                 "k_sync_snapshot"]
+
 # kernel class (swim_kernel_time index names) -> the kernels rocprof sees under it
 KERNEL_NAMES = {"k_gossip_apply": ["k_gossip_apply", "k_gossip_apply_b", "k_gossip_apply_h4", "k_gossip_apply_b_h4"],
                 "k_gossip_select": ["k_gossip_select", "k_gossip_select_h4"],
@@ -362,6 +367,10 @@ def main():
                     help="per (member, slot) infection rounds: 0 = the library's choice (DESIGN.md §4.4)")
     ap.add_argument("--unbatched", action="store_true", help="one ring slot per gossip (A/B of DESIGN.md §3.12)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--timing", default="major", choices=["major", "all"],
+                    help="kernel classes bracketed by HIP events in the timed region: the ones that can dominate "
+                         "a period (gossip select / pull / apply, suspicion sweep, SYNC merges), or every class "
+                         "(each event pair adds a few microseconds of stream time to every small launch)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for --gpus > 1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     args = ap.parse_args()
@@ -403,7 +412,7 @@ def main():
     crashed = inject_faults(c, args.workload, args.warmup, args.seed)
     crash_period = args.warmup
     s0 = c.stats()
-    c.kernel_timing(True)
+    c.kernel_timing(True, classes=None if args.timing == "all" else MAJOR_CLASSES)
     barrier()
     c.sync()
     t0 = time.perf_counter()
@@ -508,7 +517,7 @@ def main():
         "rates": {"gossip_first_receipts_per_s": d["gossip_first_receipts"] / elapsed,
                   "gossips_created_per_s": d["gossips_created"] / elapsed,
                   "gossip_requests_per_s": d["gossip_sends"] / elapsed},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": dom, "timed_classes": args.timing, "achieved": rl["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": rl["frac"], "traffic": pmc_traffic(dom, args.workload, world, args.steps, args.warmup),
                      "bytes_per_launch": rl["bytes_per_launch"], "avg_launch_ms": rl["avg_launch_ms"],
                      "launches": rl["launches"]},

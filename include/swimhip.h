@@ -397,6 +397,8 @@ int swim_debug_sends(swim_handle* h, uint64_t* out2n, uint32_t n);
  * 5 sync_ack, 6 sync_snapshot, 7 bookkeeping, 8 gossip_select, 9 gossip_inhist, 10 gossip_pairwin
  * (fill + prune), 11 gossip_record. Returns accumulated time since the last reset. */
 int swim_kernel_time(swim_handle* h, uint32_t idx, double* ms, uint64_t* launches);
+/* enable: 0 = off, 1 = every class, otherwise a mask of (1 << class) bits: only those launches are
+ * bracketed by events (each event pair costs the stream a few microseconds). */
 int swim_kernel_time_reset(swim_handle* h, int enable);
 
 #ifdef __cplusplus

@@ -85,6 +85,7 @@ struct swim_handle {
   std::string err;
   // timing
   bool timing = false;
+  uint32_t tmask = ~0u;  // kernel classes bracketed by HIP events while timing
   std::vector<hipEvent_t> pool;
   struct Pending {
     int cls;
@@ -182,7 +183,7 @@ bool debug_sync() {
 
 template <typename F>
 void timed(swim_handle* h, int cls, const char* name, F&& launch) {
-  if (!h->timing) {
+  if (!h->timing || !((h->tmask >> cls) & 1u)) {
     launch();
   } else {
     hipEvent_t a = take_event(h), b = take_event(h);
@@ -2188,6 +2189,7 @@ int swim_kernel_time_reset(swim_handle* h, int enable) {
     h->acc_n[i] = 0;
   }
   h->timing = enable != 0;
+  h->tmask = enable == 1 ? ~0u : (uint32_t)enable;  // (a class mask: only those launches get events)
   return SWIM_OK;
 }
 

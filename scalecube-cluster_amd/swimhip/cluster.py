@@ -336,8 +336,14 @@ class SwimCluster:
     def sync(self):
         self._call("sync", self._h)
 
-    def kernel_timing(self, enable: bool):
-        self._call("kernel_time_reset", self._h, 1 if enable else 0)
+    def kernel_timing(self, enable: bool, classes=None):
+        """Reset the per-class device times; with `classes` (names of KERNEL_CLASSES) only those
+        launches are bracketed by HIP events."""
+        mask = 1 if enable else 0
+        if enable and classes:
+            mask = sum(1 << self.KERNEL_CLASSES.index(c) for c in classes)
+            mask = mask if mask != 1 else 1 | (1 << 30)  # (class 0 alone: not the "every class" value)
+        self._call("kernel_time_reset", self._h, mask)
 
     def kernel_times(self) -> dict:
         """{kernel class: (total device ms, launches)} since the last kernel_timing() reset."""
