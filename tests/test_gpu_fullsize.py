@@ -133,10 +133,10 @@ def test_c2_convergence_tail_is_fd_driven():
 
 @pytest.mark.parametrize("workload,min_gossips", [("c5s", 100_000), ("c5g", 1_000)])
 def test_c5_shapes_fullsize_properties(workload, min_gossips):
-    """C5 (BASELINE configs[4]: 2^20 members, N x K views with K = 256, LAN defaults, 256 concurrent
-    crashes, the suspicion-timeout sweep) as stated, on one GPU with 4-bit infection rounds (the
-    8-bit ones would be 2^18 slots x 2^20 members = 256 GiB), plus its two round-3
-    shapes: the full churn at 262,144 members and the full size with 8 crashes. The SYNC re-spread
+    """C5's two one-GPU shapes (BASELINE configs[4] is 2^20 members, N x K views with K = 256, LAN
+    defaults, 256 concurrent crashes, the suspicion-timeout sweep; as stated it needs the 8-GPU node,
+    DESIGN.md §6.4): the full churn at 262,144 members (c5s) and the full size, 2^20 members, with 8
+    crashes (c5g). Neither is C5 as stated, whose storm outgrows any ring one GPU holds. The SYNC re-spread
     storm (each accepted SUSPECT record re-gossiped, MembershipProtocolImpl.java:649-656) is held by
     gossip batches. After 120 periods every crashed member is gone from every
     alive view (suspicion timeout 95 / 105 periods), no alive member was removed, no buffer
