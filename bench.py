@@ -541,7 +541,16 @@ def main():
     }
     c.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N = 1 figure
-        out["cpu_baseline"] = cpu_baseline(args.workload, args.warmup, args.cpu_budget, args.seed, args.steps)
+        cb = out["cpu_baseline"] = cpu_baseline(args.workload, args.warmup, args.cpu_budget, args.seed, args.steps)
+        # The comparison: the CPU sample runs a smaller cluster of the same schedule (the full-size storm
+        # does not fit the oracle's host tables), and a storm's work per member-period grows with N, so
+        # member-periods/s of the two are not the same unit of work; first gossip receipts (one
+        # onGossipReq of a new gossip id each, GossipProtocolImpl.java:171-183) are
+        if cb and cb.get("value") and cb.get("gossip_first_receipts_per_s"):
+            out["vs_cpu"] = {"basis": "gossip first receipts per second (work-normalised: the CPU sample's cluster "
+                                      "is smaller, and per-member-period work grows with N)",
+                             "ratio": out["rates"]["gossip_first_receipts_per_s"] / cb["gossip_first_receipts_per_s"],
+                             "member_periods_ratio_not_comparable": out["value"] / cb["value"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
