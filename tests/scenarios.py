@@ -53,6 +53,21 @@ def _lan_loss(c, n_crash, periods, loss, t0=5):
         yield
 
 
+def _c3_half(c, t0, length, after, crash_frac=0.10):
+    """SURVEY §8(d)'s C3 partition as written: a simultaneous crash of `crash_frac` of the members
+    and a half/half cut by id parity for `length` periods from t0, healed by SYNC (every accepted
+    SUSPECT record re-spread, MembershipProtocolImpl.java:649-656), bench.py's c3half schedule."""
+    import bench
+
+    c.step(t0)
+    yield
+    c.crash(bench.crash_set(c.n, crash_frac, c.seed))
+    c.partition((np.arange(c.n) % 2).astype(np.uint8), t0, t0 + length)
+    for _ in range(length + after):
+        c.step(1)
+        yield
+
+
 def _partition_heal(c, t_part, length, after):
     g = (np.arange(c.n) % 2).astype(np.uint8)
     c.partition(g, t_part, t_part + length)
@@ -242,6 +257,9 @@ SCENARIOS = {
 
 # Larger shapes, run only where their cost is the point (sharded rehearsals of BASELINE configs)
 SCENARIOS_EXTRA = {
+    # the C3 half/half heal at 1,024 members: ~4.96e5 gossips re-spread in the heal's first periods
+    # (the oracle needs ~2 minutes)
+    "c3half1024": (ClusterConfig.defaultLanConfig(), 1024, 3, lambda c: _c3_half(c, 3, 40, 20)),
     # C4's schedule shape (BASELINE configs[3]: LAN defaults, 1 % loss, 0.1 % simultaneous crash)
     # at 4,096 members
     "lan4096_c4_shape": (ClusterConfig.defaultLanConfig(), 4096, 13, lambda c: _lan_loss(c, 4, 16, 1.0, t0=3)),

@@ -351,6 +351,16 @@ def test_refused_set_delay_leaves_the_handle_unchanged():
         assert [e.key() for e in a.events()] == [e.key() for e in b.events()]
 
 
+def test_c3_half_partition_1024_matches_oracle():
+    """SURVEY §8(d)'s C3 partition as written (10 % crash, half/half cut by id parity for 40 periods,
+    healed by SYNC) at 1,024 members against the oracle: on heal every SYNC / SYNC_ACK re-spreads each
+    accepted SUSPECT record (MembershipProtocolImpl.java:649-656), ~5e5 gossips in batch slots whose
+    records merge through the record dictionary and the merge marks. Events, counters and digests
+    every 5 periods through the heal and the first suspicion timeouts."""
+    scenarios.run_pair("c3half1024", SwimCluster, OracleCluster, compare_every=5, full_tables=False,
+                       event_capacity=1 << 22)
+
+
 # The sharded rehearsals' shapes of BASELINE configs 3 and 4 (tests/test_sharded.py compares their
 # shards with the unsharded handle), pinned to the oracle here: C4's schedule (1 % loss, 0.1 % crash,
 # LAN; one gossip per slot) and C5's (64 concurrent crashes, no loss, gossip batches, past the first
