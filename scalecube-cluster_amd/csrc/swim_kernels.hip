@@ -3033,15 +3033,40 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     // with set bits of 512 bitmap words are flattened across the wave (one block per lane: its
     // eight entry records in two 16-B loads beside its subject), then the words are cleared.
     static_assert(DICT_WAYS == 8, "a bitmap byte per block");
+    // The merge marks are read with the bitmap words (a lane's word covers 4 blocks: their 4 marks
+    // and generations are one 16-B load each, consecutive lanes consecutive lines), so the blocks whose set entries are all marked drop out before the per-block pass.
+    const uint4* mrow4 = reinterpret_cast<const uint4*>(mrow);
+    const uint4* gen4 = reinterpret_cast<const uint4*>(P.d_gen);
     for (uint32_t t0 = 0; t0 < bw; t0 += 512u) {
-      uint32_t bm = 0u;  // bit 4u + j: word t0 + 64u + lane has set entries in its block j
+      uint32_t bm = 0u;   // bit 4u + j: word t0 + 64u + lane has set entries in its block j, not all marked
+      uint32_t nzw = 0u;  // bit u: word t0 + 64u + lane has set entries
 #pragma unroll
-      for (uint32_t u = 0; u < 8u; ++u) {
-        const uint32_t t = t0 + 64u * u + lane;
-        const uint32_t w = t < bw ? s_bm[t] : 0u;
-        const uint32_t nz = (uint32_t)((w & 0xFFu) != 0u) | ((uint32_t)((w & 0xFF00u) != 0u) << 1) |
-                            ((uint32_t)((w & 0xFF0000u) != 0u) << 2) | ((uint32_t)((w >> 24) != 0u) << 3);
-        bm |= nz << (4u * u);
+      for (uint32_t h2 = 0; h2 < 4u; ++h2) {  // (two words in flight per step: registers)
+        uint32_t wv[2];
+        uint4 mv[2], gv[2];
+#pragma unroll
+        for (uint32_t uu = 0; uu < 2u; ++uu) {
+          const uint32_t t = t0 + 64u * (2u * h2 + uu) + lane;
+          wv[uu] = t < bw ? s_bm[t] : 0u;
+          mv[uu] = wv[uu] ? mrow4[t] : make_uint4(0u, 0u, 0u, 0u);
+          gv[uu] = wv[uu] ? gen4[t] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t uu = 0; uu < 2u; ++uu) {
+          const uint32_t u = 2u * h2 + uu;
+          if (wv[uu]) nzw |= 1u << u;
+          const uint32_t mk[4] = {mv[uu].x, mv[uu].y, mv[uu].z, mv[uu].w};
+          const uint32_t gg[4] = {gv[uu].x, gv[uu].y, gv[uu].z, gv[uu].w};
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t m = (wv[uu] >> (8u * j)) & 0xFFu;
+            if (!m) continue;
+            if ((mk[j] >> 8) == (gg[j] & GEN_MASK) && (m & ~mk[j] & 0xFFu) == 0u)
+              ++nskip;  // every set entry already found not to override the present cell (MPI:489)
+            else
+              bm |= 1u << (4u * u + j);
+          }
+        }
       }
       uint32_t tot;
       const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
@@ -3055,34 +3080,28 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
           const uint32_t sid = base / DICT_WAYS;
           const uint32_t m = (s_bm[t] >> (8u * j)) & 0xFFu;
-          // the merge mark (every load of the block in flight at once): when every set entry is
-          // marked, none overrides the cell (MPI:489) and the cell is not read
           uint32_t* mkp = mrow + sid;
-          const uint32_t mk = *mkp, g = P.d_gen[sid] & GEN_MASK;
+          const uint32_t mk = *mkp, g = P.d_gen[sid] & GEN_MASK;  // (lines the scan just read)
           const uint4* dr = reinterpret_cast<const uint4*>(P.d_rec + base);
           const uint4 r0 = dr[0], r1 = dr[1];
           const uint32_t subj = P.d_subj[sid];
           const bool mvalid = (mk >> 8) == g;
-          if (mvalid && (m & ~mk & 0xFFu) == 0u) {
-            ++nskip;
+          uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
+                              max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
+          best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
+                               max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
+          if (any_none && (int32_t)(P.none_last[subj] - c_lo) > 0) {
+            spill(subj, best);
           } else {
-            uint32_t best = max(max((m & 1u) ? r0.x : 0u, (m & 2u) ? r0.y : 0u),
-                                max((m & 4u) ? r0.z : 0u, (m & 8u) ? r0.w : 0u));
-            best = max(best, max(max((m & 16u) ? r1.x : 0u, (m & 32u) ? r1.y : 0u),
-                                 max((m & 64u) ? r1.z : 0u, (m & 128u) ? r1.w : 0u)));
-            if (any_none && (int32_t)(P.none_last[subj] - c_lo) > 0) {
-              spill(subj, best);
+            const uint32_t c = cell_get(P, p, subj);
+            if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE)) {  // (the latter: OV_TRACK)
+              apply(subj, best);
             } else {
-              const uint32_t c = cell_get(P, p, subj);
-              if (is_overrides(best, c) || (P.nxk && P.colmap[subj] == NONE)) {  // (the latter: OV_TRACK)
-                apply(subj, best);
-              } else {
-                ++nsubj;
-                // no set entry overrides the present cell: mark them (an absent cell is not
-                // marked: a record that does not override it may override a re-added one)
-                const uint32_t nm = (g << 8) | (((mvalid ? mk : 0u) | m) & 0xFFu);
-                if (c != SWIM_ABSENT && nm != mk) *mkp = nm;
-              }
+              ++nsubj;
+              // no set entry overrides the present cell: mark them (an absent cell is not
+              // marked: a record that does not override it may override a re-added one)
+              const uint32_t nm = (g << 8) | (((mvalid ? mk : 0u) | m) & 0xFFu);
+              if (c != SWIM_ABSENT && nm != mk) *mkp = nm;
             }
           }
         }
@@ -3090,7 +3109,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       wsync();  // every lane has read its blocks' bits
 #pragma unroll
       for (uint32_t u = 0; u < 8u; ++u)
-        if ((bm >> (4u * u)) & 0xFu) s_bm[t0 + 64u * u + lane] = 0u;
+        if ((nzw >> u) & 1u) s_bm[t0 + 64u * u + lane] = 0u;
     }
     wsync();
     APPLYB_MARK(2);
