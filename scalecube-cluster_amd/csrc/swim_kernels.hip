@@ -1416,6 +1416,49 @@ __device__ __forceinline__ uint32_t wave_owner(uint32_t off, uint32_t q) {
 }
 
 // position of the k-th (0-based) set bit of m, k < popcount(m)
+__device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k);
+
+// OR of v over the 64 lanes (DPP row shifts and broadcasts, then lane 63; every lane must call)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= dpp_in<0x111, 0xF>(v);
+  v |= dpp_in<0x112, 0xF>(v);
+  v |= dpp_in<0x114, 0xF>(v);
+  v |= dpp_in<0x118, 0xF>(v);
+  v |= dpp_in<0x142, 0xA>(v);
+  v |= dpp_in<0x143, 0xC>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// wave_owner for a window of 64 items: lane x gets the owner of item q0 + x, where lane L owns items
+// [off_L, off_L + cnt_L) (off = the exclusive scan of cnt). Instead of six dependent lane shuffles
+// (LDS round trips), the VALU finds it: the lanes whose ranges meet the window (a ballot, in item
+// order), their clipped start positions (one 64-bit OR over the wave), and for item x the rank of the
+// last start at or before x among them. A lane whose item does not exist gets an arbitrary owner, as
+// with wave_owner (callers test q < total).
+#ifndef SWIM_OWNER_BALLOT
+#define SWIM_OWNER_BALLOT 1
+#endif
+__device__ __forceinline__ uint32_t wave_owner_at(uint32_t off, uint32_t cnt, uint32_t q0) {
+  const uint32_t lane = threadIdx.x & 63u;
+#if SWIM_OWNER_BALLOT
+  const bool meets = cnt != 0u && off < q0 + 64u && off + cnt > q0;
+  const unsigned long long lanes = __ballot(meets);
+  const uint32_t st = meets ? (off > q0 ? off - q0 : 0u) : 64u;
+  const uint32_t s_lo = wave_or(st < 32u ? (1u << st) : 0u);
+  const uint32_t s_hi = wave_or(st >= 32u && st < 64u ? (1u << (st - 32u)) : 0u);
+  const uint32_t below_lo = lane >= 31u ? s_lo : s_lo & ((2u << lane) - 1u);
+  const uint32_t below_hi = lane < 32u ? 0u : (lane == 63u ? s_hi : s_hi & ((2u << (lane - 32u)) - 1u));
+  const uint32_t r = (uint32_t)(__popc(below_lo) + __popc(below_hi));
+  if (r == 0u) return 0u;
+  const uint32_t l_lo = (uint32_t)lanes, l_hi = (uint32_t)(lanes >> 32);
+  const uint32_t c = (uint32_t)__popc(l_lo);
+  return (r - 1u) < c ? kth_set_bit(l_lo, r - 1u) : 32u + kth_set_bit(l_hi, r - 1u - c);
+#else
+  (void)cnt;
+  return wave_owner(off, q0 + lane);
+#endif
+}
+
 __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
   uint32_t pos = 0;
 #pragma unroll
@@ -1631,7 +1674,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
           const uint32_t q = q0 + lane;
-          const uint32_t o = wave_owner(off, q);
+          const uint32_t o = wave_owner_at(off, (uint32_t)__popc(mixm), q0);
           const uint32_t mo = __shfl(mixm, (int)o, 64), oo = __shfl(off, (int)o, 64);
           if (q < tot) {
             const uint32_t j = kth_set_bit(mo, q - oo);
@@ -2913,7 +2956,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       const uint32_t off = wave_excl_scan((uint32_t)__popc(rm), &tot);
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
-        const uint32_t o = wave_owner(off, q);
+        const uint32_t o = wave_owner_at(off, (uint32_t)__popc(rm), q0);
         const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(ws, (int)o, 64), oo = __shfl(off, (int)o, 64);
         uint2 cr = make_uint2(0u, 0u);
         if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
@@ -2974,7 +3017,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #pragma unroll
             for (uint32_t u = 0; u < AW_QILP; ++u) {
               const uint32_t ee = e0 + 64u * u + lane;
-              const uint32_t eo = wave_owner(qoff, ee);
+              const uint32_t eo = wave_owner_at(qoff, nq, e0 + 64u * u);
               // (every lane shuffles: a lane past qtot may own nothing yet be another lane's source)
               bx[u] = __shfl(cr.x, (int)eo, 64);
               const uint32_t lo = __shfl(len, (int)eo, 64), oo = __shfl(qoff, (int)eo, 64);
@@ -3004,7 +3047,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         const uint32_t off = wave_excl_scan((uint32_t)__popc(sb), &tot);
         for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
           const uint32_t q = q0 + lane;
-          const uint32_t o = wave_owner(off, q);
+          const uint32_t o = wave_owner_at(off, (uint32_t)__popc(sb), q0);
           const uint32_t bo = __shfl(sb, (int)o, 64), oo = __shfl(off, (int)o, 64);
           word(q < tot ? 32u * (c0 + o) + kth_set_bit(bo, q - oo) : NONE);
         }
@@ -3072,7 +3115,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
-        const uint32_t o = wave_owner(off, q);
+        const uint32_t o = wave_owner_at(off, (uint32_t)__popc(bm), q0);
         const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
         if (q < tot) {
           const uint32_t b = kth_set_bit(bo, q - oo);
