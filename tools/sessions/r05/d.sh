@@ -16,6 +16,9 @@ rc=$?; echo "c3 shfl rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_c2 -o run -- \
     python3 bench.py --workload c2 --steps 20 --warmup 5 --no-cpu-baseline --converge 0 > $out/prof_c2.json 2> $out/prof_c2.err
 rc=$?; echo "c2 prof rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_steady -o run -- \
+    python3 bench.py --workload steady65k --steps 30 --warmup 5 --no-cpu-baseline --converge 0 > $out/prof_steady.json 2> $out/prof_steady.err
+rc=$?; echo "steady prof rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest tests/test_c4_rehearsal.py -m gpu -x -v -s -p no:cacheprovider --timeout 540 --timeout-method thread \
    > $out/pytest_c4_rehearsal.log 2>&1
 rc=$?; echo "c4 rehearsal rc=$rc" >> $out/status.log; exit $rc
