@@ -80,6 +80,12 @@ int main() {
     check(oracle_spread(h, 0, 0xABCDu), "spread");
     const uint32_t upd[] = {3, 30};
     check(oracle_update_metadata(h, upd, 2), "update_metadata");
+    // a real node's SYNC and a forwarded membership gossip (the wire bridge)
+    const uint32_t subj[] = {2, 7, 11, 12}, recs[] = {SWIM_PACK(0, SWIM_SUSPECT), SWIM_PACK(2, SWIM_ALIVE), SWIM_DEAD,
+                                                      SWIM_PACK(1, SWIM_SUSPECT)};
+    check(oracle_deliver_records(h, 12, subj, recs, 4, SWIM_R_SYNC), "deliver_records sync");
+    check(oracle_deliver_records(h, 20, subj, recs, 2, SWIM_R_MEMBERSHIP_GOSSIP | SWIM_DELIVER_FORWARD),
+          "deliver_records forward");
     check(oracle_step(h, 6), "step");
     const uint32_t leave[] = {60};
     check(oracle_leave(h, leave, 1), "leave");
