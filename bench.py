@@ -139,13 +139,15 @@ def kernel_bytes(name, d, rounds_per_period=5):
         # run starts (4), infection rounds read-modify-write (32 + 32), liveness word (4), list entry (4).
         # One-gossip slots (k_gossip_apply): per subject run one ring record (8 B), per subject the
         # table cell and its deadline (8 B). Batch slots (k_gossip_apply_b):
-        # per run top its record range (8 B), per record its dictionary entry id (4 B), per block with
+        # per run top its record range (8 B), per record its dictionary entry id (2 B with at most
+        # 8,192 dictionary blocks, else 4: entry_id_bytes), per block with
         # received entries its merge mark and the block's generation (8 B), and per block merged (not
         # skipped by its mark) the entry's record, the block's subject and the table cell (12 B)
         recs = d.get("apply_records", 0)
         if recs:
             blocks = d["apply_subjects"] + d.get("apply_skipped", 0)
-            return 93 * d["apply_words"] + 8 * d["apply_runs"] + 4 * recs + 8 * blocks + 12 * d["apply_subjects"]
+            return (93 * d["apply_words"] + 8 * d["apply_runs"] + d.get("id_bytes", 4) * recs + 8 * blocks
+                    + 12 * d["apply_subjects"])
         return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
     if name == "k_susp_sweep":  # stream a u16 deadline column; per fired cell the deadline write, the
         # view cell read + write, and (a handle with an event ring) its 24-B REMOVED event
@@ -198,6 +200,12 @@ def pmc_traffic(kernel, workload="c3", world=1, steps=None, warmup=None):
         return None
     k = max(cands, key=lambda v: v.get("dispatches", 0))
     return k["fetch_bytes_x2"] + k["write_bytes"]
+
+
+def entry_id_bytes(w):
+    """Bytes of a record's dictionary entry id: 16 bits while the dictionary has at most 8,192 blocks
+    (the library's c_id16), else 32."""
+    return 2 if (w.get("dsub") or 8192) <= 8192 else 4
 
 
 def roofline_of(name, ktimes, d, world, rounds_per_period=5):
@@ -439,6 +447,7 @@ def main():
     ktimes = c.kernel_times()
     c.kernel_timing(False)
     d = {k: s1[k] - s0[k] for k in s1}
+    d["id_bytes"] = entry_id_bytes(w)
     n_events = c.discard_events() if ecap else 0  # (none expected: no timeout falls due in the window)
 
     # dominant kernel + roofline over the timed region

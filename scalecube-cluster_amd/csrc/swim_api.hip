@@ -22,6 +22,9 @@ using namespace swim;
 namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
+#ifndef SWIM_CID16
+#define SWIM_CID16 1
+#endif
 constexpr uint32_t DICT_GRID = 128;  // workgroups of the record-dictionary kernels (grid-stride)
 
 uint32_t pow2ceil(uint64_t v) {
@@ -553,7 +556,9 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject
           // runs it takes as run tops (C4's lossy storm: apply 373 -> 104 ms per 20 periods, §6.4)
           if (P.batched || h->dict_on)
-            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b, dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b),
+            hipLaunchKernelGGL(P.cid16 ? (P.hd4 ? k_gossip_apply_b16_h4 : k_gossip_apply_b16)
+                                       : (P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b),
+                               dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b),
                                h->apply_lds_b, s, P);
           else
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
@@ -965,7 +970,9 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     h->apply_blocks_b = (uint32_t)std::max(1, cus) * per_cu_b;
     for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply), reinterpret_cast<const void*>(&k_gossip_apply_h4)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
-    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b), reinterpret_cast<const void*>(&k_gossip_apply_b_h4)})
+    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b), reinterpret_cast<const void*>(&k_gossip_apply_b_h4),
+                          reinterpret_cast<const void*>(&k_gossip_apply_b16),
+                          reinterpret_cast<const void*>(&k_gossip_apply_b16_h4)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
@@ -1098,7 +1105,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.c_hash, h->CC);
   h->dict_on = c.gossip_batching == 0;
   if (h->dict_on) {
-    ALLOC(P.c_id, h->CC);
+    // 16-bit entry ids while every id (dict_subjects x 8 ways) and the two sentinels fit (SWIM_CID16=0: 32-bit)
+    P.cid16 = (SWIM_CID16 && P.dsids * DICT_WAYS <= 65536u) ? 1u : 0u;
+    if (P.cid16) {
+      ALLOC(P.c_id16, h->CC);
+    } else {
+      ALLOC(P.c_id, h->CC);
+    }
     ALLOC(P.sid_of, N);
     ALLOC(P.d_subj, P.dsids);
     ALLOC(P.d_rec, (size_t)P.dsids * DICT_WAYS);

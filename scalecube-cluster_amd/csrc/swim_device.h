@@ -271,6 +271,9 @@ struct KP {
   uint32_t* d_last;   // [dsids * DICT_WAYS] unwrapped index + 1 of the newest ring record naming the entry
   uint32_t* d_free;   // [dsids] stack of free blocks
   uint32_t* c_id;     // [CC] entry of each record-ring record; ID_USER, or ID_NONE (slow path)
+  uint16_t* c_id16;   // [CC] the same as 16-bit ids (cid16: dictionaries of <= 8,192 blocks; ID16_USER,
+                      // ID16_NONE): a 16-B load carries 8 records' entries instead of 4
+  uint32_t cid16;
   // Merge marks of the batched apply: per (local row, block) the entries whose
   // records the receiver already found not to override its (present) cell, tagged with the block's
   // generation: mark = gen24 << 8 | way mask. A block's generation moves whenever one of its entries
@@ -409,6 +412,8 @@ constexpr uint32_t DICT_IDS = DICT_SIDS * DICT_WAYS;
 constexpr uint32_t DICT_WORDS = DICT_IDS / 32u;  // a receiver's entry bitmap
 constexpr uint32_t ID_USER = 0xFFFFFFFEu;        // c_id of a user gossip (subject >= N)
 constexpr uint32_t ID_NONE = NONE;               // c_id of a record that found no entry
+constexpr uint32_t ID16_USER = 0xFFFEu, ID16_NONE = 0xFFFFu;  // their 16-bit forms (c_id16): entry ids of
+                                                               // 16-bit handles stay below 0xFFFE
 constexpr uint32_t DICT_LOCK = 0xFFFFFFFEu;      // sid_of while k_dict_claim allocates the block
 // sid_of of a subject whose claim found no block: DICT_NOBLK | (the commit's first record index &
 // DICT_TAG_MASK); a later commit may claim again (k_dict_claim). Never a block id (< 2^20).

@@ -741,7 +741,9 @@ __global__ void k_dict_entries(KP P) {
     } else {
       const uint32_t sid = P.sid_of[sr.x];
       if (sid < P.dsids) {
-        for (uint32_t k = 0; k < DICT_WAYS; ++k) {
+        // (16-bit ids: the two top ids of an 8,192-block dictionary are the sentinels, never entries)
+        const uint32_t ways = (P.cid16 && sid * DICT_WAYS + DICT_WAYS > ID16_USER) ? ID16_USER - sid * DICT_WAYS : DICT_WAYS;
+        for (uint32_t k = 0; k < ways; ++k) {
           uint32_t* e = &P.d_rec[sid * DICT_WAYS + k];
           uint32_t v = *e;
           if (v == 0u) v = atomicCAS(e, 0u, sr.y);
@@ -752,7 +754,10 @@ __global__ void k_dict_entries(KP P) {
         }
       }
     }
-    P.c_id[x & P.cmask] = id;
+    if (P.cid16)
+      P.c_id16[x & P.cmask] = (uint16_t)(id == ID_USER ? ID16_USER : (id == ID_NONE ? ID16_NONE : id));
+    else
+      P.c_id[x & P.cmask] = id;
     if (id < P.dsids * DICT_WAYS)
       atomicMax(&P.d_last[id], x + 1u);
     else if (id == ID_NONE) {
@@ -1436,7 +1441,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 // last start at or before x among them. A lane whose item does not exist gets an arbitrary owner, as
 // with wave_owner (callers test q < total).
 #ifndef SWIM_OWNER_BALLOT
-#define SWIM_OWNER_BALLOT 1
+#define SWIM_OWNER_BALLOT 0
 #endif
 __device__ __forceinline__ uint32_t wave_owner_at(uint32_t off, uint32_t cnt, uint32_t q0) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -2835,7 +2840,7 @@ static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range
 #ifndef SWIM_AW_MINW
 #define SWIM_AW_MINW 1
 #endif
-template <bool HD4>
+template <bool HD4, bool C16>
 __device__ __forceinline__ void apply_b_body(const KP& P) {
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
@@ -2847,6 +2852,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
   const uint32_t W32 = P.GC >> 5;
   const uint32_t bw = (min(P.ctl->d_hw, P.dsids) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
   const uint32_t dids = P.dsids * DICT_WAYS;
+  constexpr uint32_t IDG = C16 ? 8u : 4u;  // entry ids per 16-B load
   // a live record has no dictionary entry: the subjects of such records merge through the spill table
   // (their entry records too), so every subject is merged exactly once per round
   const uint32_t c_lo = live_rec_lo(P);
@@ -2909,7 +2915,16 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           rowscan = true;
       }
     };
-    // record-ring record x of a received run top
+    // entry ids of the record ring: IDG per 16-B load (4 of 32 bits, or 8 of 16 bits)
+    auto id_load = [&](uint32_t x) -> uint4 {
+      return C16 ? *reinterpret_cast<const uint4*>(P.c_id16 + (x & P.cmask))
+                 : *reinterpret_cast<const uint4*>(P.c_id + (x & P.cmask));
+    };
+    auto id_at = [&](const uint4& v, uint32_t k) -> uint32_t {
+      const uint32_t w = (k / (IDG / 4u)) == 0u ? v.x : (k / (IDG / 4u)) == 1u ? v.y : (k / (IDG / 4u)) == 2u ? v.z : v.w;
+      return C16 ? ((k & 1u) ? (w >> 16) : (w & 0xFFFFu)) : w;
+    };
+    // record-ring record x of a received run top (ids at or above dids: a user gossip or no entry)
     auto record = [&](uint32_t x, uint32_t id) {
       if (id < dids) {
         atomicOr(&s_bm[id >> 5], 1u << (id & 31u));
@@ -2977,38 +2992,37 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           }
         }
 #endif
-        // long ranges (batches): the whole wave walks each, 16-B quads of entry ids per lane
+        // long ranges (batches): the whole wave walks each, 16-B loads of entry ids per lane (4 ids,
+        // or 8 of 16 bits)
         unsigned long long big = __ballot(len >= AW_LONG);
         while (big) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
           const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
-          // aligned 16-B quads of entry ids from the quad holding b0: 4 records per lane per load
-          const uint32_t a0 = b0 & ~3u, span = b1 - a0;
-          for (uint32_t x0 = 0; x0 < span; x0 += 256u * AW_VILP) {
+          // aligned 16-B groups of entry ids from the group holding b0: IDG records per lane per load
+          const uint32_t a0 = b0 & ~(IDG - 1u), span = b1 - a0;
+          for (uint32_t x0 = 0; x0 < span; x0 += 64u * IDG * AW_VILP) {
             uint4 v[AW_VILP];
 #pragma unroll
             for (uint32_t u = 0; u < AW_VILP; ++u) {
-              const uint32_t d = x0 + 256u * u + 4u * lane;
-              v[u] = d < span ? *reinterpret_cast<const uint4*>(P.c_id + ((a0 + d) & P.cmask))
-                              : make_uint4(dids, dids, dids, dids);
+              const uint32_t d = x0 + 64u * IDG * u + IDG * lane;
+              v[u] = d < span ? id_load(a0 + d) : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < AW_VILP; ++u) {
-              const uint32_t x = a0 + x0 + 256u * u + 4u * lane;
-              const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+              const uint32_t x = a0 + x0 + 64u * IDG * u + IDG * lane;
 #pragma unroll
-              for (uint32_t k = 0; k < 4u; ++k)
-                if ((x + k - b0) < (b1 - b0)) record(x + k, ids[k]);
+              for (uint32_t k = 0; k < IDG; ++k)
+                if ((x + k - b0) < (b1 - b0)) record(x + k, id_at(v[u], k));
             }
           }
         }
         APPLYB_SUB(t_big);
-        // short ranges (single gossips, small batches): their aligned 16-B quads of entry ids
-        // flattened across the lanes, one quad per lane per load (one owner search per quad)
+        // short ranges (single gossips, small batches): their aligned 16-B groups of entry ids
+        // flattened across the lanes, one group per lane per load (one owner search per group)
         {
           const bool sh = len != 0u && len < AW_LONG;
-          const uint32_t nq = sh ? ((cr.x & 3u) + len + 3u) >> 2 : 0u;
+          const uint32_t nq = sh ? ((cr.x & (IDG - 1u)) + len + IDG - 1u) / IDG : 0u;
           uint32_t qtot;
           const uint32_t qoff = wave_excl_scan(nq, &qtot);
           for (uint32_t e0 = 0; e0 < qtot; e0 += 64u * AW_QILP) {
@@ -3022,16 +3036,14 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
               bx[u] = __shfl(cr.x, (int)eo, 64);
               const uint32_t lo = __shfl(len, (int)eo, 64), oo = __shfl(qoff, (int)eo, 64);
               bl[u] = ee < qtot ? lo : 0u;
-              qb[u] = (bx[u] & ~3u) + 4u * (ee - oo);
-              v[u] = ee < qtot ? *reinterpret_cast<const uint4*>(P.c_id + (qb[u] & P.cmask))
-                               : make_uint4(dids, dids, dids, dids);
+              qb[u] = (bx[u] & ~(IDG - 1u)) + IDG * (ee - oo);
+              v[u] = ee < qtot ? id_load(qb[u]) : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < AW_QILP; ++u) {
-              const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-              for (uint32_t k = 0; k < 4u; ++k)
-                if ((qb[u] + k - bx[u]) < bl[u]) record(qb[u] + k, ids[k]);
+              for (uint32_t k = 0; k < IDG; ++k)
+                if ((qb[u] + k - bx[u]) < bl[u]) record(qb[u] + k, id_at(v[u], k));
             }
           }
         }
@@ -3197,8 +3209,10 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #endif
   flush_tally(P, T);
 }
-__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(KP P) { apply_b_body<false>(P); }
-__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_h4(KP P) { apply_b_body<true>(P); }
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(KP P) { apply_b_body<false, false>(P); }
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_h4(KP P) { apply_b_body<true, false>(P); }
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16(KP P) { apply_b_body<false, true>(P); }
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_h4(KP P) { apply_b_body<true, true>(P); }
 
 // hd4 handles, once a period: escape entries whose slot the row no longer holds with nibble 15
 // (swept, or rewritten with a small offset) become tombstones, so the table holds only live escapes

@@ -351,13 +351,18 @@ def test_refused_set_delay_leaves_the_handle_unchanged():
         assert [e.key() for e in a.events()] == [e.key() for e in b.events()]
 
 
-def test_c3_half_partition_1024_matches_oracle():
+@pytest.mark.parametrize("dsub", [None, 16384], ids=["id16", "id32"])
+def test_c3_half_partition_1024_matches_oracle(dsub):
     """SURVEY §8(d)'s C3 partition as written (10 % crash, half/half cut by id parity for 40 periods,
     healed by SYNC) at 1,024 members against the oracle: on heal every SYNC / SYNC_ACK re-spreads each
     accepted SUSPECT record (MembershipProtocolImpl.java:649-656), ~5e5 gossips in batch slots whose
     records merge through the record dictionary and the merge marks. Events, counters and digests
-    every 5 periods through the heal and the first suspicion timeouts."""
-    scenarios.run_pair("c3half1024", SwimCluster, OracleCluster, compare_every=5, full_tables=False,
+    every 5 periods through the heal and the first suspicion timeouts. The default 8,192-block
+    dictionary names entries in 16 bits; a 16,384-block one (dict_subjects) in 32."""
+    def make(cfg, n, seed, **kw):
+        return SwimCluster(cfg, n, seed, **({"dict_subjects": dsub} if dsub else {}), **kw)
+
+    scenarios.run_pair("c3half1024", make, OracleCluster, compare_every=5, full_tables=False,
                        event_capacity=1 << 22)
 
 
