@@ -280,8 +280,11 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
   // here; a local stage is bounded by the phase (`bound`: a gossip round stages at most one
   // refutation per member, MPI:549-569; k_commit fails loudly if a bound is ever exceeded)
   const bool big = stg != nullptr ? bound > CS_SMALL : n > CS_SMALL;
-  C.radix = big ? 1u : 0u;
-  const uint32_t tiles = stg ? h->cs_maxt : std::max<uint32_t>(1, (n + CS_TILE - 1) / CS_TILE);
+  // radix grids of the tiles the bound allows (a gossip round: nloc / CS_TILE), not of the stage's
+  // capacity: launches that find a small batch return at once, and are cheaper the smaller they are
+  const uint32_t tiles = stg ? (bound == NONE ? h->cs_maxt : std::min(h->cs_maxt, blocks_for(bound, CS_TILE)))
+                             : std::max<uint32_t>(1, (n + CS_TILE - 1) / CS_TILE);
+  C.radix = big ? tiles : 0u;
   timed(h, 7, "k_commit", [&] {
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
     if (big) {
@@ -456,7 +459,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, "k_gossip_select", [&] {
-          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
         });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
@@ -541,14 +544,14 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(h->n_in_pairs, 256)), dim3(256), 0, s, P,
                                h->n_in_pairs);
         }
-        timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
+        timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P); });
         timed(h, 1, "k_gossip_pull", [&] {
           if (P.dq)
-            hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull_dq, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
           else if (P.loss_mode == 1u)  // the loss draws' instance (§3.16's split, for registers)
-            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
           else
-            hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
         });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
@@ -578,16 +581,13 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         break;
       case PC_SUSP:  // phase G+1: suspicion timeouts
         set_phase(h, P, G + 1);
-        memset_ctl_u32(h, offsetof(Ctl, due_count));
         timed(h, 7, "k_due", [&] { hipLaunchKernelGGL(k_due, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 3, "k_susp_sweep", [&] { hipLaunchKernelGGL(k_susp_sweep, dim3(2048), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         // phase G+2: SYNC requests
         set_phase(h, P, G + 2);
-        memset_ctl_u32(h, offsetof(Ctl, stage_count));
-        HIPC(h, hipMemsetAsync(P.ctl->xs_cnt, 0, sizeof(uint32_t) * SWIM_MAX_WORLD, s));
-        (void)hipMemsetAsync(P.recv_count, 0, (size_t)N * 4, s);
-        (void)hipMemsetAsync(P.recv_fill, 0, (size_t)N * 4, s);
+        // (stage_count, xs_cnt and the work-list counts were reset by k_due, recv_count / recv_fill
+        // by k_susp_sweep)
         if (P.tmode)  // the touched columns this period's SYNC payloads carry
           timed(h, 7, "k_tlist", [&] { hipLaunchKernelGGL(k_tlist, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 7, "k_sync_select", [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
@@ -633,7 +633,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         });
         if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         if (P.njoin) hipLaunchKernelGGL(k_join_scatter, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
-        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(std::min(nloc, SY_GRID)), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
         if (SH) {  // SYNC_ACK tables back to the requesters' shards, in the order received
@@ -655,7 +655,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(nloc), dim3(256), 0, s, P); });
+        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(std::min(nloc, SY_GRID)), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
@@ -1180,6 +1180,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
+  ALLOC(P.sy_mlist, NL);  // SYNC work lists (k_scan_apply / k_sync_select)
+  ALLOC(P.sy_alist, NL);
   {  // infectedFrom bookkeeping: in-history rings, delivery records, pruned pairs
     const uint64_t f = (uint64_t)c.gossip_fanout, W32 = h->GC / 32;
     // deliveries recorded per round: those whose receiver may select the sender within the

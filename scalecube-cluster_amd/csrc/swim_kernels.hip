@@ -382,7 +382,8 @@ struct CSort {
   uint32_t* ctr;    // [CS_MAXPASS] tiles handed out per pass
   uint32_t* stat;   // [CS_MAXPASS][maxt][256] look-back status: flag | count
   uint32_t maxt, npass;
-  uint32_t radix;   // 0: the host launched no radix kernels (the phase cannot stage > CS_SMALL)
+  uint32_t radix;   // tiles the host launched the radix kernels with (the phase's bound on its
+                    // gossips); 0: none (the phase cannot stage > CS_SMALL)
 };
 
 __device__ __forceinline__ uint32_t cs_n(const KP& P, const uint4* stg, uint32_t n_host) {
@@ -446,11 +447,11 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
   const uint32_t t = threadIdx.x;
   const uint32_t n = cs_n(P, stg, n_host);
   if (n > CS_SMALL) {  // a storm phase: reset the radix sort's counters for this batch
-    if (!C.radix) {  // the host's bound on this phase's gossips was wrong: fail loudly
+    const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
+    if (nt > C.radix) {  // the host's bound on this phase's gossips was wrong: fail loudly
       if (t == 0) atomicOr(&P.ctl->overflow, OV_BUG);
       return;
     }
-    const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
     for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) C.ghist[i] = 0u;
     if (t < CS_MAXPASS) C.ctr[t] = 0u;
     for (uint32_t p = 0; p < C.npass; ++p)
@@ -1479,7 +1480,7 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
 }
 
 template <bool HD4>
-__device__ __forceinline__ void select_body(const KP& P) {
+__device__ __forceinline__ void select_body(const KP& P, uint32_t mb) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
@@ -1488,7 +1489,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
-  const uint32_t m = P.row0 + blockIdx.x * 4u + w;
+  const uint32_t m = P.row0 + mb * 4u + w;
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
@@ -1874,8 +1875,20 @@ __device__ __forceinline__ void select_body(const KP& P) {
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
 }
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) { select_body<false>(P); }
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) { select_body<true>(P); }
+// The wave-per-member round kernels (select, inhist, pull) launch at most ROUND_GRID workgroups,
+// each walking member blocks of 4 at a grid stride: a round with nothing to gossip (the fault-free
+// steady state) costs a few microseconds instead of dispatching nloc / 4 workgroups (65,536
+// members: 16,384 workgroups, 27 + 10 + 17 us per round)
+#ifndef SWIM_ROUND_GRID
+#define SWIM_ROUND_GRID 4096
+#endif
+constexpr uint32_t ROUND_GRID = SWIM_ROUND_GRID;
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) select_body<false>(P, mb);
+}
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) select_body<true>(P, mb);
+}
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
 
@@ -2058,10 +2071,10 @@ __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
 // messages can reach p joins p's in-history (round, record); a delivery p may answer with gossips
 // of its own within the horizon (may_select on p's post-selection cursor) gets a record, which
 // k_gossip_record fills after k_gossip_pull (GossipState.addToInfected, GPI:181).
-__global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
+__device__ __forceinline__ void inhist_body(const KP& P, uint32_t mb) {
   SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t p = P.row0 + mb * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
   if (lane == 0) P.ih_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.ih_head[p];  // k_gossip_select's window
   const uint32_t deg = P.in_cnt[p];
@@ -2150,6 +2163,10 @@ __global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
   add_stat(P, ST_IF_RECORDS, nrec);
 }
 
+__global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) inhist_body(P, mb);
+}
+
 // One wave per receiver p: spreadGossipsTo (GossipProtocolImpl.java:215-251) seen from the
 // receiving side. Every sender that picked p sends each gossip of its start-of-round window as
 // one GossipRequest (:225-239); p adopts a gossip iff it does not hold it (onGossipReq :171-183).
@@ -2189,14 +2206,14 @@ constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a 
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
 // common instance keeps the one-at-a-time loop and 4 waves per SIMD).
 template <bool DQ, bool LOSS>
-__device__ __forceinline__ void pull_body(const KP& P) {
+__device__ __forceinline__ void pull_body(const KP& P, uint32_t mb) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t p = P.row0 + mb * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
@@ -2465,14 +2482,20 @@ __device__ __forceinline__ void pull_body(const KP& P) {
   add_stat(P, ST_G_PULLW, words);
 }
 
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<false, false>(P, mb);
+}
 // the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
 // per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
 #ifndef SWIM_PULL_LOSS_WAVES
 #define SWIM_PULL_LOSS_WAVES 6
 #endif
-__global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) { pull_body<false, true>(P); }
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true, true>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<false, true>(P, mb);
+}
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) {
+  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<true, true>(P, mb);
+}
 
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
@@ -2853,6 +2876,8 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
   const uint32_t bw = (min(P.ctl->d_hw, P.dsids) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
   const uint32_t dids = P.dsids * DICT_WAYS;
   constexpr uint32_t IDG = C16 ? 8u : 4u;  // entry ids per 16-B load
+  // ids at or above dlim are no entry (16 bits: the two sentinels top an 8,192-block dictionary)
+  const uint32_t dlim = C16 ? min(dids, ID16_USER) : dids;
   // a live record has no dictionary entry: the subjects of such records merge through the spill table
   // (their entry records too), so every subject is merged exactly once per round
   const uint32_t c_lo = live_rec_lo(P);
@@ -2924,9 +2949,9 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       const uint32_t w = (k / (IDG / 4u)) == 0u ? v.x : (k / (IDG / 4u)) == 1u ? v.y : (k / (IDG / 4u)) == 2u ? v.z : v.w;
       return C16 ? ((k & 1u) ? (w >> 16) : (w & 0xFFFFu)) : w;
     };
-    // record-ring record x of a received run top (ids at or above dids: a user gossip or no entry)
+    // record-ring record x of a received run top (ids at or above dlim: a user gossip or no entry)
     auto record = [&](uint32_t x, uint32_t id) {
-      if (id < dids) {
+      if (id < dlim) {
         atomicOr(&s_bm[id >> 5], 1u << (id & 31u));
         return;
       }
@@ -3501,6 +3526,12 @@ __global__ void __launch_bounds__(1024) k_due(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds[16];
   const uint32_t nc = ncells(P);
+  if (threadIdx.x == 0) {  // this period's SYNC counters (k_sync_select on), in place of host memsets
+    P.ctl->stage_count = 0u;
+    P.ctl->sy_mn = 0u;
+    P.ctl->sy_an = 0u;
+  }
+  if (threadIdx.x < SWIM_MAX_WORLD) P.ctl->xs_cnt[threadIdx.x] = 0u;
   uint32_t base = 0;
   for (uint32_t j0 = 0; j0 < nc; j0 += 65536u) {
     const uint32_t c0 = j0 + 64u * threadIdx.x;
@@ -3555,6 +3586,11 @@ __global__ void __launch_bounds__(256) k_susp_sweep(KP P) {
   uint32_t fired = 0;
   const uint32_t n = P.ctl->due_count, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t nob = (P.nloc + 255u) / 256u, ncb = (n + SW_COLS - 1u) / SW_COLS;
+  // the SYNC phase's per-receiver request counts start from zero (in place of two host memsets)
+  for (uint32_t i = blockIdx.x * 256u + tid; i < P.N; i += gridDim.x * 256u) {
+    P.recv_count[i] = 0u;
+    P.recv_fill[i] = 0u;
+  }
   for (uint32_t u = blockIdx.x; u < nob * ncb; u += gridDim.x) {
     const uint32_t ob = u % nob, c0 = (u / nob) * SW_COLS;  // neighbouring workgroups: neighbouring observers
     const uint32_t nc = min(SW_COLS, n - c0);
@@ -3758,6 +3794,9 @@ __global__ void k_sync_select(KP P) {
       }
     }
   }
+  // k_sync_ack's work: the requesters with a staged (or remote) request
+  const bool req = i < P.row0 + P.nloc && (P.req_stage[2 * i] != NONE || P.req_stage[2 * i + 1] != NONE);
+  wave_push(&P.ctl->sy_an, P.sy_alist, req, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -3794,6 +3833,11 @@ __global__ void k_join_select(KP P) {
       if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
     }
   }
+  // a local joiner whose initial SYNC_ACK comes back takes k_sync_ack's work list too (once: not
+  // if k_sync_select listed it for a request of its own)
+  const bool jack = i >= P.row0 && i < P.row0 + P.nloc && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap &&
+                    P.req_stage[2 * i] == NONE && P.req_stage[2 * i + 1] == NONE;
+  wave_push(&P.ctl->sy_an, P.sy_alist, jack, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -3901,6 +3945,10 @@ __global__ void __launch_bounds__(1024) k_scan_apply(KP P, const uint32_t* tbase
       run += v[k];
     }
   if (blockIdx.x == ntiles - 1u && threadIdx.x == 0) P.recv_off[P.N] = tbase[blockIdx.x] + tot;
+  // k_sync_merge's work: the local receivers with requests
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k)
+    wave_push(&P.ctl->sy_mn, P.sy_mlist, v[k] != 0u && b + k >= P.row0 && b + k < P.row0 + P.nloc, b + k);
 }
 
 __global__ void k_sync_scatter(KP P) {
@@ -4035,12 +4083,11 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
 #endif
-__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
-  SWIM_GUARD(P);
-  __shared__ uint32_t s_list[BUCKET_MAX];
-  __shared__ uint32_t s_lds4[4];
-  const uint32_t j = P.row0 + blockIdx.x;
-  if (j >= P.row0 + P.nloc) return;
+// A workgroup per listed receiver (sy_mlist, built by k_scan_apply), over a grid of at most SY_GRID
+// workgroups: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups took
+// 29 us of the fault-free period when ~1,800 had requests)
+constexpr uint32_t SY_GRID = 2048;
+__device__ __forceinline__ void sync_merge_one(const KP& P, uint32_t j, uint32_t* s_list, uint32_t* s_lds4) {
   uint32_t cntj = P.recv_count[j];
   if (cntj == 0u) return;
   if (cntj > (uint32_t)BUCKET_MAX) {
@@ -4099,12 +4146,19 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
   flush_tally(P, T);
 }
 
-// onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
-__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
+__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
   SWIM_GUARD(P);
+  __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
-  const uint32_t i = P.row0 + blockIdx.x;
-  if (i >= P.row0 + P.nloc) return;
+  const uint32_t n = P.ctl->sy_mn;
+  for (uint32_t u = blockIdx.x; u < n; u += gridDim.x) {
+    sync_merge_one(P, P.sy_mlist[u], s_list, s_lds4);
+    __syncthreads();  // (s_list is refilled for the next receiver)
+  }
+}
+
+// onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
+__device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* s_lds4) {
   uint32_t kd[3], to[3], n = 0;  // kind 0 / 1: request 2i + kind; kind 2: the initial SYNC's first ack
   for (uint32_t k = 0; k < 2; ++k) {
     const uint32_t qq = 2 * i + k;
@@ -4153,6 +4207,17 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
   add_stat(P, ST_ACK_CELLS, threadIdx.x == 0 ? n * sync_cells(P) : 0u);
   add_stat(P, ST_GOSSIPS_CREATED, created);
   flush_tally(P, T);
+}
+
+// A workgroup per listed requester (sy_alist: k_sync_select, k_join_select), SY_GRID at most
+__global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
+  SWIM_GUARD(P);
+  __shared__ uint32_t s_lds4[4];
+  const uint32_t n = P.ctl->sy_an;
+  for (uint32_t u = blockIdx.x; u < n; u += gridDim.x) {
+    sync_ack_one(P, P.sy_alist[u], s_lds4);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------
