@@ -567,7 +567,6 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
                                h->apply_lds, s, P);
         });
-        timed(h, 7, "k_spill_clear", [&] { hipLaunchKernelGGL(k_spill_clear, dim3(64), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         if (h->n_leaving) hipLaunchKernelGGL(k_leave_stop, dim3(gL), dim3(256), 0, s, P);
         h->pc = PC_R_C;

@@ -134,7 +134,7 @@ struct Ctl {
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
-  uint32_t sp_n;        // spill-table slots claimed this round (sp_used), reset by k_finalize
+  uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
   uint32_t sy_mn;       // this period's SYNC receivers (sy_mlist, k_scan_apply) and requesters
   uint32_t sy_an;       // awaiting a SYNC_ACK (sy_alist, k_sync_select / k_join_select); reset by k_due

@@ -37,18 +37,16 @@ __global__ void k_fill_u32(uint32_t* p, size_t n, uint32_t v) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-// the spill-table slots the round's apply claimed become empty again (k_finalize then resets the count)
-__global__ void k_spill_clear(KP P) {
-  const uint32_t n = min(P.ctl->sp_n, P.spmask + 1u);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const uint32_t hs = P.sp_used[t];
-    P.sp_key[hs] = 0ull;
-    P.sp_val[hs] = 0u;
-  }
-}
-
 __global__ void k_finalize(KP P) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) P.ctl->sp_n = 0u;  // (k_spill_clear ran before, if at all)
+  {  // the spill-table slots the round's apply claimed become empty again (the next round's
+     // k_gossip_prep resets their count: the finalizes of later phases clear nothing new)
+    const uint32_t n = min(P.ctl->sp_n, P.spmask + 1u);
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+      const uint32_t hs = P.sp_used[t];
+      P.sp_key[hs] = 0ull;
+      P.sp_val[hs] = 0u;
+    }
+  }
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P.row0 + P.nloc) {
@@ -1264,6 +1262,7 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
   __shared__ uint32_t s_lo, s_hi, s_blo, s_bhi, s_first;
   __shared__ uint32_t s_part[16];
   Ctl* c = P.ctl;
+  if (threadIdx.x == 0) c->sp_n = 0u;  // the last round's spill slots were cleared by its k_finalize
   if (c->overflow) {  // the run has failed (reported at the next swim_sync): list nothing, touch nothing
     if (threadIdx.x == 0) {
       c->n_act = 0;
