@@ -459,7 +459,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, "k_gossip_select", [&] {
-          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
+          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
         });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
@@ -544,14 +544,14 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(k_gossip_unpack, dim3(blocks_for(h->n_in_pairs, 256)), dim3(256), 0, s, P,
                                h->n_in_pairs);
         }
-        timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P); });
+        timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 1, "k_gossip_pull", [&] {
           if (P.dq)
-            hipLaunchKernelGGL(k_gossip_pull_dq, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
           else if (P.loss_mode == 1u)  // the loss draws' instance (§3.16's split, for registers)
-            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
           else
-            hipLaunchKernelGGL(k_gossip_pull, dim3(std::min(blocks_for(nloc, 4), ROUND_GRID)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
         });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
@@ -1179,7 +1179,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
-  ALLOC(P.sy_mlist, NL);  // SYNC work lists (k_scan_apply / k_sync_select)
+  ALLOC(P.sy_mlist, NL);  // SYNC work lists (recv_one / k_sync_select)
   ALLOC(P.sy_alist, NL);
   {  // infectedFrom bookkeeping: in-history rings, delivery records, pruned pairs
     const uint64_t f = (uint64_t)c.gossip_fanout, W32 = h->GC / 32;

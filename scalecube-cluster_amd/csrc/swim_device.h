@@ -136,7 +136,7 @@ struct Ctl {
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
-  uint32_t sy_mn;       // this period's SYNC receivers (sy_mlist, k_scan_apply) and requesters
+  uint32_t sy_mn;       // this period's SYNC receivers (sy_mlist, recv_one) and requesters
   uint32_t sy_an;       // awaiting a SYNC_ACK (sy_alist, k_sync_select / k_join_select); reset by k_due
 };
 
@@ -313,7 +313,7 @@ struct KP {
   uint32_t* recv_off;   // [N+1]
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
-  uint32_t* sy_mlist;   // [nloc] local receivers of this period's SYNCs (k_sync_merge's work list)
+  uint32_t* sy_mlist;   // [nloc] local receivers of this period's SYNCs (k_sync_merge's work list, recv_one)
   uint32_t* sy_alist;   // [nloc] local requesters that may take a SYNC_ACK (k_sync_ack's work list)
   uint4* stg;         // [stg_cap] gossips created since the last commit: origin, subject, record, id hash
   uint32_t stg_cap;
@@ -1003,6 +1003,11 @@ __device__ __forceinline__ void wave_push(uint32_t* cnt, uint32_t* list, bool pr
   if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(b));
   base = (uint32_t)__shfl((int)base, (int)leader, 64);
   if (pred) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = v;
+}
+
+// one more SYNC request for local receiver j: the first one lists j for k_sync_merge (sy_mlist)
+__device__ __forceinline__ void recv_one(const KP& P, uint32_t j) {
+  if (atomicAdd(&P.recv_count[j], 1u) == 0u) P.sy_mlist[atomicAdd(&P.ctl->sy_mn, 1u)] = j;
 }
 
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {

@@ -1479,7 +1479,7 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
 }
 
 template <bool HD4>
-__device__ __forceinline__ void select_body(const KP& P, uint32_t mb) {
+__device__ __forceinline__ void select_body(const KP& P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
@@ -1488,10 +1488,20 @@ __device__ __forceinline__ void select_body(const KP& P, uint32_t mb) {
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
-  const uint32_t m = P.row0 + mb * 4u + w;
+  const uint32_t m = P.row0 + blockIdx.x * 4u + w;
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
+  if (lo >= hi) {  // no live gossip anywhere (a quiet round): nothing is held, sent or swept
+    if (lane == 0 && m < P.row0 + P.nloc) P.npeers[m] = 0u;
+    if (m == P.dbg_watch && lane == 0) {
+      uint32_t* L = P.dbg_log + (r & 255u) * 8u;
+      L[0] = r;
+      L[1] = L[2] = L[3] = 0u;
+      L[4] = L[5] = L[6] = NONE;
+    }
+    return;
+  }
 #ifdef SWIM_SEL_PROF  // per-wave phase wall clock (100 MHz), summed: dbg_log u64 [8..11]
   unsigned long long tp = wall_clock64();
 #define SEL_MARK(q)                                                                        \
@@ -1874,20 +1884,8 @@ __device__ __forceinline__ void select_body(const KP& P, uint32_t mb) {
   add_stat(P, ST_G_HDREAD, hdw);
   add_stat(P, ST_G_WINW, winw);
 }
-// The wave-per-member round kernels (select, inhist, pull) launch at most ROUND_GRID workgroups,
-// each walking member blocks of 4 at a grid stride: a round with nothing to gossip (the fault-free
-// steady state) costs a few microseconds instead of dispatching nloc / 4 workgroups (65,536
-// members: 16,384 workgroups, 27 + 10 + 17 us per round)
-#ifndef SWIM_ROUND_GRID
-#define SWIM_ROUND_GRID 4096
-#endif
-constexpr uint32_t ROUND_GRID = SWIM_ROUND_GRID;
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) select_body<false>(P, mb);
-}
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) select_body<true>(P, mb);
-}
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) { select_body<false>(P); }
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) { select_body<true>(P); }
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
 
@@ -2070,10 +2068,10 @@ __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
 // messages can reach p joins p's in-history (round, record); a delivery p may answer with gossips
 // of its own within the horizon (may_select on p's post-selection cursor) gets a record, which
 // k_gossip_record fills after k_gossip_pull (GossipState.addToInfected, GPI:181).
-__device__ __forceinline__ void inhist_body(const KP& P, uint32_t mb) {
+__global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
   SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = P.row0 + mb * 4u + (threadIdx.x >> 6);
+  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
   if (lane == 0) P.ih_rhead[lrow(P, p) * 256u + (P.round & 255u)] = P.ih_head[p];  // k_gossip_select's window
   const uint32_t deg = P.in_cnt[p];
@@ -2162,10 +2160,6 @@ __device__ __forceinline__ void inhist_body(const KP& P, uint32_t mb) {
   add_stat(P, ST_IF_RECORDS, nrec);
 }
 
-__global__ void __launch_bounds__(256) k_gossip_inhist(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) inhist_body(P, mb);
-}
-
 // One wave per receiver p: spreadGossipsTo (GossipProtocolImpl.java:215-251) seen from the
 // receiving side. Every sender that picked p sends each gossip of its start-of-round window as
 // one GossipRequest (:225-239); p adopts a gossip iff it does not hold it (onGossipReq :171-183).
@@ -2205,14 +2199,14 @@ constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a 
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
 // common instance keeps the one-at-a-time loop and 4 waves per SIMD).
 template <bool DQ, bool LOSS>
-__device__ __forceinline__ void pull_body(const KP& P, uint32_t mb) {
+__device__ __forceinline__ void pull_body(const KP& P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = P.row0 + mb * 4u + (threadIdx.x >> 6);
+  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
   if (p >= P.row0 + P.nloc) return;  // whole wave
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
@@ -2481,20 +2475,16 @@ __device__ __forceinline__ void pull_body(const KP& P, uint32_t mb) {
   add_stat(P, ST_G_PULLW, words);
 }
 
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<false, false>(P, mb);
-}
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
 // the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
 // per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
 #ifndef SWIM_PULL_LOSS_WAVES
 #define SWIM_PULL_LOSS_WAVES 6
 #endif
 __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<false, true>(P, mb);
+  pull_body<false, true>(P);
 }
-__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) {
-  for (uint32_t mb = blockIdx.x; mb * 4u < P.nloc; mb += gridDim.x) pull_body<true, true>(P, mb);
-}
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true, true>(P); }
 
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
@@ -3450,7 +3440,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     P.rs_ref[rec[0]] = g;
-    atomicAdd(&P.recv_count[rec[1]], 1u);
+    recv_one(P, rec[1]);
   }
 }
 
@@ -3789,7 +3779,7 @@ __global__ void k_sync_select(KP P) {
         }
         P.req_stage[2 * i + k] = slot;
         P.stage_req[slot] = 2 * i + k;
-        atomicAdd(&P.recv_count[to[k]], 1u);
+        recv_one(P, to[k]);
       }
     }
   }
@@ -3828,7 +3818,7 @@ __global__ void k_join_select(KP P) {
         P.jslot[i] = slot;
       }
       const uint32_t rcv = route(P, s);
-      atomicAdd(&P.recv_count[rcv], 1u);
+      recv_one(P, rcv);
       if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
     }
   }
@@ -3944,10 +3934,6 @@ __global__ void __launch_bounds__(1024) k_scan_apply(KP P, const uint32_t* tbase
       run += v[k];
     }
   if (blockIdx.x == ntiles - 1u && threadIdx.x == 0) P.recv_off[P.N] = tbase[blockIdx.x] + tot;
-  // k_sync_merge's work: the local receivers with requests
-#pragma unroll
-  for (uint32_t k = 0; k < 4u; ++k)
-    wave_push(&P.ctl->sy_mn, P.sy_mlist, v[k] != 0u && b + k >= P.row0 && b + k < P.row0 + P.nloc, b + k);
 }
 
 __global__ void k_sync_scatter(KP P) {
@@ -4082,7 +4068,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
 #endif
-// A workgroup per listed receiver (sy_mlist, built by k_scan_apply), over a grid of at most SY_GRID
+// A workgroup per listed receiver (sy_mlist, built by recv_one), over a grid of at most SY_GRID
 // workgroups: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups took
 // 29 us of the fault-free period when ~1,800 had requests)
 constexpr uint32_t SY_GRID = 2048;
