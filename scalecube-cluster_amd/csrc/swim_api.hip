@@ -25,6 +25,12 @@ constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 #ifndef SWIM_CID16
 #define SWIM_CID16 1
 #endif
+#ifndef SWIM_RS_FUSE
+#define SWIM_RS_FUSE 1  // the radix chain in one launch where its grid allows (k_rs_fused)
+#endif
+#ifndef SWIM_RS_FUSE_ALL
+#define SWIM_RS_FUSE_ALL 0  // (tests: every radix sort in one launch of CS_FUSE workgroups at most)
+#endif
 constexpr uint32_t DICT_GRID = 128;  // workgroups of the record-dictionary kernels (grid-stride)
 
 uint32_t pow2ceil(uint64_t v) {
@@ -287,7 +293,9 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
   C.radix = big ? tiles : 0u;
   timed(h, 7, "k_commit", [&] {
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
-    if (big) {
+    if (big && SWIM_RS_FUSE && (tiles <= CS_FUSE || SWIM_RS_FUSE_ALL)) {
+      hipLaunchKernelGGL(k_rs_fused, dim3(std::min(tiles, CS_FUSE)), dim3(CS_THREADS), 0, s, P, stg, n, C);
+    } else if (big) {
       hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C);
       for (uint32_t p = 0; p < C.npass; ++p) {
         const bool even = (p & 1u) == 0u;
@@ -1151,7 +1159,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   }
   h->cs_maxt = (uint32_t)((P.stg_cap * (uint64_t)world + CS_TILE - 1) / CS_TILE);
   ALLOC(h->cs_ghist, CS_MAXPASS * 256);
-  ALLOC(h->cs_ctr, CS_MAXPASS);
+  ALLOC(h->cs_ctr, CS_MAXPASS + 1);
   ALLOC(h->cs_stat, (size_t)CS_MAXPASS * h->cs_maxt * 256);
   ALLOC(h->d_blx, 2);
   ALLOC(P.wlast, h->GC / 32);

@@ -377,7 +377,7 @@ constexpr uint32_t CS_AGG = 0x40000000u, CS_INC = 0x80000000u, CS_CNT = 0x3FFFFF
 struct CSort {
   unsigned long long *k0, *v0, *k1, *v1;  // ping-pong key / value buffers
   uint32_t* ghist;  // [CS_MAXPASS][256] digit counts of the whole batch per pass
-  uint32_t* ctr;    // [CS_MAXPASS] tiles handed out per pass
+  uint32_t* ctr;    // [CS_MAXPASS + 1] tiles handed out per pass; k_rs_fused's barrier count
   uint32_t* stat;   // [CS_MAXPASS][maxt][256] look-back status: flag | count
   uint32_t maxt, npass;
   uint32_t radix;   // tiles the host launched the radix kernels with (the phase's bound on its
@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
       return;
     }
     for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) C.ghist[i] = 0u;
-    if (t < CS_MAXPASS) C.ctr[t] = 0u;
+    if (t <= CS_MAXPASS) C.ctr[t] = 0u;  // tile counters per pass, then k_rs_fused's barrier
     for (uint32_t p = 0; p < C.npass; ++p)
       for (uint32_t i = t; i < nt * 256u; i += CS_THREADS) C.stat[(size_t)p * C.maxt * 256u + i] = 0u;
     return;
@@ -500,11 +500,12 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
 }
 
 // every pass's digit counts (a tile per workgroup); the stage moves into (k0, v0)
-__global__ void __launch_bounds__(CS_THREADS) k_rs_hist(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+__device__ __forceinline__ void rs_hist_tile(const KP& P, const uint4* stg, uint32_t n, const CSort& C, uint32_t tile) {
   __shared__ uint32_t s_h[CS_MAXPASS][256];
-  const uint32_t n = cs_n(P, stg, n_host), t = threadIdx.x;
-  const uint32_t base = blockIdx.x * CS_TILE;
-  if (n <= CS_SMALL || base >= n) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t base = tile * CS_TILE;
+  if (base >= n) return;
+  __syncthreads();  // (a fused loop's previous tile has read s_h)
   for (uint32_t i = t; i < CS_MAXPASS * 256u; i += CS_THREADS) (&s_h[0][0])[i] = 0u;
   __syncthreads();
   for (uint32_t q = 0; q < CS_PER; ++q) {
@@ -528,18 +529,22 @@ __global__ void __launch_bounds__(CS_THREADS) k_rs_hist(KP P, const uint4* stg, 
   }
 }
 
-__global__ void __launch_bounds__(CS_THREADS) k_rs_pass(KP P, const uint4* stg, uint32_t n_host, CSort C, uint32_t p,
-                                                        const unsigned long long* sk, const unsigned long long* sv,
-                                                        unsigned long long* dk, unsigned long long* dv) {
+__global__ void __launch_bounds__(CS_THREADS) k_rs_hist(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n > CS_SMALL) rs_hist_tile(P, stg, n, C, blockIdx.x);
+}
+
+__device__ __forceinline__ bool rs_pass_tile(const KP& P, uint32_t n, const CSort& C, uint32_t p,
+                                             const unsigned long long* sk, const unsigned long long* sv,
+                                             unsigned long long* dk, unsigned long long* dv) {
   __shared__ uint32_t s_h[256], s_off[256], s_cnt[CS_WAVES][256], s_lds[CS_WAVES];
   __shared__ uint32_t s_tile;
-  const uint32_t n = cs_n(P, stg, n_host), t = threadIdx.x;
-  if (n <= CS_SMALL) return;
+  const uint32_t t = threadIdx.x;
   if (t == 0) s_tile = atomicAdd(&C.ctr[p], 1u);  // tiles in start order: predecessors are running
   if (t < 256u) s_h[t] = 0u;
   __syncthreads();
   const uint32_t tile = s_tile, base = tile * CS_TILE;
-  if (base >= n) return;  // uniform
+  if (base >= n) return false;  // uniform
   const uint32_t sh = 8u * p;
   unsigned long long key[CS_PER];
   uint32_t dg[CS_PER];
@@ -615,16 +620,24 @@ __global__ void __launch_bounds__(CS_THREADS) k_rs_pass(KP P, const uint4* stg, 
     }
     __syncthreads();
   }
+  return true;
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_rs_pass(KP P, const uint4* stg, uint32_t n_host, CSort C, uint32_t p,
+                                                        const unsigned long long* sk, const unsigned long long* sv,
+                                                        unsigned long long* dk, unsigned long long* dv) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n > CS_SMALL) (void)rs_pass_tile(P, n, C, p, sk, sv, dk, dv);
 }
 
 // Slots opened per tile of the sorted batch (C.stat is free once the passes are done: tile
 // counts in stat[0 .. nt), their exclusive scan in stat[maxt .. maxt + nt), k_excl_scan)
-__global__ void __launch_bounds__(CS_THREADS) k_rs_slots(KP P, const uint4* stg, uint32_t n_host, CSort C,
-                                                         const unsigned long long* k) {
+__device__ __forceinline__ void rs_slots_tile(const KP& P, uint32_t n, const CSort& C, const unsigned long long* k,
+                                              uint32_t tile) {
   __shared__ uint32_t s_lds[CS_WAVES];
-  const uint32_t n = cs_n(P, stg, n_host);
-  if (n <= CS_SMALL || blockIdx.x * CS_TILE >= n) return;
-  const uint32_t i0 = blockIdx.x * CS_TILE + CS_PER * threadIdx.x;
+  if (tile * CS_TILE >= n) return;
+  __syncthreads();  // (a fused loop's previous tile has read s_lds)
+  const uint32_t i0 = tile * CS_TILE + CS_PER * threadIdx.x;
   uint32_t cnt = 0;
   for (uint32_t q = 0; q < CS_PER; ++q) {
     const uint32_t i = i0 + q;
@@ -632,21 +645,31 @@ __global__ void __launch_bounds__(CS_THREADS) k_rs_slots(KP P, const uint4* stg,
   }
   uint32_t tot;
   cs_block_scan(cnt, &tot, s_lds);
-  if (threadIdx.x == 0) C.stat[blockIdx.x] = tot;
+  if (threadIdx.x == 0) C.stat[tile] = tot;
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_rs_slots(KP P, const uint4* stg, uint32_t n_host, CSort C,
+                                                         const unsigned long long* k) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n > CS_SMALL) rs_slots_tile(P, n, C, k, blockIdx.x);
+}
+
+__device__ __forceinline__ void rs_commit_tile(const KP& P, uint32_t n, const CSort& C, const unsigned long long* k,
+                                               const unsigned long long* v, uint32_t tile) {
+  __shared__ uint32_t s_lds[CS_WAVES];
+  if (tile * CS_TILE >= n) return;
+  __syncthreads();  // (a fused loop's previous tile has read s_lds)
+  commit_block(P, P.ctl->gcount, P.ctl->ccount, n, tile * CS_TILE, C.stat[C.maxt + tile],
+               [&](uint32_t i) { return k[i]; }, [&](uint32_t i) { return v[i]; }, s_lds);
 }
 
 __global__ void __launch_bounds__(CS_THREADS) k_rs_commit(KP P, const uint4* stg, uint32_t n_host, CSort C,
                                                           const unsigned long long* k, const unsigned long long* v) {
-  __shared__ uint32_t s_lds[CS_WAVES];
   const uint32_t n = cs_n(P, stg, n_host);
-  if (n <= CS_SMALL || blockIdx.x * CS_TILE >= n) return;
-  commit_block(P, P.ctl->gcount, P.ctl->ccount, n, blockIdx.x * CS_TILE, C.stat[C.maxt + blockIdx.x],
-               [&](uint32_t i) { return k[i]; }, [&](uint32_t i) { return v[i]; }, s_lds);
+  if (n > CS_SMALL) rs_commit_tile(P, n, C, k, v, blockIdx.x);
 }
 
-__global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
-  const uint32_t n = cs_n(P, stg, n_host);
-  if (n <= CS_SMALL) return;
+__device__ __forceinline__ void rs_fin_one(const KP& P, const uint4* stg, uint32_t n, const CSort& C) {
   const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
   P.ctl->g_prev = P.ctl->gcount;
   P.ctl->gcount += C.stat[C.maxt + nt - 1u] + C.stat[nt - 1u];
@@ -654,6 +677,11 @@ __global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
   P.ctl->ccount += n;
   if (stg) P.ctl->stg_count = 0u;
   atomicAdd(&P.stat_shards[ST_COMMIT_RADIX], 1ull);  // (one thread: shard 0)
+}
+
+__global__ void k_rs_fin(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n > CS_SMALL) rs_fin_one(P, stg, n, C);
 }
 
 // Does a possibly-live ring slot hold a batch of several gossips? (swim_set_loss)
@@ -801,7 +829,7 @@ __global__ void k_dict_free(KP P) {
 }
 
 // Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
-__global__ void __launch_bounds__(CS_THREADS) k_excl_scan(const uint32_t* in, uint32_t* out, uint32_t n) {
+__device__ __forceinline__ void excl_scan_block(const uint32_t* in, uint32_t* out, uint32_t n) {
   __shared__ uint32_t s_lds4[CS_WAVES];
   const uint32_t per = (n + CS_THREADS - 1u) / CS_THREADS;
   const uint32_t a = min(n, threadIdx.x * per), e = min(n, a + per);
@@ -814,6 +842,62 @@ __global__ void __launch_bounds__(CS_THREADS) k_excl_scan(const uint32_t* in, ui
     out[i] = run;
     run += v;
   }
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_excl_scan(const uint32_t* in, uint32_t* out, uint32_t n) {
+  excl_scan_block(in, out, n);
+}
+
+// The radix chain in one launch (k_rs_hist, a k_rs_pass per digit, k_rs_slots, the tile scan,
+// k_rs_commit, k_rs_fin, with a grid barrier between steps) on a grid of at most CS_FUSE
+// workgroups, each walking tiles at a grid stride (the passes take tiles in start order from their
+// counters, as k_rs_pass does): every workgroup of such a grid is resident at once, so the barrier
+// cannot wait on one that was never scheduled. The host takes it for phases whose bound allows at
+// most CS_FUSE tiles (a gossip round: nloc / 4,096), where a batch the LDS sort took returns at
+// once: one launch instead of eleven, most of a quiet round's commit.
+constexpr uint32_t CS_FUSE = 32;
+__device__ __forceinline__ void cs_grid_sync(const KP& P, uint32_t* bar, uint32_t& target) {
+  __threadfence();  // every wave's stores complete before the workgroup arrives
+  __syncthreads();
+  target += gridDim.x;
+  if (threadIdx.x == 0) {
+    atomicAdd(bar, 1u);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > (1u << 24)) {  // a workgroup never arrived: fail loudly, never hang
+        atomicOr(&P.ctl->overflow, OV_BUG);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __threadfence();  // and the other workgroups' stores visible after it (no stale L1 lines)
+}
+
+__global__ void __launch_bounds__(CS_THREADS) k_rs_fused(KP P, const uint4* stg, uint32_t n_host, CSort C) {
+  const uint32_t n = cs_n(P, stg, n_host);
+  if (n <= CS_SMALL) return;  // (uniform over the grid: no workgroup enters a barrier)
+  uint32_t* bar = C.ctr + CS_MAXPASS;  // reset with the tile counters by k_commit
+  uint32_t target = 0;
+  for (uint32_t tile = blockIdx.x; tile * CS_TILE < n; tile += gridDim.x) rs_hist_tile(P, stg, n, C, tile);
+  cs_grid_sync(P, bar, target);
+  for (uint32_t p = 0; p < C.npass; ++p) {
+    const bool even = (p & 1u) == 0u;
+    while (rs_pass_tile(P, n, C, p, even ? C.k0 : C.k1, even ? C.v0 : C.v1, even ? C.k1 : C.k0, even ? C.v1 : C.v0)) {
+    }
+    cs_grid_sync(P, bar, target);
+  }
+  const bool in0 = (C.npass & 1u) == 0u;
+  const unsigned long long* ks = in0 ? C.k0 : C.k1;
+  for (uint32_t tile = blockIdx.x; tile * CS_TILE < n; tile += gridDim.x) rs_slots_tile(P, n, C, ks, tile);
+  cs_grid_sync(P, bar, target);
+  if (blockIdx.x == 0) excl_scan_block(C.stat, C.stat + C.maxt, C.maxt);
+  cs_grid_sync(P, bar, target);
+  for (uint32_t tile = blockIdx.x; tile * CS_TILE < n; tile += gridDim.x)
+    rs_commit_tile(P, n, C, ks, in0 ? C.v0 : C.v1, tile);
+  cs_grid_sync(P, bar, target);
+  if (blockIdx.x == 0 && threadIdx.x == 0) rs_fin_one(P, stg, n, C);
 }
 
 // ---------------------------------------------------------------------------------------

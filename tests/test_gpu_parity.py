@@ -271,7 +271,10 @@ def test_commit_radix_path_parity():
     chip-wide radix sort (k_rs_hist, k_rs_pass with decoupled look-back, k_rs_commit). At the
     parity sizes only storm phases get there, so a variant built with a 32-gossip LDS sort
     (-DSWIM_CS_SMALL=32) runs the churn scenario and the C3 storm at N = 1,024 through it: bit-exact
-    with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable)."""
+    with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable).
+    The variant sorts every batch in the single-launch chain (k_rs_fused, -DSWIM_RS_FUSE_ALL=1: at most
+    32 workgroups walking the tiles, grid barriers between the steps), which the product takes for
+    gossip rounds; the product's parity runs cover the eleven-launch chain of bigger phases."""
     out = _run_variant("libswimhip_cs32.so", _SPILL_SCRIPT)
     radix = int(out.split("RADIX")[-1].split()[0])
     assert radix > 0, "the chip-wide radix sort never ran"
