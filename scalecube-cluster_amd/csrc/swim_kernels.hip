@@ -3828,6 +3828,7 @@ __global__ void k_sync_select(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
+  bool req = false;  // a staged (or remote) request: k_sync_ack's work list
   if (i < P.row0 + P.nloc) {
     P.req_to[2 * i] = NONE;
     P.req_to[2 * i + 1] = NONE;
@@ -3854,6 +3855,7 @@ __global__ void k_sync_select(KP P) {
           const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
           P.xs_pend[(size_t)dst * 2u * P.nloc + o] = 2 * i + k;
           P.req_stage[2 * i + k] = REMOTE;
+          req = true;
           continue;
         }
         const uint32_t slot = atomicAdd(&P.ctl->stage_count, 1u);
@@ -3863,12 +3865,11 @@ __global__ void k_sync_select(KP P) {
         }
         P.req_stage[2 * i + k] = slot;
         P.stage_req[slot] = 2 * i + k;
+        req = true;
         recv_one(P, to[k]);
       }
     }
   }
-  // k_sync_ack's work: the requesters with a staged (or remote) request
-  const bool req = i < P.row0 + P.nloc && (P.req_stage[2 * i] != NONE || P.req_stage[2 * i + 1] != NONE);
   wave_push(&P.ctl->sy_an, P.sy_alist, req, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
