@@ -593,8 +593,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         // phase G+2: SYNC requests
         set_phase(h, P, G + 2);
-        // (stage_count, xs_cnt and the work-list counts were reset by k_due, recv_count / recv_fill
-        // by k_susp_sweep)
+        // (stage_count and xs_cnt were reset by k_due, recv_count / recv_fill by k_susp_sweep)
         if (P.tmode)  // the touched columns this period's SYNC payloads carry
           timed(h, 7, "k_tlist", [&] { hipLaunchKernelGGL(k_tlist, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 7, "k_sync_select", [&] { hipLaunchKernelGGL(k_sync_select, dim3(gL), dim3(256), 0, s, P); });
@@ -640,7 +639,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         });
         if (n_rec) hipLaunchKernelGGL(k_sync_scatter_remote, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         if (P.njoin) hipLaunchKernelGGL(k_join_scatter, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
-        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(std::min(nloc, SY_GRID)), dim3(256), 0, s, P); });
+        timed(h, 4, "k_sync_merge", [&] { hipLaunchKernelGGL(k_sync_merge, dim3(blocks_for(nloc, SY_MEMBERS)), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_ACK;
         if (SH) {  // SYNC_ACK tables back to the requesters' shards, in the order received
@@ -662,7 +661,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
           if (n_rec) hipLaunchKernelGGL(k_sync_ack_unpack, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
         }
-        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(std::min(nloc, SY_GRID)), dim3(256), 0, s, P); });
+        timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(blocks_for(nloc, SY_MEMBERS)), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
@@ -1187,8 +1186,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.recv_off, N + 1ull);
   ALLOC(P.recv_fill, N);
   ALLOC(P.bucket, 2ull * h->scap);  // local requests + requests received from other shards
-  ALLOC(P.sy_mlist, NL);  // SYNC work lists (recv_one / k_sync_select)
-  ALLOC(P.sy_alist, NL);
   {  // infectedFrom bookkeeping: in-history rings, delivery records, pruned pairs
     const uint64_t f = (uint64_t)c.gossip_fanout, W32 = h->GC / 32;
     // deliveries recorded per round: those whose receiver may select the sender within the

@@ -136,8 +136,6 @@ struct Ctl {
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
-  uint32_t sy_mn;       // this period's SYNC receivers (sy_mlist, recv_one) and requesters
-  uint32_t sy_an;       // awaiting a SYNC_ACK (sy_alist, k_sync_select / k_join_select); reset by k_due
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
@@ -313,8 +311,6 @@ struct KP {
   uint32_t* recv_off;   // [N+1]
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
-  uint32_t* sy_mlist;   // [nloc] local receivers of this period's SYNCs (k_sync_merge's work list, recv_one)
-  uint32_t* sy_alist;   // [nloc] local requesters that may take a SYNC_ACK (k_sync_ack's work list)
   uint4* stg;         // [stg_cap] gossips created since the last commit: origin, subject, record, id hash
   uint32_t stg_cap;
   // cross-shard exchange (world > 1)
@@ -992,22 +988,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   x += dpp_in<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
   *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
-}
-
-// append v to list (count *cnt) where pred holds: one atomic per wave (all lanes must call)
-__device__ __forceinline__ void wave_push(uint32_t* cnt, uint32_t* list, bool pred, uint32_t v) {
-  const unsigned long long b = __ballot(pred);
-  if (b == 0ull) return;
-  const uint32_t lane = threadIdx.x & 63u, leader = (uint32_t)__builtin_ctzll(b);
-  uint32_t base = 0u;
-  if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(b));
-  base = (uint32_t)__shfl((int)base, (int)leader, 64);
-  if (pred) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = v;
-}
-
-// one more SYNC request for local receiver j: the first one lists j for k_sync_merge (sy_mlist)
-__device__ __forceinline__ void recv_one(const KP& P, uint32_t j) {
-  if (atomicAdd(&P.recv_count[j], 1u) == 0u) P.sy_mlist[atomicAdd(&P.ctl->sy_mn, 1u)] = j;
 }
 
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {

@@ -3524,7 +3524,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     P.rs_ref[rec[0]] = g;
-    recv_one(P, rec[1]);
+    atomicAdd(&P.recv_count[rec[1]], 1u);
   }
 }
 
@@ -3601,8 +3601,6 @@ __global__ void __launch_bounds__(1024) k_due(KP P) {
   const uint32_t nc = ncells(P);
   if (threadIdx.x == 0) {  // this period's SYNC counters (k_sync_select on), in place of host memsets
     P.ctl->stage_count = 0u;
-    P.ctl->sy_mn = 0u;
-    P.ctl->sy_an = 0u;
   }
   if (threadIdx.x < SWIM_MAX_WORLD) P.ctl->xs_cnt[threadIdx.x] = 0u;
   uint32_t base = 0;
@@ -3828,7 +3826,6 @@ __global__ void k_sync_select(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
-  bool req = false;  // a staged (or remote) request: k_sync_ack's work list
   if (i < P.row0 + P.nloc) {
     P.req_to[2 * i] = NONE;
     P.req_to[2 * i + 1] = NONE;
@@ -3855,7 +3852,6 @@ __global__ void k_sync_select(KP P) {
           const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
           P.xs_pend[(size_t)dst * 2u * P.nloc + o] = 2 * i + k;
           P.req_stage[2 * i + k] = REMOTE;
-          req = true;
           continue;
         }
         const uint32_t slot = atomicAdd(&P.ctl->stage_count, 1u);
@@ -3865,12 +3861,10 @@ __global__ void k_sync_select(KP P) {
         }
         P.req_stage[2 * i + k] = slot;
         P.stage_req[slot] = 2 * i + k;
-        req = true;
-        recv_one(P, to[k]);
+        atomicAdd(&P.recv_count[to[k]], 1u);
       }
     }
   }
-  wave_push(&P.ctl->sy_an, P.sy_alist, req, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -3903,15 +3897,10 @@ __global__ void k_join_select(KP P) {
         P.jslot[i] = slot;
       }
       const uint32_t rcv = route(P, s);
-      recv_one(P, rcv);
+      atomicAdd(&P.recv_count[rcv], 1u);
       if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
     }
   }
-  // a local joiner whose initial SYNC_ACK comes back takes k_sync_ack's work list too (once: not
-  // if k_sync_select listed it for a request of its own)
-  const bool jack = i >= P.row0 && i < P.row0 + P.nloc && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap &&
-                    P.req_stage[2 * i] == NONE && P.req_stage[2 * i + 1] == NONE;
-  wave_push(&P.ctl->sy_an, P.sy_alist, jack, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -4153,10 +4142,22 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
 #endif
-// A workgroup per listed receiver (sy_mlist, built by recv_one), over a grid of at most SY_GRID
-// workgroups: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups took
-// 29 us of the fault-free period when ~1,800 had requests)
-constexpr uint32_t SY_GRID = 2048;
+// A workgroup per 32 members, which merges the requests of those that received any, one member
+// after the other: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups
+// took 29 us of the fault-free period when ~1,800 had requests). Work lists built with an atomic
+// counter cost as much again: ~1,000 waves serialised on one address.
+constexpr uint32_t SY_MEMBERS = 32;
+// bit q: member j0 + q of the block passes `pred` (wave 0 evaluates it, then the block shares it)
+template <typename Pred>
+__device__ __forceinline__ uint32_t sync_block_mask(uint32_t j0, uint32_t j1, Pred pred, uint32_t* s_mask) {
+  if (threadIdx.x < 64u) {
+    const uint32_t j = j0 + threadIdx.x;
+    const unsigned long long b = __ballot(threadIdx.x < SY_MEMBERS && j < j1 && pred(j));
+    if (threadIdx.x == 0) *s_mask = (uint32_t)b;
+  }
+  __syncthreads();
+  return *s_mask;
+}
 __device__ __forceinline__ void sync_merge_one(const KP& P, uint32_t j, uint32_t* s_list, uint32_t* s_lds4) {
   uint32_t cntj = P.recv_count[j];
   if (cntj == 0u) return;
@@ -4220,9 +4221,11 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
-  const uint32_t n = P.ctl->sy_mn;
-  for (uint32_t u = blockIdx.x; u < n; u += gridDim.x) {
-    sync_merge_one(P, P.sy_mlist[u], s_list, s_lds4);
+  __shared__ uint32_t s_mask;
+  const uint32_t j0 = P.row0 + blockIdx.x * SY_MEMBERS;
+  for (uint32_t m = sync_block_mask(j0, P.row0 + P.nloc, [&](uint32_t j) { return P.recv_count[j] != 0u; }, &s_mask);
+       m; m &= m - 1u) {
+    sync_merge_one(P, j0 + (uint32_t)__builtin_ctz(m), s_list, s_lds4);
     __syncthreads();  // (s_list is refilled for the next receiver)
   }
 }
@@ -4279,13 +4282,17 @@ __device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* 
   flush_tally(P, T);
 }
 
-// A workgroup per listed requester (sy_alist: k_sync_select, k_join_select), SY_GRID at most
+// A workgroup per 32 members, for those with a request out (or an initial SYNC, joining)
 __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
-  const uint32_t n = P.ctl->sy_an;
-  for (uint32_t u = blockIdx.x; u < n; u += gridDim.x) {
-    sync_ack_one(P, P.sy_alist[u], s_lds4);
+  __shared__ uint32_t s_mask;
+  const uint32_t i0 = P.row0 + blockIdx.x * SY_MEMBERS;
+  auto waits = [&](uint32_t i) {
+    return P.req_stage[2 * i] != NONE || P.req_stage[2 * i + 1] != NONE || (P.njoin && P.joining[i]);
+  };
+  for (uint32_t m = sync_block_mask(i0, P.row0 + P.nloc, waits, &s_mask); m; m &= m - 1u) {
+    sync_ack_one(P, i0 + (uint32_t)__builtin_ctz(m), s_lds4);
     __syncthreads();
   }
 }
