@@ -309,15 +309,11 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
       hipLaunchKernelGGL(k_rs_commit, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C, ks, in0 ? C.v0 : C.v1);
       hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n, C);
     }
-    // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights)
-    if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P, 0u);
+    // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights);
     // the record dictionary of the batched apply: every commit while batching is
-    // enabled, so records committed before the first batch have their entries too
-    if (h->dict_on) {
-      hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, P.dsids / 256)), dim3(256), 0, s, P);
-    }
+    // enabled, so records committed before the first batch have their entries too. One launch.
+    if (P.batched || h->dict_on)
+      hipLaunchKernelGGL(k_commit_tail, dim3(DICT_GRID), dim3(256), 0, s, P, P.batched ? 1u : 0u, h->dict_on ? 1u : 0u);
   });
   return SWIM_OK;
 }

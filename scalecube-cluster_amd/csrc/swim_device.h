@@ -136,6 +136,7 @@ struct Ctl {
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
+  uint32_t dict_bar;    // k_commit_tail's grid-barrier count (reset by k_commit)
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29

@@ -444,6 +444,7 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
   __shared__ uint32_t s_idx[CS_SMALL];
   const uint32_t t = threadIdx.x;
   const uint32_t n = cs_n(P, stg, n_host);
+  if (t == 0) P.ctl->dict_bar = 0u;  // k_commit_tail's barrier count
   if (n > CS_SMALL) {  // a storm phase: reset the radix sort's counters for this batch
     const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
     if (nt > C.radix) {  // the host's bound on this phase's gossips was wrong: fail loudly
@@ -696,7 +697,7 @@ __global__ void k_multi_live(KP P, uint32_t* out) {
 
 // Gossips per bitmap word (wsum) and per slot (scnt) of the words the last commit wrote slots into,
 // or (all) of every word that may be live (batch slots start: the words committed before them)
-__global__ void k_commit_wsum(KP P, uint32_t all) {
+__device__ __forceinline__ void commit_wsum_body(const KP& P, uint32_t all) {
   const uint32_t g1 = P.ctl->gcount;
   const uint32_t g0 = all ? (g1 - P.ctl->glo > P.GC ? g1 - P.GC : P.ctl->glo) : P.ctl->g_prev;
   const uint32_t w0 = g0 >> 5, w1 = (g1 + 31u) >> 5;
@@ -718,6 +719,8 @@ __global__ void k_commit_wsum(KP P, uint32_t all) {
   }
 }
 
+__global__ void k_commit_wsum(KP P, uint32_t all) { commit_wsum_body(P, all); }
+
 // ---- record dictionary, after every commit: claim, entries, free ----
 // A block for each subject of the commit's records that has none: the CAS winner pops a free
 // block (or takes a new one); when none is left the subject is marked with this commit's
@@ -726,7 +729,7 @@ __global__ void k_commit_wsum(KP P, uint32_t all) {
 // DICT_SIDS by at most the commit's subjects (< 2^21), and k_dict_entries clamps it back, so it can
 // never wrap onto blocks in use. (A compare-and-swap loop that never passed DICT_SIDS serialized
 // thousands of claims of one storm commit: C3 18.2 -> 20.6 ms/period.) No thread waits on another.
-__global__ void k_dict_claim(KP P) {
+__device__ __forceinline__ void dict_claim_body(const KP& P) {
   const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0, nfree = P.ctl->d_nfree;
   const uint32_t tag = DICT_NOBLK | (c0 & DICT_TAG_MASK);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -751,7 +754,7 @@ __global__ void k_dict_claim(KP P) {
 
 // Each record's entry in its subject's block: an entry holding the same record, else the first
 // empty one (claimed by CAS); a full block or no block: ID_NONE, remembered in d_none_last.
-__global__ void k_dict_entries(KP P) {
+__device__ __forceinline__ void dict_entries_body(const KP& P) {
   const uint32_t c0 = P.ctl->c_prev, n = P.ctl->ccount - c0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the blocks k_dict_claim popped leave the stack
     const uint32_t t = P.ctl->d_taken, f = P.ctl->d_nfree;
@@ -796,7 +799,7 @@ __global__ void k_dict_entries(KP P) {
 
 // Entries no live record names are emptied; a block left empty goes back on the stack (its
 // subject gets a block again with its next record).
-__global__ void k_dict_free(KP P) {
+__device__ __forceinline__ void dict_free_body(const KP& P) {
   const uint32_t hw = min(P.ctl->d_hw, P.dsids), c_lo = live_rec_lo(P);
   for (uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x; sid < hw; sid += gridDim.x * blockDim.x) {
     const uint32_t subj = P.d_subj[sid];
@@ -826,6 +829,43 @@ __global__ void k_dict_free(KP P) {
       P.d_free[atomicAdd(&P.ctl->d_nfree, 1u)] = sid;
     }
   }
+}
+
+__global__ void k_dict_claim(KP P) { dict_claim_body(P); }
+__global__ void k_dict_entries(KP P) { dict_entries_body(P); }
+__global__ void k_dict_free(KP P) { dict_free_body(P); }
+
+// The commit's tail in one launch: the batch slots' counter weights, then the record dictionary's
+// claims, entries and frees with a grid barrier between the dictionary steps (DICT_GRID workgroups
+// of 256 threads, every one resident at once), where four launches per commit were (§6.5).
+__device__ __forceinline__ void dict_grid_sync(const KP& P, uint32_t& target) {
+  __threadfence();
+  __syncthreads();
+  target += gridDim.x;
+  if (threadIdx.x == 0) {
+    atomicAdd(&P.ctl->dict_bar, 1u);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(&P.ctl->dict_bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > (1u << 24)) {  // a workgroup never arrived: fail loudly, never hang
+        atomicOr(&P.ctl->overflow, OV_BUG);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __threadfence();
+}
+
+__global__ void __launch_bounds__(256) k_commit_tail(KP P, uint32_t wsum, uint32_t dict) {
+  uint32_t target = 0;  // (k_commit reset the barrier count)
+  if (wsum) commit_wsum_body(P, 0u);
+  if (!dict) return;  // (uniform)
+  dict_claim_body(P);
+  dict_grid_sync(P, target);
+  dict_entries_body(P);
+  dict_grid_sync(P, target);
+  dict_free_body(P);
 }
 
 // Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
