@@ -4182,11 +4182,12 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
 #endif
-// A workgroup per 32 members, which merges the requests of those that received any, one member
+// A workgroup per 8 members, which merges the requests of those that received any, one member
 // after the other: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups
 // took 29 us of the fault-free period when ~1,800 had requests). Work lists built with an atomic
-// counter cost as much again: ~1,000 waves serialised on one address.
-constexpr uint32_t SY_MEMBERS = 32;
+// counter cost as much again: ~1,000 waves serialised on one address. (32 members per workgroup:
+// fault-free 0.67 ms per period, but C3's heal merges serialise within the blocks, 0.26 -> 0.38 ms.)
+constexpr uint32_t SY_MEMBERS = 8;
 // bit q: member j0 + q of the block passes `pred` (wave 0 evaluates it, then the block shares it)
 template <typename Pred>
 __device__ __forceinline__ uint32_t sync_block_mask(uint32_t j0, uint32_t j1, Pred pred, uint32_t* s_mask) {
@@ -4322,7 +4323,7 @@ __device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* 
   flush_tally(P, T);
 }
 
-// A workgroup per 32 members, for those with a request out (or an initial SYNC, joining)
+// A workgroup per 8 members, for those with a request out (or an initial SYNC, joining)
 __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
