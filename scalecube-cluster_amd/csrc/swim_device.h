@@ -96,6 +96,10 @@ constexpr uint32_t STAT_SHARDS = 64;  // power of two
 constexpr uint32_t STAT_STRIDE = 64;  // u64 per shard (512 B), >= ST_COUNT
 static_assert(ST_COUNT <= (int)STAT_STRIDE, "stat shard too small");
 
+// SYNC work lists are striped by local member id over SY_STRIPES counters: one counter per list
+// serialised ~1,000 same-address atomics per fault-free period
+constexpr uint32_t SY_STRIPES = 64;
+
 struct Ctl {
   unsigned long long rsv_stats[ST_COUNT];
   uint32_t gcount;      // gossips ever created (ids); slot = id & (GC-1)
@@ -136,7 +140,8 @@ struct Ctl {
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
-  uint32_t dict_bar;    // k_commit_tail's grid-barrier count (reset by k_commit)
+  uint32_t sy_mcnt[SY_STRIPES];  // this period's SYNC receivers per work-list stripe (recv_one)
+  uint32_t sy_acnt[SY_STRIPES];  // and requesters awaiting a SYNC_ACK (k_sync_select, k_join_select)
 };
 
 // act[] entry: word offset from w_beg in bits 0..25, window class in 26..27, sweep class in 28..29
@@ -312,6 +317,9 @@ struct KP {
   uint32_t* recv_off;   // [N+1]
   uint32_t* recv_fill;  // [N]
   uint32_t* bucket;     // [scap]
+  uint32_t* sy_mlist;   // [SY_STRIPES][sy_cap] local receivers of this period's SYNCs (k_sync_merge's work)
+  uint32_t* sy_alist;   // [SY_STRIPES][sy_cap] local requesters that may take a SYNC_ACK (k_sync_ack's work)
+  uint32_t sy_cap;      // ceil(nloc / SY_STRIPES): a stripe's capacity (a member is listed once per list)
   uint4* stg;         // [stg_cap] gossips created since the last commit: origin, subject, record, id hash
   uint32_t stg_cap;
   // cross-shard exchange (world > 1)
@@ -989,6 +997,17 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   x += dpp_in<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
   *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
+}
+
+// list member v (local index l) in its stripe of a SYNC work list
+__device__ __forceinline__ void sy_push(uint32_t* cnt, uint32_t* list, uint32_t cap, uint32_t l, uint32_t v) {
+  const uint32_t st = l % SY_STRIPES;
+  list[(size_t)st * cap + atomicAdd(&cnt[st], 1u)] = v;
+}
+
+// one more SYNC request for local receiver j: the first one lists j for k_sync_merge
+__device__ __forceinline__ void recv_one(const KP& P, uint32_t j) {
+  if (atomicAdd(&P.recv_count[j], 1u) == 0u) sy_push(P.ctl->sy_mcnt, P.sy_mlist, P.sy_cap, j - P.row0, j);
 }
 
 __device__ __forceinline__ void add_stat(const KP& P, int idx, uint32_t v) {

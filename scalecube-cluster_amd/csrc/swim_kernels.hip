@@ -444,7 +444,6 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
   __shared__ uint32_t s_idx[CS_SMALL];
   const uint32_t t = threadIdx.x;
   const uint32_t n = cs_n(P, stg, n_host);
-  if (t == 0) P.ctl->dict_bar = 0u;  // k_commit_tail's barrier count
   if (n > CS_SMALL) {  // a storm phase: reset the radix sort's counters for this batch
     const uint32_t nt = (n + CS_TILE - 1u) / CS_TILE;
     if (nt > C.radix) {  // the host's bound on this phase's gossips was wrong: fail loudly
@@ -835,38 +834,6 @@ __global__ void k_dict_claim(KP P) { dict_claim_body(P); }
 __global__ void k_dict_entries(KP P) { dict_entries_body(P); }
 __global__ void k_dict_free(KP P) { dict_free_body(P); }
 
-// The commit's tail in one launch: the batch slots' counter weights, then the record dictionary's
-// claims, entries and frees with a grid barrier between the dictionary steps (DICT_GRID workgroups
-// of 256 threads, every one resident at once), where four launches per commit were (§6.5).
-__device__ __forceinline__ void dict_grid_sync(const KP& P, uint32_t& target) {
-  __threadfence();
-  __syncthreads();
-  target += gridDim.x;
-  if (threadIdx.x == 0) {
-    atomicAdd(&P.ctl->dict_bar, 1u);
-    uint32_t spins = 0;
-    while (__hip_atomic_load(&P.ctl->dict_bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > (1u << 24)) {  // a workgroup never arrived: fail loudly, never hang
-        atomicOr(&P.ctl->overflow, OV_BUG);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  __threadfence();
-}
-
-__global__ void __launch_bounds__(256) k_commit_tail(KP P, uint32_t wsum, uint32_t dict) {
-  uint32_t target = 0;  // (k_commit reset the barrier count)
-  if (wsum) commit_wsum_body(P, 0u);
-  if (!dict) return;  // (uniform)
-  dict_claim_body(P);
-  dict_grid_sync(P, target);
-  dict_entries_body(P);
-  dict_grid_sync(P, target);
-  dict_free_body(P);
-}
 
 // Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
 __device__ __forceinline__ void excl_scan_block(const uint32_t* in, uint32_t* out, uint32_t n) {
@@ -896,11 +863,14 @@ __global__ void __launch_bounds__(CS_THREADS) k_excl_scan(const uint32_t* in, ui
 // most CS_FUSE tiles (a gossip round: nloc / 4,096), where a batch the LDS sort took returns at
 // once: one launch instead of eleven, most of a quiet round's commit.
 constexpr uint32_t CS_FUSE = 32;
+// (the workgroup barrier completes every wave's stores to the XCD's L2; thread 0's agent-scope
+// fences then write that L2 back before the arrival and invalidate it after the wait: one L2
+// write-back / invalidate per workgroup and barrier, not per wave, which on 8 XCDs costs microseconds)
 __device__ __forceinline__ void cs_grid_sync(const KP& P, uint32_t* bar, uint32_t& target) {
-  __threadfence();  // every wave's stores complete before the workgroup arrives
   __syncthreads();
   target += gridDim.x;
   if (threadIdx.x == 0) {
+    __threadfence();
     atomicAdd(bar, 1u);
     uint32_t spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -910,9 +880,9 @@ __device__ __forceinline__ void cs_grid_sync(const KP& P, uint32_t* bar, uint32_
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    __threadfence();  // the other workgroups' stores visible after it (no stale L1 / L2 lines)
   }
   __syncthreads();
-  __threadfence();  // and the other workgroups' stores visible after it (no stale L1 lines)
 }
 
 __global__ void __launch_bounds__(CS_THREADS) k_rs_fused(KP P, const uint4* stg, uint32_t n_host, CSort C) {
@@ -3564,7 +3534,7 @@ __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     P.rs_ref[rec[0]] = g;
-    atomicAdd(&P.recv_count[rec[1]], 1u);
+    recv_one(P, rec[1]);
   }
 }
 
@@ -3643,6 +3613,10 @@ __global__ void __launch_bounds__(1024) k_due(KP P) {
     P.ctl->stage_count = 0u;
   }
   if (threadIdx.x < SWIM_MAX_WORLD) P.ctl->xs_cnt[threadIdx.x] = 0u;
+  if (threadIdx.x < SY_STRIPES) {
+    P.ctl->sy_mcnt[threadIdx.x] = 0u;
+    P.ctl->sy_acnt[threadIdx.x] = 0u;
+  }
   uint32_t base = 0;
   for (uint32_t j0 = 0; j0 < nc; j0 += 65536u) {
     const uint32_t c0 = j0 + 64u * threadIdx.x;
@@ -3866,6 +3840,7 @@ __global__ void k_sync_select(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
+  bool req = false;  // a staged (or remote) request: k_sync_ack's work
   if (i < P.row0 + P.nloc) {
     P.req_to[2 * i] = NONE;
     P.req_to[2 * i + 1] = NONE;
@@ -3892,6 +3867,7 @@ __global__ void k_sync_select(KP P) {
           const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
           P.xs_pend[(size_t)dst * 2u * P.nloc + o] = 2 * i + k;
           P.req_stage[2 * i + k] = REMOTE;
+          req = true;
           continue;
         }
         const uint32_t slot = atomicAdd(&P.ctl->stage_count, 1u);
@@ -3901,10 +3877,12 @@ __global__ void k_sync_select(KP P) {
         }
         P.req_stage[2 * i + k] = slot;
         P.stage_req[slot] = 2 * i + k;
-        atomicAdd(&P.recv_count[to[k]], 1u);
+        req = true;
+        recv_one(P, to[k]);
       }
     }
   }
+  if (req) sy_push(P.ctl->sy_acnt, P.sy_alist, P.sy_cap, i - P.row0, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -3937,10 +3915,15 @@ __global__ void k_join_select(KP P) {
         P.jslot[i] = slot;
       }
       const uint32_t rcv = route(P, s);
-      atomicAdd(&P.recv_count[rcv], 1u);
+      recv_one(P, rcv);
       if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
     }
   }
+  // a joiner whose initial SYNC_ACK comes back is k_sync_ack's work too (k_sync_ack's own test; once:
+  // not when k_sync_select listed it for a request of its own)
+  if (i >= P.row0 && i < P.row0 + P.nloc && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap &&
+      P.req_stage[2 * i] == NONE && P.req_stage[2 * i + 1] == NONE)
+    sy_push(P.ctl->sy_acnt, P.sy_alist, P.sy_cap, i - P.row0, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
 }
@@ -4182,23 +4165,30 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 #ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
 #endif
-// A workgroup per 8 members, which merges the requests of those that received any, one member
-// after the other: a period's ~N/S receivers, not a workgroup per member (65,536 launched workgroups
-// took 29 us of the fault-free period when ~1,800 had requests). Work lists built with an atomic
-// counter cost as much again: ~1,000 waves serialised on one address. (32 members per workgroup:
-// fault-free 0.67 ms per period, but C3's heal merges serialise within the blocks, 0.26 -> 0.38 ms.)
-constexpr uint32_t SY_MEMBERS = 8;
-// bit q: member j0 + q of the block passes `pred` (wave 0 evaluates it, then the block shares it)
-template <typename Pred>
-__device__ __forceinline__ uint32_t sync_block_mask(uint32_t j0, uint32_t j1, Pred pred, uint32_t* s_mask) {
-  if (threadIdx.x < 64u) {
-    const uint32_t j = j0 + threadIdx.x;
-    const unsigned long long b = __ballot(threadIdx.x < SY_MEMBERS && j < j1 && pred(j));
-    if (threadIdx.x == 0) *s_mask = (uint32_t)b;
+// A workgroup per listed member, over a grid of at most SY_GRID workgroups: a period's ~N/S
+// receivers (requesters), not a workgroup per member (65,536 launched workgroups took 29 us of the
+// fault-free period when ~1,800 had requests; a workgroup per 32 members serialised C3's heal merges).
+// The lists are striped (sy_push): the u-th entry is in the last stripe whose count prefix is <= u.
+constexpr uint32_t SY_GRID = 2048;
+template <typename F>
+__device__ __forceinline__ void sy_for_each(const uint32_t* cnt, const uint32_t* list, uint32_t cap, uint32_t* s_pre, F f) {
+  if (threadIdx.x < 64u) {  // (wave 0, every lane: SY_STRIPES = 64)
+    const uint32_t v = cnt[threadIdx.x];
+    uint32_t tot;
+    s_pre[threadIdx.x] = wave_excl_scan(v, &tot);
+    if (threadIdx.x == 0) s_pre[64] = tot;
   }
   __syncthreads();
-  return *s_mask;
+  const uint32_t tot = s_pre[64];
+  for (uint32_t u = blockIdx.x; u < tot; u += gridDim.x) {
+    uint32_t st = 0;
+    for (uint32_t step = 32u; step; step >>= 1)
+      if (st + step < SY_STRIPES && s_pre[st + step] <= u) st += step;
+    f(list[(size_t)st * cap + (u - s_pre[st])]);
+    __syncthreads();
+  }
 }
+static_assert(SY_STRIPES == 64, "sy_for_each scans the stripe counts in one wave");
 __device__ __forceinline__ void sync_merge_one(const KP& P, uint32_t j, uint32_t* s_list, uint32_t* s_lds4) {
   uint32_t cntj = P.recv_count[j];
   if (cntj == 0u) return;
@@ -4262,13 +4252,9 @@ __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_merge(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_list[BUCKET_MAX];
   __shared__ uint32_t s_lds4[4];
-  __shared__ uint32_t s_mask;
-  const uint32_t j0 = P.row0 + blockIdx.x * SY_MEMBERS;
-  for (uint32_t m = sync_block_mask(j0, P.row0 + P.nloc, [&](uint32_t j) { return P.recv_count[j] != 0u; }, &s_mask);
-       m; m &= m - 1u) {
-    sync_merge_one(P, j0 + (uint32_t)__builtin_ctz(m), s_list, s_lds4);
-    __syncthreads();  // (s_list is refilled for the next receiver)
-  }
+  __shared__ uint32_t s_pre[SY_STRIPES + 1];
+  // (sy_for_each's barrier after each receiver: s_list is refilled for the next one)
+  sy_for_each(P.ctl->sy_mcnt, P.sy_mlist, P.sy_cap, s_pre, [&](uint32_t j) { sync_merge_one(P, j, s_list, s_lds4); });
 }
 
 // onSyncAck (MembershipProtocolImpl.java:343-349) at requester i = blockIdx.
@@ -4323,19 +4309,12 @@ __device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* 
   flush_tally(P, T);
 }
 
-// A workgroup per 8 members, for those with a request out (or an initial SYNC, joining)
+// A workgroup per listed requester (k_sync_select, k_join_select), SY_GRID at most
 __global__ void __launch_bounds__(256, SWIM_SYNC_WAVES) k_sync_ack(KP P) {
   SWIM_GUARD(P);
   __shared__ uint32_t s_lds4[4];
-  __shared__ uint32_t s_mask;
-  const uint32_t i0 = P.row0 + blockIdx.x * SY_MEMBERS;
-  auto waits = [&](uint32_t i) {
-    return P.req_stage[2 * i] != NONE || P.req_stage[2 * i + 1] != NONE || (P.njoin && P.joining[i]);
-  };
-  for (uint32_t m = sync_block_mask(i0, P.row0 + P.nloc, waits, &s_mask); m; m &= m - 1u) {
-    sync_ack_one(P, i0 + (uint32_t)__builtin_ctz(m), s_lds4);
-    __syncthreads();
-  }
+  __shared__ uint32_t s_pre[SY_STRIPES + 1];
+  sy_for_each(P.ctl->sy_acnt, P.sy_alist, P.sy_cap, s_pre, [&](uint32_t i) { sync_ack_one(P, i, s_lds4); });
 }
 
 // ---------------------------------------------------------------------------------------
