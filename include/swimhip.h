@@ -193,6 +193,8 @@ typedef struct swim_stats {
   uint64_t apply_skipped;     /* dictionary blocks the batched apply skipped by their merge mark: every
                                  received record already found not to override the cell (DESIGN.md
                                  §3.15); 0 in the oracle */
+  uint64_t apply_bitmaps;     /* long record ranges the batched apply ORed as their slot's entry bitmap
+                                 instead of walking their ids; 0 in the oracle */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;

@@ -25,6 +25,10 @@ constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 #ifndef SWIM_CID16
 #define SWIM_CID16 1
 #endif
+#ifndef SWIM_RB_CAP
+#define SWIM_RB_CAP 2048  // slot entry bitmaps (k_slot_bm; 0: none)
+#endif
+constexpr uint32_t RB_GRID = 256;  // k_slot_bm's workgroups (a grid stride over the commit's new slots)
 #ifndef SWIM_RS_FUSE
 #define SWIM_RS_FUSE 1  // the radix chain in one launch where its grid allows (k_rs_fused)
 #endif
@@ -318,6 +322,8 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
       hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, P.dsids / 256)), dim3(256), 0, s, P);
+      // the entry bitmaps of this commit's long batch ranges (dsids bytes of LDS per workgroup)
+      if (P.batched && P.rb_cap) hipLaunchKernelGGL(k_slot_bm, dim3(RB_GRID), dim3(256), P.dsids, s, P);
     }
   });
   return SWIM_OK;
@@ -981,6 +987,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
                           reinterpret_cast<const void*>(&k_gossip_apply_b16),
                           reinterpret_cast<const void*>(&k_gossip_apply_b16_h4)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_slot_bm), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)P.dsids);
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",
@@ -1126,6 +1134,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.d_free, P.dsids);
     ALLOC(P.d_gen, P.dsids);
     ALLOC(P.dmark, NL * P.dsids);
+    // slot entry bitmaps of long record ranges (k_slot_bm), a ring of SWIM_RB_CAP of dsids bytes each
+    P.rb_cap = SWIM_RB_CAP;
+    if (P.rb_cap) {
+      ALLOC(P.rb_bits, (size_t)P.rb_cap * (P.dsids / 4u));
+      ALLOC(P.rb_tag, P.rb_cap);
+      ALLOC(P.g_rb, h->GC);
+    }
   }
   ALLOC(P.wsum, h->GC / 32);
   ALLOC(P.scnt, h->GC);
@@ -1294,6 +1309,10 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     (void)hipMemsetAsync(P.d_last, 0, (size_t)P.dsids * DICT_WAYS * 4, s);
     hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.dsids, 256)), dim3(256), 0, s, P.d_gen, (size_t)P.dsids, 1u);
     (void)hipMemsetAsync(P.dmark, 0, NL * P.dsids * 4, s);
+    if (P.rb_cap) {
+      (void)hipMemsetAsync(P.rb_tag, 0xFF, (size_t)P.rb_cap * 4, s);
+      (void)hipMemsetAsync(P.g_rb, 0xFF, (size_t)h->GC * 4, s);
+    }
   }
   (void)hipMemsetAsync(P.wlast, 0, (size_t)(h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.runw, 0, (size_t)(h->GC / 32) * 4, s);
@@ -1940,6 +1959,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->apply_pairs = stats[ST_APPLY_PAIRS];
   out->commit_radix = stats[ST_COMMIT_RADIX];
   out->apply_skipped = stats[ST_APPLY_SKIP];
+  out->apply_bitmaps = stats[ST_APPLY_RBM];
   out->escape_entries = ctl.hx_live;
   out->escape_capacity = h->base.hd4 ? (uint64_t)h->base.hxmask + 1u : 0u;
   {  // gossips in the live slots: the record ring from the oldest live slot's first record

@@ -63,6 +63,7 @@ enum StatIdx : int {
   ST_APPLY_PAIRS,  // receiver pairs k_gossip_apply processed in two half-workgroups (SWIM_APPLY_PAIR)
   ST_COMMIT_RADIX, // commit phases sorted by the chip-wide radix sort (more than CS_SMALL gossips)
   ST_APPLY_SKIP,   // dictionary blocks k_gossip_apply_b skipped by their merge mark (no cell read)
+  ST_APPLY_RBM,    // long record ranges k_gossip_apply_b ORed as a slot entry bitmap (k_slot_bm)
   ST_COUNT
 };
 
@@ -140,6 +141,7 @@ struct Ctl {
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
+  uint32_t rb_next;     // slot entry bitmaps handed out (mod rb_cap)
   uint32_t sy_mcnt[SY_STRIPES];  // this period's SYNC receivers per work-list stripe (recv_one)
   uint32_t sy_acnt[SY_STRIPES];  // and requesters awaiting a SYNC_ACK (k_sync_select, k_join_select)
 };
@@ -252,6 +254,12 @@ struct KP {
   // gossip (loss set, or batching off). Its records live in the record ring c_sr / c_hash at
   // absolute indices [g_cref.x, g_cref.y).
   uint2* g_cref;      // [GC] record range of each slot (absolute indices into c_sr, mod CC)
+  // slot entry bitmaps: a long record range's dictionary entries as one bitmap
+  // (dsids / 4 words), built once at its commit, ORed by a receiver instead of walking the ids
+  uint32_t* rb_bits;  // [rb_cap][dsids / 4]
+  uint32_t* rb_tag;   // [rb_cap] the range start (c_sr index) a bitmap was built for; NONE: unusable
+  uint32_t* g_rb;     // [GC] a slot's bitmap (rb_tag must still name its range), or NONE
+  uint32_t rb_cap;    // bitmaps in the pool (a ring: a newer range takes the oldest)
   uint2* c_sr;        // [CC] (subject, packed record) of every gossip of a live slot
   uint32_t* c_hash;   // [CC] its canonical id hash (GossipProtocolImpl.generateGossipId, :211-213)
   uint32_t cmask;     // CC - 1

@@ -830,6 +830,51 @@ __device__ __forceinline__ void dict_free_body(const KP& P) {
   }
 }
 
+// Slot entry bitmaps of this commit's long ranges: a workgroup per new slot whose range holds at
+// least as many records as the dictionary's bitmap has words in use (below that, walking the ids
+// costs a receiver fewer LDS operations than ORing the bitmap). Records without an entry (a user
+// gossip, a full block) leave the range without one: a receiver walks those ranges.
+__global__ void __launch_bounds__(256) k_slot_bm(KP P) {
+  extern __shared__ uint32_t s_rb[];  // dsids / 4 words
+  __shared__ uint32_t s_flag;
+  const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount, nbw = P.dsids / 4u;
+  const uint32_t bw = (min(P.ctl->d_hw, P.dsids) * DICT_WAYS + 31u) >> 5;
+  const uint32_t dids = P.dsids * DICT_WAYS, dlim = P.cid16 ? min(dids, ID16_USER) : dids;
+  for (uint32_t g = g0 + blockIdx.x; (int32_t)(g1 - g) > 0; g += gridDim.x) {
+    const uint32_t sl = gmod(P, g);
+    const uint2 cr = P.g_cref[sl];
+    if (cr.y - cr.x < bw || cr.y - cr.x < 64u) continue;  // (uniform)
+    for (uint32_t t = threadIdx.x; t < nbw; t += blockDim.x) s_rb[t] = 0u;
+    if (threadIdx.x == 0) s_flag = 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cr.y - cr.x; i += blockDim.x) {
+      const uint32_t x = cr.x + i;
+      const uint32_t id = P.cid16 ? (uint32_t)P.c_id16[x & P.cmask] : P.c_id[x & P.cmask];
+      const uint32_t idn = P.cid16 ? (id >= ID16_USER ? NONE : id) : id;
+      if (idn < dlim)
+        atomicOr(&s_rb[idn >> 5], 1u << (idn & 31u));
+      else
+        s_flag = 1u;
+    }
+    __syncthreads();
+    if (s_flag == 0u) {
+      __shared__ uint32_t s_rbi;
+      if (threadIdx.x == 0) s_rbi = atomicAdd(&P.ctl->rb_next, 1u) % P.rb_cap;
+      __syncthreads();
+      const uint32_t rb = s_rbi;
+      uint32_t* dst = P.rb_bits + (size_t)rb * nbw;
+      for (uint32_t t = threadIdx.x; t < nbw; t += blockDim.x) dst[t] = s_rb[t];
+      if (threadIdx.x == 0) {
+        P.rb_tag[rb] = cr.x;
+        P.g_rb[sl] = rb;
+      }
+    } else if (threadIdx.x == 0) {
+      P.g_rb[sl] = NONE;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void k_dict_claim(KP P) { dict_claim_body(P); }
 __global__ void k_dict_entries(KP P) { dict_entries_body(P); }
 __global__ void k_dict_free(KP P) { dict_free_body(P); }
@@ -2944,7 +2989,8 @@ __host__ __device__ __forceinline__ uint32_t aw_words(uint32_t dsids) { return d
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
 #ifndef SWIM_AW_MINW
-#define SWIM_AW_MINW 1
+#define SWIM_AW_MINW 4  // (the LDS bitmap caps the 8,192-block dictionary at 4 waves per SIMD anyway:
+                        // registers beyond 128 would only lower that)
 #endif
 template <bool HD4, bool C16>
 __device__ __forceinline__ void apply_b_body(const KP& P) {
@@ -3082,7 +3128,8 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         const uint32_t o = wave_owner_at(off, (uint32_t)__popc(rm), q0);
         const uint32_t mo = __shfl(rm, (int)o, 64), wo = __shfl(ws, (int)o, 64), oo = __shfl(off, (int)o, 64);
         uint2 cr = make_uint2(0u, 0u);
-        if (q < tot) cr = P.g_cref[wo * 32u + kth_set_bit(mo, q - oo)];
+        const uint32_t slq = wo * 32u + kth_set_bit(mo, q - oo);  // the run top's ring slot
+        if (q < tot) cr = P.g_cref[slq];
         const uint32_t len = cr.y - cr.x;
         ent += len;
 #ifdef SWIM_APPLY_PROF
@@ -3107,6 +3154,28 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           const int L = __builtin_ctzll(big);
           big &= big - 1ull;
           const uint32_t b0 = __shfl(cr.x, L, 64), b1 = __shfl(cr.y, L, 64);
+          if (b1 - b0 >= bw && P.rb_cap) {  // the range's entry bitmap, if its commit built one (k_slot_bm)
+            const uint32_t sl = __shfl(slq, L, 64);
+            uint32_t rb = P.g_rb[sl];
+            if (rb != NONE && P.rb_tag[rb] != b0) rb = NONE;  // (taken by a newer range since)
+            if (rb != NONE) {  // (uniform)
+              const uint32_t nbw = P.dsids / 4u;
+              const uint32_t* src = P.rb_bits + (size_t)rb * nbw;
+              for (uint32_t t = 4u * lane; t < bw; t += 256u) {
+                if (t + 3u < nbw) {
+                  const uint4 v = *reinterpret_cast<const uint4*>(src + t);
+                  s_bm[t] |= v.x;
+                  s_bm[t + 1u] |= v.y;
+                  s_bm[t + 2u] |= v.z;
+                  s_bm[t + 3u] |= v.w;
+                } else {
+                  for (uint32_t k = 0; t + k < bw; ++k) s_bm[t + k] |= src[t + k];
+                }
+              }
+              if (lane == 0) atomicAdd(&P.stat_shards[(blockIdx.x & (STAT_SHARDS - 1u)) * STAT_STRIDE + ST_APPLY_RBM], 1ull);
+              continue;
+            }
+          }
           // aligned 16-B groups of entry ids from the group holding b0: IDG records per lane per load
           const uint32_t a0 = b0 & ~(IDG - 1u), span = b1 - a0;
           for (uint32_t x0 = 0; x0 < span; x0 += 64u * IDG * AW_VILP) {

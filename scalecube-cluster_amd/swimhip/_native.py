@@ -124,6 +124,7 @@ STAT_FIELDS = [
     "escape_entries",
     "escape_capacity",
     "apply_skipped",
+    "apply_bitmaps",
 ]
 
 

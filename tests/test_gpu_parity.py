@@ -361,12 +361,15 @@ def test_c3_half_partition_1024_matches_oracle(dsub):
     accepted SUSPECT record (MembershipProtocolImpl.java:649-656), ~5e5 gossips in batch slots whose
     records merge through the record dictionary and the merge marks. Events, counters and digests
     every 5 periods through the heal and the first suspicion timeouts. The default 8,192-block
-    dictionary names entries in 16 bits; a 16,384-block one (dict_subjects) in 32."""
+    dictionary names entries in 16 bits; a 16,384-block one (dict_subjects) in 32.
+    The heal's long batch ranges reach their receivers as slot entry bitmaps."""
     def make(cfg, n, seed, **kw):
         return SwimCluster(cfg, n, seed, **({"dict_subjects": dsub} if dsub else {}), **kw)
 
-    scenarios.run_pair("c3half1024", make, OracleCluster, compare_every=5, full_tables=False,
-                       event_capacity=1 << 22)
+    a, _ = scenarios.run_pair("c3half1024", make, OracleCluster, compare_every=5, full_tables=False,
+                              event_capacity=1 << 22)
+    # the heal's long batch ranges were ORed as their slots' entry bitmaps (k_slot_bm), not walked
+    assert a.stats()["apply_bitmaps"] > 0
 
 
 # The sharded rehearsals' shapes of BASELINE configs 3 and 4 (tests/test_sharded.py compares their
