@@ -143,11 +143,13 @@ def kernel_bytes(name, d, rounds_per_period=5):
         # 8,192 dictionary blocks, else 4: entry_id_bytes), per block with
         # received entries its merge mark and the block's generation (8 B), and per block merged (not
         # skipped by its mark) the entry's record, the block's subject and the table cell (12 B)
+        # (records of long ranges ORed as their slot's entry bitmap: the bitmap's bytes, dsids, instead)
         recs = d.get("apply_records", 0)
         if recs:
             blocks = d["apply_subjects"] + d.get("apply_skipped", 0)
-            return (93 * d["apply_words"] + 8 * d["apply_runs"] + d.get("id_bytes", 4) * recs + 8 * blocks
-                    + 12 * d["apply_subjects"])
+            walked = recs - d.get("apply_bitmap_records", 0)
+            return (93 * d["apply_words"] + 8 * d["apply_runs"] + d.get("id_bytes", 4) * walked
+                    + d.get("dict_bytes", 8192) * d.get("apply_bitmaps", 0) + 8 * blocks + 12 * d["apply_subjects"])
         return 93 * d["apply_words"] + 8 * d["apply_runs"] + 8 * d["apply_subjects"]
     if name == "k_susp_sweep":  # stream a u16 deadline column; per fired cell the deadline write, the
         # view cell read + write, and (a handle with an event ring) its 24-B REMOVED event
@@ -449,6 +451,7 @@ def main():
     c.kernel_timing(False)
     d = {k: s1[k] - s0[k] for k in s1}
     d["id_bytes"] = entry_id_bytes(w)
+    d["dict_bytes"] = w.get("dsub") or 8192  # a slot entry bitmap: one bit per entry, 8 per block
     n_events = c.discard_events() if ecap else 0  # (none expected: no timeout falls due in the window)
 
     # dominant kernel + roofline over the timed region
@@ -546,7 +549,7 @@ def main():
                                    "gossip_pull_words", "gossip_probes", "events_removed", "gossip_sends",
                                    "infected_suppressed", "infected_pruned_pairs", "infected_records",
                                    "apply_words", "apply_runs", "apply_subjects", "apply_records", "apply_spills",
-                                   "apply_skipped")},
+                                   "apply_skipped", "apply_bitmaps", "apply_bitmap_records")},
         "gossip_slots": {"live_at_end": s1["live_gossip_slots"], "gossips_live_at_end": s1["live_gossip_records"]},
     }
     c.close()

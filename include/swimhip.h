@@ -195,6 +195,7 @@ typedef struct swim_stats {
                                  §3.15); 0 in the oracle */
   uint64_t apply_bitmaps;     /* long record ranges the batched apply ORed as their slot's entry bitmap
                                  instead of walking their ids; 0 in the oracle */
+  uint64_t apply_bitmap_records; /* the records of those ranges (their ids were not read)          */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;

@@ -1960,6 +1960,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->commit_radix = stats[ST_COMMIT_RADIX];
   out->apply_skipped = stats[ST_APPLY_SKIP];
   out->apply_bitmaps = stats[ST_APPLY_RBM];
+  out->apply_bitmap_records = stats[ST_APPLY_RBREC];
   out->escape_entries = ctl.hx_live;
   out->escape_capacity = h->base.hd4 ? (uint64_t)h->base.hxmask + 1u : 0u;
   {  // gossips in the live slots: the record ring from the oldest live slot's first record

@@ -64,6 +64,7 @@ enum StatIdx : int {
   ST_COMMIT_RADIX, // commit phases sorted by the chip-wide radix sort (more than CS_SMALL gossips)
   ST_APPLY_SKIP,   // dictionary blocks k_gossip_apply_b skipped by their merge mark (no cell read)
   ST_APPLY_RBM,    // long record ranges k_gossip_apply_b ORed as a slot entry bitmap (k_slot_bm)
+  ST_APPLY_RBREC,  // ... and their records
   ST_COUNT
 };
 

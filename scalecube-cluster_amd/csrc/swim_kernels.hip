@@ -3172,7 +3172,11 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
                   for (uint32_t k = 0; t + k < bw; ++k) s_bm[t + k] |= src[t + k];
                 }
               }
-              if (lane == 0) atomicAdd(&P.stat_shards[(blockIdx.x & (STAT_SHARDS - 1u)) * STAT_STRIDE + ST_APPLY_RBM], 1ull);
+              if (lane == 0) {
+                unsigned long long* st = P.stat_shards + (blockIdx.x & (STAT_SHARDS - 1u)) * STAT_STRIDE;
+                atomicAdd(&st[ST_APPLY_RBM], 1ull);
+                atomicAdd(&st[ST_APPLY_RBREC], (unsigned long long)(b1 - b0));
+              }
               continue;
             }
           }

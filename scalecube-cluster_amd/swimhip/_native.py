@@ -125,6 +125,7 @@ STAT_FIELDS = [
     "escape_capacity",
     "apply_skipped",
     "apply_bitmaps",
+    "apply_bitmap_records",
 ]
 
 
