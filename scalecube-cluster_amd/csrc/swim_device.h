@@ -487,7 +487,11 @@ __device__ __forceinline__ void dq_window(const KP& P, uint32_t p, uint32_t* lo,
   *hi = h;
 }
 constexpr uint32_t DQ_PAIR = 0x10000u;   // k_gossip_select: the chosen peer delivered delayed messages
-constexpr uint32_t PCHUNK = 1024;  // active-list positions per wave in the infectedFrom kernels
+#ifndef SWIM_PCHUNK
+#define SWIM_PCHUNK 1024
+#endif
+constexpr uint32_t PCHUNK = SWIM_PCHUNK;  // active-list positions per wave in the infectedFrom kernels
+static_assert(PCHUNK % 64u == 0u, "SWIM_PCHUNK: a multiple of 64");
 
 __device__ __forceinline__ void ifrom_overflow(const KP& P, uint32_t why) {
   atomicOr(&P.ctl->overflow, OV_IFROM);
