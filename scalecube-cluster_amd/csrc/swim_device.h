@@ -488,7 +488,7 @@ __device__ __forceinline__ void dq_window(const KP& P, uint32_t p, uint32_t* lo,
 }
 constexpr uint32_t DQ_PAIR = 0x10000u;   // k_gossip_select: the chosen peer delivered delayed messages
 #ifndef SWIM_PCHUNK
-#define SWIM_PCHUNK 1024
+#define SWIM_PCHUNK 256  // (1,024: C2 4.64 -> 4.25 ms per period at 256, C4's schedule and C3 a little faster too)
 #endif
 constexpr uint32_t PCHUNK = SWIM_PCHUNK;  // active-list positions per wave in the infectedFrom kernels
 static_assert(PCHUNK % 64u == 0u, "SWIM_PCHUNK: a multiple of 64");

@@ -483,7 +483,16 @@ __global__ void __launch_bounds__(CS_THREADS) k_commit(KP P, const uint4* stg, u
           }
         }
       }
-      __syncthreads();
+      // a stage with j < 64 pairs elements of one wave (element i belongs to thread i mod 1,024):
+      // the next stage of the same k reads only what this wave wrote, so a wave-level barrier
+      // does; the workgroup barrier is needed after j >= 64 and at the end of each k
+      if (j >= 64u || j == 1u) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
   static_assert(CS_SMALL <= CS_PER * CS_THREADS, "k_commit: one commit_block covers the LDS sort");
   const uint32_t nslots = commit_block(
