@@ -267,3 +267,30 @@ def _overflow_worker(rank, world, port):
 def test_overflow_on_one_rank_fails_every_rank():
     """An overflow only one shard detects raises SWIM_EOVERFLOW on both ranks (no hang)."""
     mp.spawn(_overflow_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _leave_mismatch_worker(rank, world, port):
+    from swimhip import ClusterConfig, SwimCluster
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        c = ShardedSwimCluster(ClusterConfig.defaultLocalConfig(), 64, seed=3)
+        c.step(2)
+        if rank == 0:  # past the collective argument check: only rank 0's library counts the leave
+            SwimCluster.leave(c, [5])
+        with pytest.raises(SwimError) as ei:
+            c.step(4)
+        assert ei.value.code == -22
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_leave_on_one_rank_fails_every_rank():
+    """swim_leave sets the layout of every later commit-exchange block (a {gossips, stopped} header),
+    so the library's status all-gather carries each rank's leave count: a rank that left members the
+    others did not fails every rank with SWIM_EINVAL at the next exchange, instead of one rank
+    reading another's header as gossips."""
+    mp.spawn(_leave_mismatch_worker, args=(2, _free_port()), nprocs=2, join=True)
