@@ -561,12 +561,16 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 1, "k_gossip_pull", [&] {
+          // small shards: a workgroup per receiver, its 4 waves splitting the active list
+          const bool split = nloc <= PULL_SPLIT_N;
           if (P.dq)
             hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
           else if (P.loss_mode == 1u)  // the loss draws' instance (§3.16's split, for registers)
-            hipLaunchKernelGGL(k_gossip_pull_loss, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(split ? k_gossip_pull_loss_s4 : k_gossip_pull_loss, dim3(split ? nloc : blocks_for(nloc, 4)),
+                               dim3(256), 0, s, P);
           else
-            hipLaunchKernelGGL(k_gossip_pull, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(split ? k_gossip_pull_s4 : k_gossip_pull, dim3(split ? nloc : blocks_for(nloc, 4)),
+                               dim3(256), 0, s, P);
         });
         timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
@@ -781,14 +785,16 @@ int tr_alltoallv(swim_handle* h, const uint64_t* sb, const uint64_t* rb) {
   return SWIM_OK;
 }
 
-// The status all-gather every exchange starts with: row = {error code, op, send words / counts}.
-// Every rank learns every rank's counts (an all-to-all-v needs them before the data moves) and
-// every error: a failure one rank detects fails all of them at the same exchange, never a hang.
+// The status all-gather every exchange starts with: row = {error code, op | swim_leave calls << 32,
+// send words / counts}. Every rank learns every rank's counts (an all-to-all-v needs them before the
+// data moves) and every error: a failure one rank detects fails all of them at the same exchange,
+// never a hang. The leave count rides along because it sets the layout of every commit block (a
+// {gossips, stopped} header once any member left): ranks that disagree fail instead of misreading.
 int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t>* rows) {
   const uint32_t W = h->world, R = 2u + W;
   std::vector<uint64_t> row(R, 0ull);
   row[0] = (uint64_t)(int64_t)code;
-  row[1] = code ? ~0ull : x.op;
+  row[1] = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | x.op);
   if (!code && x.op == SWIM_X_ALLGATHER) row[2] = x.send_words;
   if (!code && x.op == SWIM_X_ALLTOALLV)
     for (uint32_t q = 0; q < W; ++q) row[2 + q] = x.send_counts[q];
@@ -823,8 +829,11 @@ int tr_period(swim_handle* h) {
         if (rc) return fail(h, rc, mine);
         return fail(h, (int)(int64_t)rows[(size_t)q * R], "shard exchange: rank " + std::to_string(q) + " failed");
       }
-    for (uint32_t q = 1; q < W; ++q)
+    for (uint32_t q = 1; q < W; ++q) {
+      if ((rows[(size_t)q * R + 1] >> 32) != (rows[1] >> 32))
+        return fail(h, SWIM_EINVAL, "shard exchange: ranks disagree on swim_leave calls (rank " + std::to_string(q) + ")");
       if (rows[(size_t)q * R + 1] != rows[1]) return fail(h, SWIM_EINVAL, "shard exchange: ranks out of step");
+    }
     if (x.op == SWIM_X_DONE) return SWIM_OK;
     if (x.op == SWIM_X_ALLGATHER) {
       uint64_t m = 0;

@@ -1634,6 +1634,9 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
   __shared__ uint32_t s_lk[4][64];  // the MIXED pass's lack bits, by owner lane
   __shared__ uint2 s_mw[4][4 * SEL_BATCH][64];  // {list entry, holdings word} of this step's MIXED entries
+  // this step's window words by (entry, lane): a lane stores its quads' words to wb as 16-B stores
+  // (one 4-B store per MIXED position, from whichever lane finished it, cost ~20 B of HBM writes each)
+  __shared__ uint32_t s_win[4][4 * SEL_BATCH][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t m = P.row0 + blockIdx.x * 4u + w;
@@ -1712,6 +1715,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
       }
       uint32_t mixm = 0;  // entries whose infection rounds must be read
       uint32_t lackm = 0;  // entries (sent words) in which the member lacks a live gossip
+      uint32_t wbm = 0;  // entries at globally MIXED list positions: their window words go to wb
 #pragma unroll 1
       for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
         // quad jq's values by select chains (no dynamically indexed register arrays: no scratch)
@@ -1738,6 +1742,8 @@ __device__ __forceinline__ void select_body(const KP& P) {
         const uint32_t live = k < n_act ? range_mask(wi << 5, lo, hi) : 0u;
         const uint32_t held = word & live;
         uint32_t clear = 0, win = 0;
+        s_win[w][j][lane] = 0u;
+        if (k < n_act && wc == WC_MIXED) wbm |= 1u << j;
         if (held) {
           uint32_t wcm = wc, scm = sc;
           if (wcm == WC_MIXED || scm == WC_MIXED) {
@@ -1766,7 +1772,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
           // read directly (k_gossip_pull runs before any holdings change); only MIXED words need wb
           if (wc == WC_MIXED) {
             ++winw;
-            wbr[DBG_IDX(k, W32, "select wbr")] = win;
+            s_win[w][j][lane] = win;
           }
           win_l |= win != 0u;
           winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
@@ -1780,7 +1786,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
       };
       // a MIXED entry (list entry e, holdings word, list position k) from its 32 infection rounds:
       // sweep, window, age bounds, wb; true when the member lacks a live gossip of the word
-      auto finish_mixed = [&](uint32_t e, uint32_t word, uint32_t k, uint4 d0, uint4 d1) -> bool {
+      auto finish_mixed = [&](uint32_t e, uint32_t word, uint32_t j, uint32_t o, uint4 d0, uint4 d1) -> bool {
         const uint32_t wi = w_beg + (e & ACT_OFF_MASK);
         const uint32_t wc = (e >> 26) & 3u;
         const uint32_t ws = wmod(P, wi);
@@ -1819,7 +1825,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         if (wc != WC_NONE) {
           if (wc == WC_MIXED) {
             ++winw;
-            wbr[DBG_IDX(k, W32, "select wbr")] = win;
+            s_win[w][j][o] = win;
           }
           win_l |= win != 0u;
           winbits += slot_gossips(P, ws, win);  // GossipRequests: one per gossip
@@ -1844,7 +1850,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
             const uint2 mw = s_mw[w][j][o];
             uint4 d0, d1;
             hd_ld(mw.x, d0, d1);
-            if (finish_mixed(mw.x, mw.y, k0 + 256u * (j >> 2) + 4u * o + (j & 3u), d0, d1))
+            if (finish_mixed(mw.x, mw.y, j, o, d0, d1))
               atomicOr(&s_lk[w][o], 1u << j);
           }
         }
@@ -1852,6 +1858,12 @@ __device__ __forceinline__ void select_body(const KP& P) {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         lackm |= s_lk[w][lane];
       }
+#pragma unroll
+      for (uint32_t jq = 0; jq < SEL_BATCH; ++jq)  // the window words of the lane's quads (positions < n_act <= W32)
+        if ((wbm >> (4u * jq)) & 0xFu)
+          *reinterpret_cast<uint4*>(wbr + DBG_IDX(k0 + 256u * jq + 4u * lane, W32 - 3u, "select wb4")) =
+              make_uint4(s_win[w][4u * jq][lane], s_win[w][4u * jq + 1u][lane], s_win[w][4u * jq + 2u][lane],
+                         s_win[w][4u * jq + 3u][lane]);
       if (lack_ok) {  // positions k0 + 256 jq + 4 lane + i: eight lanes fill one bitmap word
 #pragma unroll
         for (uint32_t jq = 0; jq < SEL_BATCH; ++jq) {
@@ -2346,24 +2358,37 @@ constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
 // common instance keeps the one-at-a-time loop and 4 waves per SIMD).
-template <bool DQ, bool LOSS>
+// SPLIT = 1: one wave per receiver, 4 per workgroup. SPLIT = 4 (small shards, where one wave per
+// receiver leaves the SIMDs a few waves each): the workgroup's 4 waves share one receiver, each
+// walking every fourth quad of the active list; receipts meet in the LDS summary, the receiver's
+// totals are taken after a workgroup barrier (every branch on the receiver is workgroup-uniform).
+#ifndef SWIM_PULL_SPLIT_N
+#define SWIM_PULL_SPLIT_N 16384
+#endif
+constexpr uint32_t PULL_SPLIT_N = SWIM_PULL_SPLIT_N;  // shards of at most this many rows pull 4 waves per receiver
+template <bool DQ, bool LOSS, uint32_t SPLIT = 1u>
 __device__ __forceinline__ void pull_body(const KP& P) {
+  static_assert(SPLIT == 1u || (SPLIT == 4u && !DQ), "pull_body: one wave per receiver, or a workgroup (no delays)");
   SWIM_GUARD(P);
-  __shared__ uint32_t s_sum[4][NSUM];  // which active words got receipts (bit k of the list)
+  __shared__ uint32_t s_sum[4 / SPLIT][NSUM];  // which active words got receipts (bit k of the list)
   __shared__ uint32_t s_snd[4][64];  // the current chunk of sender entries (read in divergent loops)
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
+  __shared__ uint32_t s_rcpt[4 / SPLIT];  // SPLIT > 1: the receiver's receipts over its waves
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t p = P.row0 + blockIdx.x * 4u + (threadIdx.x >> 6);
-  if (p >= P.row0 + P.nloc) return;  // whole wave
+  const uint32_t part = (threadIdx.x >> 6) % SPLIT;  // this wave's share of the receiver's list quads
+  const uint32_t p = P.row0 + blockIdx.x * (4u / SPLIT) + (threadIdx.x >> 6) / SPLIT;
+  if (p >= P.row0 + P.nloc) return;  // whole wave (SPLIT > 1: the whole workgroup)
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t W32 = P.GC >> 5;
   const uint32_t deg = P.in_cnt[p];
   uint32_t probes = 0, receipts = 0, words = 0;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
-  uint32_t* sum = s_sum[threadIdx.x >> 6];
+  uint32_t* sum = s_sum[(threadIdx.x >> 6) / SPLIT];
   const uint32_t nsw = (n_act + 31u) >> 5;
   if ((deg || DQ) && P.alive[p] && n_act) {  // a stopped transport loses every message
+    // (SPLIT > 1: deg, liveness and the list length are the receiver's, so every wave of the
+    // workgroup takes this branch or none does, and its barriers are uniform)
     uint32_t* hbr = P.hb + lrow(P, p) * W32;
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     if (DQ && lane == 0)  // where this round's pushes start (dq_window)
@@ -2372,7 +2397,11 @@ __device__ __forceinline__ void pull_body(const KP& P) {
     const uint32_t* lackr =
         (!(DQ && P.delay_on) && nsw <= P.nsumw && P.lack_round[p] == P.round) ? P.lack + lrow(P, p) * P.nsumw : nullptr;
     if (nsw <= P.nsumw)
-      for (uint32_t t = lane; t < nsw; t += 64u) sum[t] = 0u;
+      for (uint32_t t = SPLIT > 1u ? threadIdx.x : lane; t < nsw; t += 64u * SPLIT) sum[t] = 0u;
+    if (SPLIT > 1u) {
+      if (threadIdx.x == 0) s_rcpt[0] = 0u;
+      __syncthreads();
+    }
     const uint32_t n_ov = deg > INCAP ? P.ctl->n_inov : 0u;
     uint32_t ov_pos = 0;
     for (uint32_t done = 0; done < deg;) {
@@ -2567,7 +2596,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           }
         if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
       };
-      for (uint32_t kq = 4u * lane; kq < n_act; kq += 256u) {
+      for (uint32_t kq = 4u * lane + 256u * part; kq < n_act; kq += 256u * SPLIT) {
         // the receiver's own select pass marked the sent words it lacks something in: skip the
         // rest without reading the list or the holdings (most of them once a storm has spread;
         // compacting the marked quads first measured no faster: the visits are latency-bound)
@@ -2606,8 +2635,13 @@ __device__ __forceinline__ void pull_body(const KP& P) {
         }
       }
     }
-    const uint32_t total = wave_sum(receipts);
-    if (lane == 0 && total) {
+    uint32_t total = wave_sum(receipts);
+    if (SPLIT > 1u) {  // the receiver's waves: receipts and summary bits meet in LDS
+      if (lane == 0 && total) atomicAdd(&s_rcpt[0], total);
+      __syncthreads();
+      total = s_rcpt[0];
+    }
+    if (lane == 0 && part == 0u && total) {
       const uint32_t idx = atomicAdd(&P.ctl->n_alist, 1u);
       P.alist[DBG_IDX(2ull * idx, 2ull * P.N, "pull alist")] = p;
       P.alist[2 * idx + 1] = total;
@@ -2615,10 +2649,11 @@ __device__ __forceinline__ void pull_body(const KP& P) {
     if (total && nsw <= P.nsumw) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      for (uint32_t t = lane; t < nsw; t += 64u) P.nsum[lrow(P, p) * P.nsumw + t] = sum[t];
+      for (uint32_t t = SPLIT > 1u ? threadIdx.x : lane; t < nsw; t += 64u * SPLIT) P.nsum[lrow(P, p) * P.nsumw + t] = sum[t];
     }
   }
-  if (lane == 0) P.in_cnt[p] = 0u;  // ready for the next round
+  if (SPLIT > 1u) __syncthreads();  // (the receiver's every wave) all have read in_cnt
+  if (lane == 0 && part == 0u) P.in_cnt[p] = 0u;  // ready for the next round
   add_stat(P, ST_G_PROBES, probes);  // (receipts are counted by k_gossip_apply, in gossips)
   add_stat(P, ST_G_PULLW, words);
 }
@@ -2633,6 +2668,11 @@ __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(
   pull_body<false, true>(P);
 }
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_dq(KP P) { pull_body<true, true>(P); }
+// small shards: a workgroup per receiver
+__global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull_s4(KP P) { pull_body<false, false, 4u>(P); }
+__global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss_s4(KP P) {
+  pull_body<false, true, 4u>(P);
+}
 
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
@@ -2979,10 +3019,15 @@ __device__ __forceinline__ void receive_word(const KP& P, uint32_t p, uint32_t w
 #endif
 constexpr uint32_t AW_SPILL = SWIM_APPLY_WSPILL;  // spilled subjects a wave lists per receiver
 constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per workgroup
+// 16-B entry-id loads in flight per lane on long ranges: 2 with 16-bit ids (8 per load), 4 with 32-bit
+// ids (large dictionaries: the half/half partition at 16,384 44.6 -> 40.3 ms per period; C3, on 16-bit
+// ids, 13.90 -> 14.11 at 4)
 #ifndef SWIM_AW_VILP
 #define SWIM_AW_VILP 2
 #endif
-constexpr uint32_t AW_VILP = SWIM_AW_VILP;        // 16-B entry-id loads in flight per lane (long ranges)
+#ifndef SWIM_AW_VILP32
+#define SWIM_AW_VILP32 4
+#endif
 #ifndef SWIM_AW_QILP
 #define SWIM_AW_QILP 2
 #endif
@@ -3014,6 +3059,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
   const uint32_t bw = (min(P.ctl->d_hw, P.dsids) * DICT_WAYS + 31u) >> 5;  // bitmap words in use
   const uint32_t dids = P.dsids * DICT_WAYS;
   constexpr uint32_t IDG = C16 ? 8u : 4u;  // entry ids per 16-B load
+  constexpr uint32_t AW_VILP = C16 ? SWIM_AW_VILP : SWIM_AW_VILP32;
   // ids at or above dlim are no entry (16 bits: the two sentinels top an 8,192-block dictionary)
   const uint32_t dlim = C16 ? min(dids, ID16_USER) : dids;
   // a live record has no dictionary entry: the subjects of such records merge through the spill table
