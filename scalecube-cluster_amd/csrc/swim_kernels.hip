@@ -3035,6 +3035,13 @@ constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flig
 #ifndef SWIM_AW_LONG
 #define SWIM_AW_LONG 256
 #endif
+// the merge pass tests AW_MC groups of 512 bitmap words (their merge marks) before it flattens their
+// blocks to merge together (fewer dependent rounds of loads per receiver than one group at a time)
+#ifndef SWIM_AW_MC
+#define SWIM_AW_MC 1
+#endif
+constexpr uint32_t AW_MC = SWIM_AW_MC;
+static_assert(AW_MC >= 1u && AW_MC <= 4u, "SWIM_AW_MC: 1..4 groups of 512 bitmap words");
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
 constexpr uint32_t AW_LONG = SWIM_AW_LONG;
@@ -3328,16 +3335,20 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     // and generations are one 16-B load each, consecutive lanes consecutive lines), so the blocks whose set entries are all marked drop out before the per-block pass.
     const uint4* mrow4 = reinterpret_cast<const uint4*>(mrow);
     const uint4* gen4 = reinterpret_cast<const uint4*>(P.d_gen);
-    for (uint32_t t0 = 0; t0 < bw; t0 += 512u) {
-      uint32_t bm = 0u;   // bit 4u + j: word t0 + 64u + lane has set entries in its block j, not all marked
-      uint32_t nzw = 0u;  // bit u: word t0 + 64u + lane has set entries
+    // AW_MC groups of 512 bitmap words are tested, then their blocks to merge flattened together
+    for (uint32_t t0 = 0; t0 < bw; t0 += 512u * AW_MC) {
+      uint32_t bm[AW_MC];  // bit 4u + j of bm[ci]: word t0 + 512 ci + 64u + lane has set entries in its block j, not all marked
+      uint32_t nzw = 0u;   // bit 8 ci + u: that word has set entries
+#pragma unroll
+      for (uint32_t ci = 0; ci < AW_MC; ++ci) {
+      bm[ci] = 0u;
 #pragma unroll
       for (uint32_t h2 = 0; h2 < 4u; ++h2) {  // (two words in flight per step: registers)
         uint32_t wv[2];
         uint4 mv[2], gv[2];
 #pragma unroll
         for (uint32_t uu = 0; uu < 2u; ++uu) {
-          const uint32_t t = t0 + 64u * (2u * h2 + uu) + lane;
+          const uint32_t t = t0 + 512u * ci + 64u * (2u * h2 + uu) + lane;
           wv[uu] = t < bw ? s_bm[t] : 0u;
           mv[uu] = wv[uu] ? mrow4[t] : make_uint4(0u, 0u, 0u, 0u);
           gv[uu] = wv[uu] ? gen4[t] : make_uint4(0u, 0u, 0u, 0u);
@@ -3345,7 +3356,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #pragma unroll
         for (uint32_t uu = 0; uu < 2u; ++uu) {
           const uint32_t u = 2u * h2 + uu;
-          if (wv[uu]) nzw |= 1u << u;
+          if (wv[uu]) nzw |= 1u << (8u * ci + u);
           const uint32_t mk[4] = {mv[uu].x, mv[uu].y, mv[uu].z, mv[uu].w};
           const uint32_t gg[4] = {gv[uu].x, gv[uu].y, gv[uu].z, gv[uu].w};
 #pragma unroll
@@ -3355,19 +3366,40 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
             if ((mk[j] >> 8) == (gg[j] & GEN_MASK) && (m & ~mk[j] & 0xFFu) == 0u)
               ++nskip;  // every set entry already found not to override the present cell (MPI:489)
             else
-              bm |= 1u << (4u * u + j);
+              bm[ci] |= 1u << (4u * u + j);
           }
         }
       }
+      }
+      uint32_t cnt = 0u;
+#pragma unroll
+      for (uint32_t ci = 0; ci < AW_MC; ++ci) cnt += (uint32_t)__popc(bm[ci]);
       uint32_t tot;
-      const uint32_t off = wave_excl_scan((uint32_t)__popc(bm), &tot);
+      const uint32_t off = wave_excl_scan(cnt, &tot);
       for (uint32_t q0 = 0; q0 < tot; q0 += 64u) {
         const uint32_t q = q0 + lane;
-        const uint32_t o = wave_owner_at(off, (uint32_t)__popc(bm), q0);
-        const uint32_t bo = __shfl(bm, (int)o, 64), oo = __shfl(off, (int)o, 64);
+        const uint32_t o = wave_owner_at(off, cnt, q0);
+        const uint32_t oo = __shfl(off, (int)o, 64);
+        // the owner's (q - oo)-th block: which of its AW_MC masks, then which bit
+        uint32_t kk = q - oo, bo = 0u, cs = 0u;
+        bool found = false;
+#pragma unroll
+        for (uint32_t ci = 0; ci < AW_MC; ++ci) {
+          const uint32_t bc = __shfl(bm[ci], (int)o, 64);  // (every lane shuffles)
+          const uint32_t c = (uint32_t)__popc(bc);
+          if (!found) {
+            if (kk < c) {
+              bo = bc;
+              cs = ci;
+              found = true;
+            } else {
+              kk -= c;
+            }
+          }
+        }
         if (q < tot) {
-          const uint32_t b = kth_set_bit(bo, q - oo);
-          const uint32_t t = t0 + 64u * (b >> 2) + o, j = b & 3u;
+          const uint32_t b = kth_set_bit(bo, kk);
+          const uint32_t t = t0 + 512u * cs + 64u * (b >> 2) + o, j = b & 3u;
           const uint32_t base = 32u * t + 8u * j;  // entry id of the block's way 0
           const uint32_t sid = base / DICT_WAYS;
           const uint32_t m = (s_bm[t] >> (8u * j)) & 0xFFu;
@@ -3399,8 +3431,8 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
       wsync();  // every lane has read its blocks' bits
 #pragma unroll
-      for (uint32_t u = 0; u < 8u; ++u)
-        if ((nzw >> u) & 1u) s_bm[t0 + 64u * u + lane] = 0u;
+      for (uint32_t u = 0; u < 8u * AW_MC; ++u)
+        if ((nzw >> u) & 1u) s_bm[t0 + 512u * (u >> 3) + 64u * (u & 7u) + lane] = 0u;
     }
     wsync();
     APPLYB_MARK(2);
