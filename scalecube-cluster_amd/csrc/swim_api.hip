@@ -74,6 +74,12 @@ struct swim_handle {
   uint32_t apply_blocks = 1, apply_blocks_b = 1, apply_waves_b = 1;
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
+  size_t apply_lds_s4 = 0;                 // k_gossip_apply_b16_s4: one bitmap per workgroup
+  // shards of at most this many rows select, pull and apply with a workgroup's 4 waves per member:
+  // one wave per member would leave the chip's SIMDs at most 4 waves each (16 per CU; C2's 4,096
+  // members on 256 CUs gain, 65,536 lose: DESIGN.md §6.5)
+  uint32_t split_rows = 4096;
+  uint32_t apply_blocks_s4 = 0;
   uint32_t CC = 0;  // record ring of the gossip batches
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
   uint32_t* crash_ids = nullptr;  // [N] the members one swim_crash call stops (allocated on first use)
@@ -474,7 +480,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, "k_gossip_select", [&] {
-          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+          if (nloc <= std::min(SEL_SPLIT_N, h->split_rows))  // small shards: a workgroup per member (its 4 waves share the holdings pass)
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4_s4 : k_gossip_select_s4, dim3(nloc), dim3(256), 0, s, P);
+          else
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
         });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
@@ -562,7 +571,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 9, "k_gossip_inhist", [&] { hipLaunchKernelGGL(k_gossip_inhist, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P); });
         timed(h, 1, "k_gossip_pull", [&] {
           // small shards: a workgroup per receiver, its 4 waves splitting the active list
-          const bool split = nloc <= PULL_SPLIT_N;
+          const bool split = nloc <= std::min(PULL_SPLIT_N, h->split_rows);
           if (P.dq)
             hipLaunchKernelGGL(k_gossip_pull_dq, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
           else if (P.loss_mode == 1u)  // the loss draws' instance (§3.16's split, for registers)
@@ -577,7 +586,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           // with the record dictionary (gossip batching on, the default) the batched apply runs whether
           // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject
           // runs it takes as run tops (C4's lossy storm: apply 373 -> 104 ms per 20 periods, §6.4)
-          if (P.batched || h->dict_on)
+          // (small shards with 16-bit ids: a workgroup of 4 waves per receiver, one bitmap per workgroup)
+          if ((P.batched || h->dict_on) && P.cid16 && nloc <= std::min(APPLY_SPLIT_N, h->split_rows))
+            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b16_h4_s4 : k_gossip_apply_b16_s4, dim3(h->apply_blocks_s4),
+                               dim3(64 * AW_WAVES), h->apply_lds_s4, s, P);
+          else if (P.batched || h->dict_on)
             hipLaunchKernelGGL(P.cid16 ? (P.hd4 ? k_gossip_apply_b16_h4 : k_gossip_apply_b16)
                                        : (P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b),
                                dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b),
@@ -978,6 +991,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     h->apply_lds = 4ull * (2ull * (1ull << lg) + SPILL_CAP + (SWIM_APPLY_PAIR ? 2u : 1u) * pres_words);
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
+    h->split_rows = 16u * (uint32_t)std::max(1, cus);
     const uint32_t per_cu = h->apply_lds <= 72u * 1024u ? 2u : 1u;  // 160 KiB LDS, 2,048 threads per CU
     h->apply_blocks = (uint32_t)std::max(1, cus) * per_cu;
     // the batch-slot variant: one receiver per wave, up to AW_WAVES waves per workgroup, each with
@@ -996,6 +1010,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
                           reinterpret_cast<const void*>(&k_gossip_apply_b16),
                           reinterpret_cast<const void*>(&k_gossip_apply_b16_h4)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
+    // the split instance: 4 waves and one bitmap per workgroup, as many workgroups as fit a CU (8 by
+    // its 2,048 threads) on every CU
+    h->apply_lds_s4 = wave_lds;
+    h->apply_blocks_s4 = (uint32_t)std::max(1, cus) *
+                         std::max<uint32_t>(1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / wave_lds)));
+    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b16_s4), reinterpret_cast<const void*>(&k_gossip_apply_b16_h4_s4)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_s4);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_slot_bm), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)P.dsids);
   }

@@ -1626,9 +1626,20 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
   return pos;
 }
 
-template <bool HD4>
+// SPLIT = 4 (a build knob, off by default): the workgroup's 4 waves share one member's holdings pass
+// (every fourth step of its active list); their sweep counts, GossipRequest counts and window flags
+// meet in LDS, and the first wave alone goes on to the peer choice, infectedFrom and the
+// registrations. Measured slower on C2's 4,096 members (select 0.41 -> 0.46 ms per period; the
+// parity file green through it), unlike the pull's split.
+#ifndef SWIM_SEL_SPLIT_N
+#define SWIM_SEL_SPLIT_N 0
+#endif
+constexpr uint32_t SEL_SPLIT_N = SWIM_SEL_SPLIT_N;  // shards of at most this many rows (and 16 per CU) select 4 waves per member
+template <bool HD4, uint32_t SPLIT = 1u>
 __device__ __forceinline__ void select_body(const KP& P) {
+  static_assert(SPLIT == 1u || SPLIT == 4u, "select_body: a wave or a workgroup per member");
   SWIM_GUARD(P);
+  __shared__ uint32_t s_red[4][4];  // SPLIT > 1: per wave {swept, GossipRequests, window non-empty}
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
@@ -1639,12 +1650,13 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint32_t s_win[4][4 * SEL_BATCH][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
-  const uint32_t m = P.row0 + blockIdx.x * 4u + w;
+  const uint32_t part = w % SPLIT;  // this wave's share of the holdings pass
+  const uint32_t m = P.row0 + blockIdx.x * (4u / SPLIT) + w / SPLIT;
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   if (lo >= hi) {  // no live gossip anywhere (a quiet round): nothing is held, sent or swept
-    if (lane == 0 && m < P.row0 + P.nloc) P.npeers[m] = 0u;
+    if (lane == 0 && part == 0u && m < P.row0 + P.nloc) P.npeers[m] = 0u;
     if (m == P.dbg_watch && lane == 0) {
       uint32_t* L = P.dbg_log + (r & 255u) * 8u;
       L[0] = r;
@@ -1684,7 +1696,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
     // load each, all issued together (bytes in flight). Words whose class the member's own age
     // bounds settle are finished in a fully unrolled pass (no dynamically indexed register
     // arrays, so nothing goes to scratch); the few left MIXED are finished one by one from a mask.
-    for (uint32_t k0 = 0; k0 < n_act; k0 += 256u * SEL_BATCH) {
+    for (uint32_t k0 = 256u * SEL_BATCH * part; k0 < n_act; k0 += 256u * SEL_BATCH * SPLIT) {
       uint32_t ev[4 * SEL_BATCH], wv[4 * SEL_BATCH];
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
@@ -1876,7 +1888,30 @@ __device__ __forceinline__ void select_body(const KP& P) {
         }
       }
     }
-    if (lack_ok && lane == 0) P.lack_round[m] = r;
+    if (lack_ok && lane == 0 && part == 0u) P.lack_round[m] = r;
+  }
+  if (SPLIT > 1u) {  // (uniform: every wave of the workgroup is the same member's)
+    const uint32_t a = wave_sum(nclear), b = wave_sum(winbits), c = __any(win_l) ? 1u : 0u;
+    if (lane == 0) {
+      s_red[w][0] = a;
+      s_red[w][1] = b;
+      s_red[w][2] = c;
+    }
+    add_stat(P, ST_G_HDREAD, hdw);
+    add_stat(P, ST_G_WINW, winw);
+    hdw = winw = 0u;
+    __syncthreads();
+    if (part != 0u) return;  // the first wave goes on alone (no barrier below)
+    nclear = winbits = 0u;
+    win_l = false;
+    if (lane == 0) {
+#pragma unroll
+      for (uint32_t q = 0; q < SPLIT; ++q) {
+        nclear += s_red[w + q][0];
+        winbits += s_red[w + q][1];
+        win_l |= s_red[w + q][2] != 0u;
+      }
+    }
   }
   SEL_MARK(0);
   uint32_t np = 0;
@@ -2046,6 +2081,9 @@ __device__ __forceinline__ void select_body(const KP& P) {
 }
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) { select_body<false>(P); }
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) { select_body<true>(P); }
+// small shards: a workgroup per member
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_s4(KP P) { select_body<false, 4u>(P); }
+__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4_s4(KP P) { select_body<true, 4u>(P); }
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
 
@@ -2365,7 +2403,7 @@ constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a 
 #ifndef SWIM_PULL_SPLIT_N
 #define SWIM_PULL_SPLIT_N 16384
 #endif
-constexpr uint32_t PULL_SPLIT_N = SWIM_PULL_SPLIT_N;  // shards of at most this many rows pull 4 waves per receiver
+constexpr uint32_t PULL_SPLIT_N = SWIM_PULL_SPLIT_N;  // shards of at most this many rows (and 16 per CU, swim_handle::split_rows) pull 4 waves per receiver
 template <bool DQ, bool LOSS, uint32_t SPLIT = 1u>
 __device__ __forceinline__ void pull_body(const KP& P) {
   static_assert(SPLIT == 1u || (SPLIT == 4u && !DQ), "pull_body: one wave per receiver, or a workgroup (no delays)");
@@ -3053,12 +3091,32 @@ static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range
 #define SWIM_AW_MINW 4  // (the LDS bitmap caps the 8,192-block dictionary at 4 waves per SIMD anyway:
                         // registers beyond 128 would only lower that)
 #endif
-template <bool HD4, bool C16>
+// SPLIT = 1: a wave per receiver. SPLIT = 4 (a build knob, off by default): the workgroup's 4 waves
+// share one receiver and one LDS bitmap, each taking every fourth group of receipt words and every
+// fourth group of bitmap words; workgroup barriers between the phases (every branch on the receiver is
+// workgroup-uniform). Measured slower on C2's 4,096 members (apply 0.70 -> 1.13 ms per period: the
+// barriers, and a 4,096-block dictionary's bitmap is two groups, so two waves merge; the parity file
+// green through it).
+#ifndef SWIM_APPLY_SPLIT_N
+#define SWIM_APPLY_SPLIT_N 0
+#endif
+constexpr uint32_t APPLY_SPLIT_N = SWIM_APPLY_SPLIT_N;  // shards of at most this many rows (and 16 per CU) apply 4 waves per receiver
+template <bool HD4, bool C16, uint32_t SPLIT = 1u>
 __device__ __forceinline__ void apply_b_body(const KP& P) {
+  static_assert(SPLIT == 1u || SPLIT == 4u, "apply_b_body: a wave or a workgroup per receiver");
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  uint32_t* s_bm = s_dyn + wv * aw_words(P.dsids);  // entry bitmap: all-zero between receivers
+  const uint32_t part = wv % SPLIT;  // this wave's share of the receiver
+  auto bsync = [] {  // the receiver's waves (SPLIT > 1: the workgroup)
+    if (SPLIT > 1u) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+  };
+  uint32_t* s_bm = s_dyn + (wv / SPLIT) * aw_words(P.dsids);  // entry bitmap: all-zero between receivers
   uint32_t* s_spl = s_bm + P.dsids / 4u;
   uint32_t* s_misc = s_spl + AW_SPILL;  // [0] spilled subjects
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
@@ -3090,7 +3148,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #else
 #define APPLYB_MARK(q)
 #endif
-  for (uint32_t t = lane; t < bw; t += 64u) s_bm[t] = 0u;
+  for (uint32_t t = lane + 64u * part; t < bw; t += 64u * SPLIT) s_bm[t] = 0u;
 #ifdef SWIM_APPLY_PROF
   unsigned long long t_w = 0, t_big = 0, t_short = 0, tq = 0;  // words / long ranges / short ranges
 #define APPLYB_SUB(acc)                \
@@ -3103,15 +3161,19 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #define APPLYB_SUB(acc)
 #endif
   APPLYB_MARK(0);
-  for (uint32_t li = blockIdx.x * nwv + wv; li < n_list; li += gridDim.x * nwv) {
+  if (SPLIT > 1u) __syncthreads();  // the bitmap is clear
+  for (uint32_t li = (blockIdx.x * nwv + wv) / SPLIT; li < n_list; li += gridDim.x * nwv / SPLIT) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t nsw = (n_act + 31u) >> 5;
     const bool summ = nsw <= P.nsumw;
     const uint32_t* sumr = P.nsum + lrow(P, p) * P.nsumw;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
-    if (lane == 0) s_misc[0] = 0u;
-    wsync();
+    if (lane == 0 && part == 0u) {
+      s_misc[0] = 0u;
+      s_misc[1] = 0u;
+    }
+    bsync();
     bool rowscan = false;  // the spill list overflowed: the round's claimed slots are scanned at the end
     uint32_t ent = 0, rc = 0;
     // lattice max into the receiver's spill-table cell; the key's claimer lists its slot
@@ -3294,9 +3356,9 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
     };
     if (!summ) {
-      for (uint32_t it0 = 0; it0 < n_act; it0 += 64u) word(it0 + lane < n_act ? it0 + lane : NONE);
+      for (uint32_t it0 = 64u * part; it0 < n_act; it0 += 64u * SPLIT) word(it0 + lane < n_act ? it0 + lane : NONE);
     } else {  // the summary's set bits, flattened across the wave
-      for (uint32_t c0 = 0; c0 < nsw; c0 += 64u) {
+      for (uint32_t c0 = 64u * part; c0 < nsw; c0 += 64u * SPLIT) {
         const uint32_t sb = c0 + lane < nsw ? sumr[c0 + lane] : 0u;
         uint32_t tot;
         const uint32_t off = wave_excl_scan((uint32_t)__popc(sb), &tot);
@@ -3315,7 +3377,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         nrecs += E;
       }
     }
-    wsync();
+    bsync();  // every record of the receiver is in the bitmap
     APPLYB_MARK(1);
     const uint32_t snap = P.cnt[p];
     uint32_t* mrow = P.dmark + lrow(P, p) * P.dsids;  // the receiver's merge marks
@@ -3336,7 +3398,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     const uint4* mrow4 = reinterpret_cast<const uint4*>(mrow);
     const uint4* gen4 = reinterpret_cast<const uint4*>(P.d_gen);
     // AW_MC groups of 512 bitmap words are tested, then their blocks to merge flattened together
-    for (uint32_t t0 = 0; t0 < bw; t0 += 512u * AW_MC) {
+    for (uint32_t t0 = 512u * AW_MC * part; t0 < bw; t0 += 512u * AW_MC * SPLIT) {
       uint32_t bm[AW_MC];  // bit 4u + j of bm[ci]: word t0 + 512 ci + 64u + lane has set entries in its block j, not all marked
       uint32_t nzw = 0u;   // bit 8 ci + u: that word has set entries
 #pragma unroll
@@ -3434,14 +3496,15 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       for (uint32_t u = 0; u < 8u * AW_MC; ++u)
         if ((nzw >> u) & 1u) s_bm[t0 + 512u * (u >> 3) + 64u * (u & 7u) + lane] = 0u;
     }
-    wsync();
+    if (SPLIT > 1u && __any(rowscan) && lane == 0) s_misc[1] = 1u;
+    bsync();  // every merge of the receiver is done, its spill list complete
     APPLYB_MARK(2);
     const uint32_t nsp = min(s_misc[0], AW_SPILL);
-    if (__any(rowscan)) {  // every spilled subject: this row's keys among the round's claimed slots
+    if (SPLIT > 1u ? s_misc[1] != 0u : __any(rowscan)) {  // every spilled subject: this row's keys among the round's claimed slots
       __threadfence();
       const uint32_t nu = min(atomicAdd(&P.ctl->sp_n, 0u), P.spmask + 1u);
       const unsigned long long k0 = lrow(P, p) * (unsigned long long)P.W + 1ull, k1 = k0 + P.W;
-      for (uint32_t t = lane; t < nu; t += 64u) {
+      for (uint32_t t = lane + 64u * part; t < nu; t += 64u * SPLIT) {
         const uint32_t hs = P.sp_used[t];  // (another wave's entry may still be stale: keys filter it)
         const unsigned long long k = P.sp_key[hs];
         if (k < k0 || k >= k1) continue;
@@ -3450,14 +3513,14 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
     } else {
       if (nsp) __threadfence();
-      for (uint32_t t = lane; t < nsp; t += 64u) {
+      for (uint32_t t = lane + 64u * part; t < nsp; t += 64u * SPLIT) {
         const uint32_t hs = s_spl[t];
         apply(subj_of(P, spill_cell(P, hs)), atomicExch(&P.sp_val[hs], 0u));
       }
     }
-    if (lane == 0) atomicAdd(&P.held[p], total);
-    nspills += lane == 0 ? s_misc[0] : 0u;
-    wsync();  // the spill counter is reset for the wave's next receiver
+    if (lane == 0 && part == 0u) atomicAdd(&P.held[p], total);
+    nspills += lane == 0 && part == 0u ? s_misc[0] : 0u;
+    bsync();  // the spill counter is reset for the next receiver
     APPLYB_MARK(3);
   }
   add_stat(P, ST_GOSSIPS_CREATED, created);
@@ -3481,6 +3544,13 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b(
 __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_h4(KP P) { apply_b_body<true, false>(P); }
 __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16(KP P) { apply_b_body<false, true>(P); }
 __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_h4(KP P) { apply_b_body<true, true>(P); }
+// small shards: a workgroup per receiver (16-bit ids: dictionaries of at most 8,192 blocks)
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_s4(KP P) {
+  apply_b_body<false, true, 4u>(P);
+}
+__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_h4_s4(KP P) {
+  apply_b_body<true, true, 4u>(P);
+}
 
 // hd4 handles, once a period: escape entries whose slot the row no longer holds with nibble 15
 // (swept, or rewritten with a small offset) become tombstones, so the table holds only live escapes

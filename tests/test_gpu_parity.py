@@ -274,7 +274,9 @@ def test_commit_radix_path_parity():
     with the oracle (the radix order must equal the bitonic order up to ties, which are unobservable).
     The variant sorts every batch in the single-launch chain (k_rs_fused, -DSWIM_RS_FUSE_ALL=1: at most
     32 workgroups walking the tiles, grid barriers between the steps), which the product takes for
-    gossip rounds; the product's parity runs cover the eleven-launch chain of bigger phases."""
+    gossip rounds; the product's parity runs cover the eleven-launch chain of bigger phases. The
+    variant also pulls with one wave per receiver at every size (-DSWIM_PULL_SPLIT_N=0), the product's
+    path above 16 rows per CU (4,096) per shard, which it splits over a workgroup's 4 waves below."""
     out = _run_variant("libswimhip_cs32.so", _SPILL_SCRIPT)
     radix = int(out.split("RADIX")[-1].split()[0])
     assert radix > 0, "the chip-wide radix sort never ran"
