@@ -593,8 +593,8 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           else if (P.batched || h->dict_on)
             hipLaunchKernelGGL(P.cid16 ? (P.hd4 ? k_gossip_apply_b16_h4 : k_gossip_apply_b16)
                                        : (P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b),
-                               dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b),
-                               h->apply_lds_b, s, P);
+                               dim3(SWIM_AW_PERSIST ? h->apply_blocks_b : blocks_for(nloc, h->apply_waves_b)),
+                               dim3(64 * h->apply_waves_b), h->apply_lds_b, s, P);
           else
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
                                h->apply_lds, s, P);

@@ -3087,6 +3087,11 @@ constexpr uint32_t AW_LONG = SWIM_AW_LONG;
 __host__ __device__ __forceinline__ uint32_t aw_words(uint32_t dsids) { return dsids / 4u + AW_SPILL + 4u; }
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
+// 1: a grid of as many workgroups as fit the chip, each wave walking the receiver list at a grid
+// stride; 0: a wave per possible receiver (the dispatcher hands out the list, waves past it return)
+#ifndef SWIM_AW_PERSIST
+#define SWIM_AW_PERSIST 1
+#endif
 #ifndef SWIM_AW_MINW
 #define SWIM_AW_MINW 4  // (the LDS bitmap caps the 8,192-block dictionary at 4 waves per SIMD anyway:
                         // registers beyond 128 would only lower that)
