@@ -2392,6 +2392,9 @@ constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step o
 #define SWIM_PULL_SILP 2
 #endif
 constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
+#ifndef SWIM_PULL_ACTSPEC
+#define SWIM_PULL_ACTSPEC 0
+#endif
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2634,12 +2637,36 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           }
         if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
       };
+#if SWIM_PULL_ACTSPEC == 2  // ... and the next step's pair loaded before this step's work
+      uint32_t lw_n = 0xFFFFFFFFu;
+      uint4 a_n = make_uint4(0u, 0u, 0u, 0u);
+      if (4u * lane + 256u * part < n_act) {
+        const uint32_t k1 = 4u * lane + 256u * part;
+        lw_n = lackr ? lackr[k1 >> 5] : 0xFFFFFFFFu;
+        a_n = *reinterpret_cast<const uint4*>(P.act + k1);
+      }
+#endif
       for (uint32_t kq = 4u * lane + 256u * part; kq < n_act; kq += 256u * SPLIT) {
         // the receiver's own select pass marked the sent words it lacks something in: skip the
-        // rest without reading the list or the holdings (most of them once a storm has spread;
-        // compacting the marked quads first measured no faster: the visits are latency-bound)
+        // rest without reading the holdings (most of them once a storm has spread; compacting the
+        // marked quads first measured no faster: the visits are latency-bound)
+#if SWIM_PULL_ACTSPEC == 2
+        const uint32_t lw = lw_n;
+        const uint4 a = a_n;
+        if (kq + 256u * SPLIT < n_act) {
+          const uint32_t k1 = kq + 256u * SPLIT;
+          lw_n = lackr ? lackr[k1 >> 5] : 0xFFFFFFFFu;
+          a_n = *reinterpret_cast<const uint4*>(P.act + k1);
+        }
+        if (!((lw >> (kq & 31u)) & 0xFu)) continue;
+#elif SWIM_PULL_ACTSPEC  // the list quad loaded beside its lack word, not after it (one round trip)
+        const uint32_t lw = lackr ? lackr[kq >> 5] : 0xFFFFFFFFu;
+        const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
+        if (!((lw >> (kq & 31u)) & 0xFu)) continue;
+#else
         if (lackr && !((lackr[kq >> 5] >> (kq & 31u)) & 0xFu)) continue;
         const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
+#endif
         uint32_t todo, anyall, anymix, ws0;
         uint32_t wcv[4], wsv[4], live[4], hw[4];
         bool quad;
