@@ -2395,6 +2395,9 @@ constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a 
 // 1: the list quad is loaded beside its lack word (one round trip per visited quad instead of two;
 // C4's schedule pull 8.02 -> 7.82 ms per period, C3 and C2 unchanged); 2: also the next step's pair
 // ahead (133 VGPRs: 3 waves per SIMD, or 20 B of scratch held to 4; slower)
+#ifndef SWIM_PULL_NOSKIP
+#define SWIM_PULL_NOSKIP 0
+#endif
 #ifndef SWIM_PULL_ACTSPEC
 #define SWIM_PULL_ACTSPEC 1
 #endif
@@ -2527,6 +2530,10 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           hw[i] = quad ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
           if (wcv[i] == WC_NONE) continue;
           ++words;
+          if (SWIM_PULL_NOSKIP) {  // which window loads the quad needs, from the list alone
+            anyall |= wcv[i] == WC_ALL ? 1u : 0u;
+            anymix |= wcv[i] == WC_MIXED ? 1u : 0u;
+          }
           if (!(DQ && P.delay_on) && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
           todo |= 1u << i;
           anyall |= wcv[i] == WC_ALL ? 1u : 0u;
@@ -2674,7 +2681,9 @@ __device__ __forceinline__ void pull_body(const KP& P) {
         uint32_t wcv[4], wsv[4], live[4], hw[4];
         bool quad;
         classify(kq, a, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
-        if (!todo) continue;
+        // (SWIM_PULL_NOSKIP: no branch on the holdings just loaded, so the senders' window loads
+        // issue beside them; a quad with nothing to do then costs its window loads)
+        if (!SWIM_PULL_NOSKIP && !todo) continue;
         deliver(kq, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
       }
 
