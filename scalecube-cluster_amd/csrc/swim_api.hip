@@ -581,7 +581,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
             hipLaunchKernelGGL(split ? k_gossip_pull_s4 : k_gossip_pull, dim3(split ? nloc : blocks_for(nloc, 4)),
                                dim3(256), 0, s, P);
         });
-        timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(1024), dim3(256), 0, s, P); });
+        timed(h, 11, "k_gossip_record", [&] { hipLaunchKernelGGL(k_gossip_record, dim3(REC_GRID), dim3(256), 0, s, P); });
         timed(h, 2, "k_gossip_apply", [&] {
           // with the record dictionary (gossip batching on, the default) the batched apply runs whether
           // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject

@@ -2200,6 +2200,10 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
 #define SWIM_REC_ILP 2
 #endif
 constexpr uint32_t REC_ILP = SWIM_REC_ILP;  // k_gossip_record's loss / delay draws per step of a lane
+#ifndef SWIM_REC_GRID
+#define SWIM_REC_GRID 1024
+#endif
+constexpr uint32_t REC_GRID = SWIM_REC_GRID;  // k_gossip_record's workgroups (4 waves each, walking the records' chunks)
 
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
 // position k (its window for p, minus lost messages: the same loss draws as k_gossip_pull).
