@@ -75,9 +75,10 @@ struct swim_handle {
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
   size_t apply_lds_s4 = 0;                 // k_gossip_apply_b16_s4: one bitmap per workgroup
-  // shards of at most this many rows select, pull and apply with a workgroup's 4 waves per member:
-  // one wave per member would leave the chip's SIMDs at most 4 waves each (16 per CU; C2's 4,096
-  // members on 256 CUs gain, 65,536 lose: DESIGN.md §6.5)
+  // shards of at most this many rows pull with a workgroup's 4 waves per receiver (select and the
+  // batched apply too when built with SWIM_SEL_SPLIT_N / SWIM_APPLY_SPLIT_N: slower, off): one wave
+  // per member would leave the chip's SIMDs at most 4 waves each (16 per CU; C2's 4,096 members on
+  // 256 CUs gain, 65,536 lose: DESIGN.md §6.5)
   uint32_t split_rows = 4096;
   uint32_t apply_blocks_s4 = 0;
   uint32_t CC = 0;  // record ring of the gossip batches
