@@ -2119,6 +2119,11 @@ __global__ void __launch_bounds__(256) k_gossip_pairfill(KP P) {
   }
 }
 
+// SWIM_PRUNE_PW = 0: a wave per (pair, record slot, chunk), most of them past the pair's records (a
+// load of the pair to find out); 1: a wave per (pair, chunk) walking the pair's records
+#ifndef SWIM_PRUNE_PW
+#define SWIM_PRUNE_PW 0
+#endif
 __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
@@ -2126,6 +2131,24 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t nch = (P.astride + PCHUNK - 1u) / PCHUNK;  // chunks of the longest record
   uint32_t removed_alive = 0;
+#if SWIM_PRUNE_PW  // a wave per (pair, chunk): the pair's records' headers in one round of loads, one lane each
+  for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {
+    const uint32_t i = u / nch, c = u % nch;
+    const uint4 sp = P.sp_list[i];
+    const uint32_t nr = min(sp.z, (uint32_t)MAXREC);
+    uint4 hdr_l = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t len_l = 0u;
+    if (lane < nr) {
+      const uint32_t rec = P.sp_recs[(size_t)i * MAXREC + lane];
+      hdr_l = P.rec_hdr[rec & (P.rcap - 1u)];
+      len_l = P.rec_len[rec & (P.rcap - 1u)];
+    }
+    uint32_t removed = 0;
+    for (uint32_t j = 0; j < nr; ++j) {
+    const uint4 hdr = make_uint4(0u, 0u, (uint32_t)__shfl((int)hdr_l.z, (int)j, 64), (uint32_t)__shfl((int)hdr_l.w, (int)j, 64));
+    const uint32_t len = (uint32_t)__shfl((int)len_l, (int)j, 64);
+    if (c * PCHUNK >= len) continue;
+#else
   for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * MAXREC * nch; u += gridDim.x * 4u) {
     const uint32_t i = u / (MAXREC * nch), j = (u / nch) % MAXREC, c = u % nch;
     const uint4 sp = P.sp_list[i];
@@ -2134,9 +2157,10 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
     const uint4 hdr = P.rec_hdr[rec & (P.rcap - 1u)];
     const uint32_t len = P.rec_len[rec & (P.rcap - 1u)];
     if (c * PCHUNK >= len) continue;
+    uint32_t removed = 0;
+#endif
     const uint32_t t = hdr.z, wbt = P.ctl->wbeg_hist[t & 255u];
     const uint32_t* act_t = P.act_ring + (size_t)(t & 255u) * P.astride;
-    uint32_t removed = 0;
     const uint32_t q1 = min(len, (c + 1u) * PCHUNK);
     for (uint32_t q = c * PCHUNK + lane; q < q1; q += 64u) {
       const uint32_t bits = P.rec_body[(hdr.w + q) & (P.bcap - 1u)];
@@ -2150,6 +2174,9 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       const uint32_t supp = bits & state_since(P, sp.x, wmod(P, wi), t, bits);
       if (supp) removed += slot_gossips(P, wmod(P, wi), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
     }
+#if SWIM_PRUNE_PW
+    }  // the pair's records
+#endif
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
       removed_alive += removed;
       if (removed) atomicAdd(&P.dbg_send[2 * sp.x + 1], (unsigned long long)removed);
