@@ -8,8 +8,9 @@ Philox-chosen crash set) and resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3s]
 
-N > 1 runs under torch.distributed.run, one rank per GPU (RANK/LOCAL_RANK/WORLD_SIZE from the
-env): the workload's ONE cluster is split into observer-row shards, one per GPU, exchanging
+N > 1 runs one rank per GPU under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE from the env;
+`--gpus N` from a plain `python bench.py` starts those N ranks itself as children and touches no GPU;
+a WORLD_SIZE that differs from --gpus is refused): the workload's ONE cluster is split into observer-row shards, one per GPU, exchanging
 gossip windows, gossip ids and SYNC tables over RCCL each round (DESIGN.md §7; strong scaling);
 barrier + max-over-ranks timing, value = the cluster's member-periods / time.
 Rank 0 prints ONE JSON line.
@@ -363,6 +364,38 @@ def cpu_baseline(workload, warmup, budget_s=15.0, seed=1, max_periods=20):
                       f"{cores} host cores at once ({wall:.1f} s wall incl. their warmup)"}
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch(gpus, argv, env=None):
+    """How this invocation gets its `gpus` ranks (one process per GPU).
+
+    Returns None when this process is already the one to run: `--gpus 1` without a launcher, or a
+    rank started by torch.distributed.run whose WORLD_SIZE equals `--gpus`. A WORLD_SIZE that
+    differs from `--gpus` is refused (ValueError): the line would name a GPU count it did not run on.
+    Otherwise (`--gpus N > 1` with no WORLD_SIZE) returns the torch.distributed.run command that
+    starts N ranks of this same script with the same arguments; the caller runs it as a child and
+    relays its exit code, touching no GPU itself (the ranks inherit stdout, so rank 0's JSON line is
+    this process's output)."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws}: launch {gpus} ranks, or pass --gpus {ws}")
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -385,6 +418,18 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for --gpus > 1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     args = ap.parse_args()
+
+    try:
+        launch = rank_launch(args.gpus, sys.argv[1:])
+    except ValueError as e:
+        ap.error(str(e))
+    if launch is not None:  # --gpus N > 1 from a plain `python bench.py`: N ranks as children, no GPU here
+        import subprocess
+
+        log(f"--gpus {args.gpus}: starting {args.gpus} ranks under torch.distributed.run")
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(launch, env=env))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

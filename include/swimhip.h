@@ -108,10 +108,12 @@ typedef struct swim_config {
                                reference's presets (3, local 2) pass at every size up to 2^27 */
   int32_t sync_interval_ms;
   int32_t sync_timeout_ms;
-  int32_t suspicion_mult;
+  int32_t suspicion_mult;   /* suspicionMult * bit_length(n_members) + 64 must stay below 2^14 periods
+                               (u16 deadline cells; larger: SWIM_EINVAL)                    */
   int32_t metadata_timeout_ms;
   uint32_t n_seeds;         /* MembershipConfig.seedMembers = members [0, n_seeds)        */
-  uint32_t gossip_capacity; /* live gossip slots (power of two; 0 = default)              */
+  uint32_t gossip_capacity; /* live gossip slots (a multiple of 1,024: a power of two masks ids,
+                               any other size takes them mod the size; 0 = default)         */
   uint32_t event_capacity;  /* buffered MembershipEvents (0 = events not recorded)        */
   uint32_t sync_capacity;   /* SYNC requests per period (0 = default)                     */
   uint32_t tracked_subjects; /* mode 1: K subject columns. A subject gets a column the first time
@@ -135,9 +137,10 @@ typedef struct swim_config {
                                96 GiB on this handle, else 8 */
   uint32_t dict_subjects;   /* record dictionary of the batched apply: subjects with live
                                gossip records that each get a block of 8 entries (a power of two, 4 ..
-                               2^20; 0 = 8,192). A subject without a block merges through the spill table;
+                               2^17; 0 = 8,192). A subject without a block merges through the spill table;
                                each receiver in flight keeps dict_subjects bytes of entry bitmap in LDS, so
-                               larger dictionaries run fewer receivers per CU */
+                               larger dictionaries run fewer receivers per CU, and a receiver's bitmap must
+                               fit a workgroup's 160 KiB of LDS (larger: SWIM_EINVAL) */
 } swim_config;
 
 typedef struct swim_stats {

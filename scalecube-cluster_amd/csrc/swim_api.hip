@@ -921,6 +921,21 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   if (c.gossip_capacity && (c.gossip_capacity % 1024u || c.gossip_capacity > (1u << 28))) return SWIM_EINVAL;
   if (c.dict_subjects && ((c.dict_subjects & (c.dict_subjects - 1u)) || c.dict_subjects < 4u || c.dict_subjects > (1u << 20)))
     return SWIM_EINVAL;
+  // one receiver's entry bitmap (dict_subjects bytes) plus its spill list must fit a workgroup's 160 KiB
+  // of LDS: at most 131,072 blocks
+  if (c.dict_subjects && 4ull * aw_words(c.dict_subjects) > 160ull * 1024u) {
+    std::fprintf(stderr, "swim_create: dict_subjects %u needs %llu B of LDS per receiver (> 160 KiB; at most 131072)\n",
+                 c.dict_subjects, 4ull * aw_words(c.dict_subjects));
+    return SWIM_EINVAL;
+  }
+  // suspicion deadlines are u16 cells decoded within +-2^14 periods of the current one (swim_device.h,
+  // dl_dec): the timeout, suspicionMult * bit_length(N) periods (ClusterMath.java:123-125), must stay
+  // well inside that window (a 64-period margin for the phases a deadline is read in)
+  if ((uint64_t)c.suspicion_mult * bitlen(c.n_members) + 64u >= (1u << 14)) {
+    std::fprintf(stderr, "swim_create: suspicionMult %d x bit_length(%u) periods does not fit the u16 deadline "
+                         "window (< %u periods)\n", c.suspicion_mult, c.n_members, (1u << 14) - 64u);
+    return SWIM_EINVAL;
+  }
   if ((c.infection_round_bits != 0u && c.infection_round_bits != 4u && c.infection_round_bits != 8u) ||
       c.gossip_batching > 1u ||
       (c.record_capacity && ((c.record_capacity & (c.record_capacity - 1)) || c.record_capacity < 1024u)))
@@ -1005,21 +1020,34 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     const uint32_t per_cu_b = std::max<uint32_t>(
         1, std::min<uint32_t>(2048 / (64 * h->apply_waves_b), (uint32_t)((160u * 1024u) / h->apply_lds_b)));
     h->apply_blocks_b = (uint32_t)std::max(1, cus) * per_cu_b;
+    // the dynamic LDS each apply instance launches with (checked: a refused size fails here, not at
+    // the first step)
+    hipError_t lds_rc = hipSuccess;
+    auto lds_attr = [&lds_rc](const void* k, uint64_t bytes) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      if (e != hipSuccess && lds_rc == hipSuccess) lds_rc = e;
+    };
     for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply), reinterpret_cast<const void*>(&k_gossip_apply_h4)})
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds);
+      lds_attr(k, h->apply_lds);
     for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b), reinterpret_cast<const void*>(&k_gossip_apply_b_h4),
                           reinterpret_cast<const void*>(&k_gossip_apply_b16),
                           reinterpret_cast<const void*>(&k_gossip_apply_b16_h4)})
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_b);
+      lds_attr(k, h->apply_lds_b);
     // the split instance: 4 waves and one bitmap per workgroup, as many workgroups as fit a CU (8 by
     // its 2,048 threads) on every CU
     h->apply_lds_s4 = wave_lds;
     h->apply_blocks_s4 = (uint32_t)std::max(1, cus) *
                          std::max<uint32_t>(1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / wave_lds)));
     for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b16_s4), reinterpret_cast<const void*>(&k_gossip_apply_b16_h4_s4)})
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->apply_lds_s4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_slot_bm), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)P.dsids);
+      lds_attr(k, h->apply_lds_s4);
+    lds_attr(reinterpret_cast<const void*>(&k_slot_bm), P.dsids);
+    if (lds_rc != hipSuccess) {
+      std::fprintf(stderr, "swim_create: dynamic LDS of the apply kernels refused (%s; apply %llu B, batched %llu B)\n",
+                   hipGetErrorString(lds_rc), (unsigned long long)h->apply_lds, (unsigned long long)h->apply_lds_b);
+      free_all(h);
+      delete h;
+      return SWIM_EHIP;
+    }
   }
   if (P.sweepmax + P.hzn + 1u >= 256u) {  // infection rounds are kept mod 2^8 (swim_device.h, hd)
     std::fprintf(stderr, "swim_create: gossipRepeatMult %u too large for N=%u (sweep %u + horizon %u rounds > 254)\n",

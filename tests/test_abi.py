@@ -81,3 +81,40 @@ def test_create_without_gpu_fails_cleanly():
     cfg = to_swim_config(ClusterConfig.defaultLocalConfig(), 8)
     h = ctypes.c_void_p()
     assert lib.swim_create(ctypes.byref(cfg), ctypes.byref(h)) == nat.SWIM_EHIP
+
+
+def _create_rc(**fields):
+    """swim_create's status for the local preset with `fields` overridden (a handle made on a GPU box is
+    destroyed again). Validation precedes every HIP call: EINVAL comes back the same with or without a GPU."""
+    lib = nat.load_swimhip()
+    from swimhip import ClusterConfig, to_swim_config
+
+    cfg = to_swim_config(ClusterConfig.defaultLocalConfig(), fields.pop("n_members", 8))
+    for k, v in fields.items():
+        setattr(cfg, k, v)
+    h = ctypes.c_void_p()
+    rc = lib.swim_create(ctypes.byref(cfg), ctypes.byref(h))
+    if rc == nat.SWIM_OK:
+        lib.swim_destroy(h)
+    return rc
+
+
+def test_create_refuses_suspicion_beyond_u16_deadline_window():
+    # deadlines are u16 cells decoded within +-2^14 periods (swim_device.h dl_dec): suspicionMult x
+    # bit_length(N) + 64 must stay below 2^14 (ClusterMath.suspicionTimeout, ClusterMath.java:123-125)
+    assert _create_rc(n_members=65536, suspicion_mult=1000) == nat.SWIM_EINVAL  # 17,000 periods
+    assert _create_rc(n_members=8, suspicion_mult=4080) == nat.SWIM_EINVAL  # 4 x 4,080 + 64 = 16,384
+    assert _create_rc(n_members=8, suspicion_mult=4079) != nat.SWIM_EINVAL
+
+
+def test_create_refuses_dictionary_beyond_lds():
+    # one receiver's entry bitmap (dict_subjects bytes) must fit a workgroup's 160 KiB of LDS
+    assert _create_rc(n_members=8, dict_subjects=1 << 18) == nat.SWIM_EINVAL
+    assert _create_rc(n_members=8, dict_subjects=1 << 20) == nat.SWIM_EINVAL
+    assert _create_rc(n_members=8, dict_subjects=1 << 17) != nat.SWIM_EINVAL
+    assert _create_rc(n_members=8, dict_subjects=3000) == nat.SWIM_EINVAL  # not a power of two
+
+
+def test_create_accepts_non_power_of_two_rings_in_kib():
+    assert _create_rc(n_members=8, gossip_capacity=5 * 1024) != nat.SWIM_EINVAL
+    assert _create_rc(n_members=8, gossip_capacity=5 * 1024 + 512) == nat.SWIM_EINVAL

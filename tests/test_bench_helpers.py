@@ -1,7 +1,14 @@
-"""bench.py's workload and byte-model helpers (CPU only)."""
+"""bench.py's workload and byte-model helpers and its rank launching (CPU only)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
+import pytest
 
 import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_c3_workload_matches_baseline_config():
@@ -46,3 +53,32 @@ def test_pmc_traffic_is_per_workload_and_single_gpu():
     if bench.pmc_traffic("k_gossip_select") is not None:
         assert bench.pmc_traffic("k_gossip_select", "c3", 2) is None
     assert bench.pmc_traffic("k_gossip_select", "no_such_workload") is None
+
+
+def test_rank_launch_single_gpu_runs_in_process():
+    assert bench.rank_launch(1, ["--steps", "2"], env={}) is None
+
+
+def test_rank_launch_spawns_n_ranks_without_launcher():
+    cmd = bench.rank_launch(4, ["--gpus", "4", "--workload", "c2"], env={})
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--workload", "c2"] and cmd[-5].endswith("bench.py")
+
+
+def test_rank_launch_under_launcher_checks_world_size():
+    assert bench.rank_launch(8, ["--gpus", "8"], env={"WORLD_SIZE": "8"}) is None
+    with pytest.raises(ValueError, match="WORLD_SIZE=2"):
+        bench.rank_launch(8, ["--gpus", "8"], env={"WORLD_SIZE": "2"})
+    with pytest.raises(ValueError, match="WORLD_SIZE=4"):
+        bench.rank_launch(1, [], env={"WORLD_SIZE": "4"})
+    with pytest.raises(ValueError):
+        bench.rank_launch(0, [], env={})
+
+
+def test_bench_cli_refuses_world_size_mismatch():
+    # the refusal happens at argument handling, before the library or any GPU is touched
+    env = dict(os.environ, WORLD_SIZE="2")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
