@@ -73,11 +73,11 @@ WORKLOADS = {
                      "simultaneous crashes",
                 n=1 << 18, preset="lan", loss=0.0, crash_n=256, part=0, gcap=1 << 18, tracked=256),
     # BASELINE configs[3]: needs >= 8 GPUs (dense 256 GiB of views); one rank's shard is 32,768 rows.
-    # Ring: 5 * 2^20 slots (a non-power-of-two ring, ids mod GC), 1.25x the ~4.2e6 live one-gossip slots
+    # Ring: 5,128 * 1,024 = 5,251,072 slots (a non-power-of-two ring, ids mod GC), 1.25x the ~4.2e6 live one-gossip slots
     # C4's storm law predicts
     "c4": dict(desc="C4: 262,144 members, dense N x N views row-sharded over the GPUs, LAN defaults, 1% loss, "
                     "0.1% simultaneous crash",
-               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=5 << 20, scap=4096),
+               n=1 << 18, preset="lan", loss=1.0, crash=0.001, part=0, gcap=5128 * 1024, scap=4096),
     # C4's schedule on ONE GPU in N x K mode (the dense 262,144^2 view needs 8 GPUs): measures the
     # storm C4's 1 % loss and 0.1 % crash create, to size C4's ring (1 % loss: one gossip per slot)
     "c4nxk": dict(desc="C4 schedule on one GPU: 262,144 members, N x K views (K = 1,024), LAN defaults, 1% loss, "
@@ -107,6 +107,12 @@ WORKLOADS = {
                            "simultaneous crash + id-parity partition for 40 periods healed via SYNC",
                       n=32768, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16384, gcap=1 << 18,
                       rcap=1 << 29, dsub=32768),
+    # ... and at the C3 size itself: 2^30 record slots (the storm's records, batched per origin commit),
+    # a 65,536-block dictionary (64 KiB of entry bitmap per receiver: 2 receivers per workgroup)
+    "c3half65k": dict(desc="C3 as SURVEY states it: 65,536 members, dense, LAN defaults, 10% simultaneous crash + "
+                           "id-parity (half/half) partition for 40 periods healed via SYNC",
+                      n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=32768, gcap=1 << 18,
+                      rcap=1 << 30, dsub=65536),
     "steady65k": dict(desc="65,536 members, dense, LAN defaults, fault-free steady state",
                       n=65536, preset="lan", loss=0.0, crash=0.0, part=0, gcap=1 << 14),
 }

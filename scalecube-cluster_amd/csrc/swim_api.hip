@@ -22,16 +22,8 @@ using namespace swim;
 namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
-#ifndef SWIM_CID16
-#define SWIM_CID16 1
-#endif
-#ifndef SWIM_RB_CAP
-#define SWIM_RB_CAP 2048  // slot entry bitmaps (k_slot_bm; 0: none)
-#endif
+constexpr uint32_t RB_CAP = 2048;  // slot entry bitmaps (k_slot_bm)
 constexpr uint32_t RB_GRID = 256;  // k_slot_bm's workgroups (a grid stride over the commit's new slots)
-#ifndef SWIM_RS_FUSE
-#define SWIM_RS_FUSE 1  // the radix chain in one launch where its grid allows (k_rs_fused)
-#endif
 #ifndef SWIM_RS_FUSE_ALL
 #define SWIM_RS_FUSE_ALL 0  // (tests: every radix sort in one launch of CS_FUSE workgroups at most)
 #endif
@@ -74,13 +66,11 @@ struct swim_handle {
   uint32_t apply_blocks = 1, apply_blocks_b = 1, apply_waves_b = 1;
   bool dict_on = false;  // batching enabled: commits keep the record dictionary
   size_t apply_lds = 0, apply_lds_b = 0;  // k_gossip_apply / k_gossip_apply_b (batch slots)
-  size_t apply_lds_s4 = 0;                 // k_gossip_apply_b16_s4: one bitmap per workgroup
-  // shards of at most this many rows pull with a workgroup's 4 waves per receiver (select and the
-  // batched apply too when built with SWIM_SEL_SPLIT_N / SWIM_APPLY_SPLIT_N: slower, off): one wave
-  // per member would leave the chip's SIMDs at most 4 waves each (16 per CU; C2's 4,096 members on
-  // 256 CUs gain, 65,536 lose: DESIGN.md §6.5)
+  // shards of at most this many rows pull with a workgroup's 4 waves per receiver: one wave per
+  // member would leave the chip's SIMDs at most 4 waves each (16 per CU; C2's 4,096 members on 256
+  // CUs gain, 65,536 lose; the same split of select and of the batched apply measured slower:
+  // DESIGN.md §6.5)
   uint32_t split_rows = 4096;
-  uint32_t apply_blocks_s4 = 0;
   uint32_t CC = 0;  // record ring of the gossip batches
   uint32_t dthr_cap = 0;  // entries of the allocated delay threshold table (swim_set_delay)
   uint32_t* crash_ids = nullptr;  // [N] the members one swim_crash call stops (allocated on first use)
@@ -304,7 +294,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
   C.radix = big ? tiles : 0u;
   timed(h, 7, "k_commit", [&] {
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
-    if (big && SWIM_RS_FUSE && (tiles <= CS_FUSE || SWIM_RS_FUSE_ALL)) {
+    if (big && (tiles <= CS_FUSE || SWIM_RS_FUSE_ALL)) {
       hipLaunchKernelGGL(k_rs_fused, dim3(std::min(tiles, CS_FUSE)), dim3(CS_THREADS), 0, s, P, stg, n, C);
     } else if (big) {
       hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C);
@@ -481,10 +471,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         timed(h, 7, "k_gossip_prep", [&] { hipLaunchKernelGGL(k_gossip_prep, dim3(1), dim3(1024), 0, s, P); });
         timed(h, 8, "k_gossip_select", [&] {
-          if (nloc <= std::min(SEL_SPLIT_N, h->split_rows))  // small shards: a workgroup per member (its 4 waves share the holdings pass)
-            hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4_s4 : k_gossip_select_s4, dim3(nloc), dim3(256), 0, s, P);
-          else
-            hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
+          hipLaunchKernelGGL(P.hd4 ? k_gossip_select_h4 : k_gossip_select, dim3(blocks_for(nloc, 4)), dim3(256), 0, s, P);
         });
         timed(h, 10, "k_gossip_pairfill", [&] { hipLaunchKernelGGL(k_gossip_pairfill, dim3(1024), dim3(256), 0, s, P); });
         timed(h, 10, "k_gossip_pairprune", [&] { hipLaunchKernelGGL(k_gossip_pairprune, dim3(2048), dim3(256), 0, s, P); });
@@ -587,15 +574,10 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           // with the record dictionary (gossip batching on, the default) the batched apply runs whether
           // or not the ring holds batch slots: one-gossip slots (probabilistic loss, delays) are subject
           // runs it takes as run tops (C4's lossy storm: apply 373 -> 104 ms per 20 periods, §6.4)
-          // (small shards with 16-bit ids: a workgroup of 4 waves per receiver, one bitmap per workgroup)
-          if ((P.batched || h->dict_on) && P.cid16 && nloc <= std::min(APPLY_SPLIT_N, h->split_rows))
-            hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_b16_h4_s4 : k_gossip_apply_b16_s4, dim3(h->apply_blocks_s4),
-                               dim3(64 * AW_WAVES), h->apply_lds_s4, s, P);
-          else if (P.batched || h->dict_on)
+          if (P.batched || h->dict_on)
             hipLaunchKernelGGL(P.cid16 ? (P.hd4 ? k_gossip_apply_b16_h4 : k_gossip_apply_b16)
                                        : (P.hd4 ? k_gossip_apply_b_h4 : k_gossip_apply_b),
-                               dim3(SWIM_AW_PERSIST ? h->apply_blocks_b : blocks_for(nloc, h->apply_waves_b)),
-                               dim3(64 * h->apply_waves_b), h->apply_lds_b, s, P);
+                               dim3(h->apply_blocks_b), dim3(64 * h->apply_waves_b), h->apply_lds_b, s, P);
           else
             hipLaunchKernelGGL(P.hd4 ? k_gossip_apply_h4 : k_gossip_apply, dim3(h->apply_blocks), dim3(APPLY_THREADS),
                                h->apply_lds, s, P);
@@ -1033,13 +1015,6 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
                           reinterpret_cast<const void*>(&k_gossip_apply_b16),
                           reinterpret_cast<const void*>(&k_gossip_apply_b16_h4)})
       lds_attr(k, h->apply_lds_b);
-    // the split instance: 4 waves and one bitmap per workgroup, as many workgroups as fit a CU (8 by
-    // its 2,048 threads) on every CU
-    h->apply_lds_s4 = wave_lds;
-    h->apply_blocks_s4 = (uint32_t)std::max(1, cus) *
-                         std::max<uint32_t>(1, std::min<uint32_t>(2048 / (64 * AW_WAVES), (uint32_t)((160u * 1024u) / wave_lds)));
-    for (const void* k : {reinterpret_cast<const void*>(&k_gossip_apply_b16_s4), reinterpret_cast<const void*>(&k_gossip_apply_b16_h4_s4)})
-      lds_attr(k, h->apply_lds_s4);
     lds_attr(reinterpret_cast<const void*>(&k_slot_bm), P.dsids);
     if (lds_rc != hipSuccess) {
       std::fprintf(stderr, "swim_create: dynamic LDS of the apply kernels refused (%s; apply %llu B, batched %llu B)\n",
@@ -1179,8 +1154,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.c_hash, h->CC);
   h->dict_on = c.gossip_batching == 0;
   if (h->dict_on) {
-    // 16-bit entry ids while every id (dict_subjects x 8 ways) and the two sentinels fit (SWIM_CID16=0: 32-bit)
-    P.cid16 = (SWIM_CID16 && P.dsids * DICT_WAYS <= 65536u) ? 1u : 0u;
+    // 16-bit entry ids while every id (dict_subjects x 8 ways) and the two sentinels fit (else 32-bit)
+    P.cid16 = (P.dsids * DICT_WAYS <= 65536u) ? 1u : 0u;
     if (P.cid16) {
       ALLOC(P.c_id16, h->CC);
     } else {
@@ -1193,8 +1168,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     ALLOC(P.d_free, P.dsids);
     ALLOC(P.d_gen, P.dsids);
     ALLOC(P.dmark, NL * P.dsids);
-    // slot entry bitmaps of long record ranges (k_slot_bm), a ring of SWIM_RB_CAP of dsids bytes each
-    P.rb_cap = SWIM_RB_CAP;
+    // slot entry bitmaps of long record ranges (k_slot_bm), a ring of RB_CAP of dsids bytes each
+    P.rb_cap = RB_CAP;
     if (P.rb_cap) {
       ALLOC(P.rb_bits, (size_t)P.rb_cap * (P.dsids / 4u));
       ALLOC(P.rb_tag, P.rb_cap);

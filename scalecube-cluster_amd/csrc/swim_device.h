@@ -442,7 +442,7 @@ static_assert(DICT_SIDS >= 4 && (DICT_SIDS & (DICT_SIDS - 1)) == 0 && DICT_SIDS 
 
 
 // Ring slot of gossip id `id` and ring word of unwrapped word index `wi`. A power-of-two ring masks;
-// any other multiple of 1,024 slots (C4's 5 * 2^20: DESIGN.md §4.2) takes the remainder, and its ids
+// any other multiple of 1,024 slots (C4's 5,128 * 1,024: DESIGN.md §4.2) takes the remainder, and its ids
 // must not wrap 2^32 (k_commit raises OV_GOSSIP before they do)
 __device__ __forceinline__ uint32_t gmod(const KP& P, uint32_t id) { return P.gpow2 ? (id & P.gmask) : id % P.GC; }
 __device__ __forceinline__ uint32_t wmod(const KP& P, uint32_t wi) {
@@ -487,9 +487,7 @@ __device__ __forceinline__ void dq_window(const KP& P, uint32_t p, uint32_t* lo,
   *hi = h;
 }
 constexpr uint32_t DQ_PAIR = 0x10000u;   // k_gossip_select: the chosen peer delivered delayed messages
-#ifndef SWIM_PCHUNK
 #define SWIM_PCHUNK 256  // (1,024: C2 4.64 -> 4.25 ms per period at 256, C4's schedule and C3 a little faster too)
-#endif
 constexpr uint32_t PCHUNK = SWIM_PCHUNK;  // active-list positions per wave in the infectedFrom kernels
 static_assert(PCHUNK % 64u == 0u, "SWIM_PCHUNK: a multiple of 64");
 

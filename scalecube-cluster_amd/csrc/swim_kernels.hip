@@ -1548,12 +1548,8 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 // one list quad per lane per step at 6 waves per SIMD (80 VGPRs, 44 B of scratch): with the MIXED
 // entries flattened across the wave, more waves in flight beat more loads per wave (C3 select 63.9
 // -> 55.3 ms per 20 periods, C4's schedule 94.9 -> 87.9)
-#ifndef SWIM_SEL_BATCH
 #define SWIM_SEL_BATCH 1
-#endif
-#ifndef SWIM_SEL_WAVES
 #define SWIM_SEL_WAVES 6
-#endif
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
 // The lane that owns item q of a wave-wide flattened list: the last lane j with off_j <= q (off =
@@ -1571,45 +1567,12 @@ __device__ __forceinline__ uint32_t wave_owner(uint32_t off, uint32_t q) {
 // position of the k-th (0-based) set bit of m, k < popcount(m)
 __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k);
 
-// OR of v over the 64 lanes (DPP row shifts and broadcasts, then lane 63; every lane must call)
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-  v |= dpp_in<0x111, 0xF>(v);
-  v |= dpp_in<0x112, 0xF>(v);
-  v |= dpp_in<0x114, 0xF>(v);
-  v |= dpp_in<0x118, 0xF>(v);
-  v |= dpp_in<0x142, 0xA>(v);
-  v |= dpp_in<0x143, 0xC>(v);
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
 // wave_owner for a window of 64 items: lane x gets the owner of item q0 + x, where lane L owns items
-// [off_L, off_L + cnt_L) (off = the exclusive scan of cnt). Instead of six dependent lane shuffles
-// (LDS round trips), the VALU finds it: the lanes whose ranges meet the window (a ballot, in item
-// order), their clipped start positions (one 64-bit OR over the wave), and for item x the rank of the
-// last start at or before x among them. A lane whose item does not exist gets an arbitrary owner, as
-// with wave_owner (callers test q < total).
-#ifndef SWIM_OWNER_BALLOT
-#define SWIM_OWNER_BALLOT 0
-#endif
+// [off_L, off_L + cnt_L) (off = the exclusive scan of cnt). A lane whose item does not exist gets an
+// arbitrary owner (callers test q < total). (A ballot / VALU variant of it measured no faster, §6.5.)
 __device__ __forceinline__ uint32_t wave_owner_at(uint32_t off, uint32_t cnt, uint32_t q0) {
-  const uint32_t lane = threadIdx.x & 63u;
-#if SWIM_OWNER_BALLOT
-  const bool meets = cnt != 0u && off < q0 + 64u && off + cnt > q0;
-  const unsigned long long lanes = __ballot(meets);
-  const uint32_t st = meets ? (off > q0 ? off - q0 : 0u) : 64u;
-  const uint32_t s_lo = wave_or(st < 32u ? (1u << st) : 0u);
-  const uint32_t s_hi = wave_or(st >= 32u && st < 64u ? (1u << (st - 32u)) : 0u);
-  const uint32_t below_lo = lane >= 31u ? s_lo : s_lo & ((2u << lane) - 1u);
-  const uint32_t below_hi = lane < 32u ? 0u : (lane == 63u ? s_hi : s_hi & ((2u << (lane - 32u)) - 1u));
-  const uint32_t r = (uint32_t)(__popc(below_lo) + __popc(below_hi));
-  if (r == 0u) return 0u;
-  const uint32_t l_lo = (uint32_t)lanes, l_hi = (uint32_t)(lanes >> 32);
-  const uint32_t c = (uint32_t)__popc(l_lo);
-  return (r - 1u) < c ? kth_set_bit(l_lo, r - 1u) : 32u + kth_set_bit(l_hi, r - 1u - c);
-#else
   (void)cnt;
-  return wave_owner(off, q0 + lane);
-#endif
+  return wave_owner(off, q0 + (threadIdx.x & 63u));
 }
 
 __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
@@ -1626,20 +1589,11 @@ __device__ __forceinline__ uint32_t kth_set_bit(uint32_t m, uint32_t k) {
   return pos;
 }
 
-// SPLIT = 4 (a build knob, off by default): the workgroup's 4 waves share one member's holdings pass
-// (every fourth step of its active list); their sweep counts, GossipRequest counts and window flags
-// meet in LDS, and the first wave alone goes on to the peer choice, infectedFrom and the
-// registrations. Measured slower on C2's 4,096 members (select 0.41 -> 0.46 ms per period; the
-// parity file green through it), unlike the pull's split.
-#ifndef SWIM_SEL_SPLIT_N
-#define SWIM_SEL_SPLIT_N 0
-#endif
-constexpr uint32_t SEL_SPLIT_N = SWIM_SEL_SPLIT_N;  // shards of at most this many rows (and 16 per CU) select 4 waves per member
-template <bool HD4, uint32_t SPLIT = 1u>
+// One wave per member. (The workgroup's 4 waves sharing one member's holdings pass, as the pull does
+// on small shards, measured slower on C2's 4,096 members: select 0.41 -> 0.46 ms per period, §6.5.)
+template <bool HD4>
 __device__ __forceinline__ void select_body(const KP& P) {
-  static_assert(SPLIT == 1u || SPLIT == 4u, "select_body: a wave or a workgroup per member");
   SWIM_GUARD(P);
-  __shared__ uint32_t s_red[4][4];  // SPLIT > 1: per wave {swept, GossipRequests, window non-empty}
   __shared__ uint32_t s_peers[4][MAXF];
   __shared__ uint32_t s_nrec[4][MAXF];          // infectedFrom records found per chosen peer
   __shared__ uint32_t s_rec[4][MAXF][MAXREC];
@@ -1650,13 +1604,12 @@ __device__ __forceinline__ void select_body(const KP& P) {
   __shared__ uint32_t s_win[4][4 * SEL_BATCH][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = threadIdx.x >> 6;
-  const uint32_t part = w % SPLIT;  // this wave's share of the holdings pass
-  const uint32_t m = P.row0 + blockIdx.x * (4u / SPLIT) + w / SPLIT;
+  const uint32_t m = P.row0 + blockIdx.x * 4u + w;
   const uint32_t N = P.N;
   const uint32_t r = P.round;
   const uint32_t lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   if (lo >= hi) {  // no live gossip anywhere (a quiet round): nothing is held, sent or swept
-    if (lane == 0 && part == 0u && m < P.row0 + P.nloc) P.npeers[m] = 0u;
+    if (lane == 0 && m < P.row0 + P.nloc) P.npeers[m] = 0u;
     if (m == P.dbg_watch && lane == 0) {
       uint32_t* L = P.dbg_log + (r & 255u) * 8u;
       L[0] = r;
@@ -1696,7 +1649,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
     // load each, all issued together (bytes in flight). Words whose class the member's own age
     // bounds settle are finished in a fully unrolled pass (no dynamically indexed register
     // arrays, so nothing goes to scratch); the few left MIXED are finished one by one from a mask.
-    for (uint32_t k0 = 256u * SEL_BATCH * part; k0 < n_act; k0 += 256u * SEL_BATCH * SPLIT) {
+    for (uint32_t k0 = 0; k0 < n_act; k0 += 256u * SEL_BATCH) {
       uint32_t ev[4 * SEL_BATCH], wv[4 * SEL_BATCH];
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
@@ -1888,30 +1841,7 @@ __device__ __forceinline__ void select_body(const KP& P) {
         }
       }
     }
-    if (lack_ok && lane == 0 && part == 0u) P.lack_round[m] = r;
-  }
-  if (SPLIT > 1u) {  // (uniform: every wave of the workgroup is the same member's)
-    const uint32_t a = wave_sum(nclear), b = wave_sum(winbits), c = __any(win_l) ? 1u : 0u;
-    if (lane == 0) {
-      s_red[w][0] = a;
-      s_red[w][1] = b;
-      s_red[w][2] = c;
-    }
-    add_stat(P, ST_G_HDREAD, hdw);
-    add_stat(P, ST_G_WINW, winw);
-    hdw = winw = 0u;
-    __syncthreads();
-    if (part != 0u) return;  // the first wave goes on alone (no barrier below)
-    nclear = winbits = 0u;
-    win_l = false;
-    if (lane == 0) {
-#pragma unroll
-      for (uint32_t q = 0; q < SPLIT; ++q) {
-        nclear += s_red[w + q][0];
-        winbits += s_red[w + q][1];
-        win_l |= s_red[w + q][2] != 0u;
-      }
-    }
+    if (lack_ok && lane == 0) P.lack_round[m] = r;
   }
   SEL_MARK(0);
   uint32_t np = 0;
@@ -2082,8 +2012,6 @@ __device__ __forceinline__ void select_body(const KP& P) {
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select(KP P) { select_body<false>(P); }
 __global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4(KP P) { select_body<true>(P); }
 // small shards: a workgroup per member
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_s4(KP P) { select_body<false, 4u>(P); }
-__global__ void __launch_bounds__(256, SWIM_SEL_WAVES) k_gossip_select_h4_s4(KP P) { select_body<true, 4u>(P); }
 
 __device__ __forceinline__ uint32_t remote_window(const KP& P, uint32_t i, uint32_t k);
 
@@ -2119,12 +2047,9 @@ __global__ void __launch_bounds__(256) k_gossip_pairfill(KP P) {
   }
 }
 
-// SWIM_PRUNE_PW = 0: a wave per (pair, record slot, chunk), most of them past the pair's records (a
-// load of the pair to find out); 1: a wave per (pair, chunk) walking the pair's records, their headers
-// loaded one per lane (C2 3.75 -> 3.62 ms per period, C3 and C4's schedule -0.7 %)
-#ifndef SWIM_PRUNE_PW
-#define SWIM_PRUNE_PW 1
-#endif
+// A wave per (pair, chunk) walking the pair's records, their headers loaded one per lane in one round
+// of loads (a wave per (pair, record slot, chunk), most of them past the pair's records, measured
+// slower: C2 3.75 -> 3.62 ms per period, C3 and C4's schedule -0.7 %)
 __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
@@ -2132,7 +2057,6 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg;
   const uint32_t nch = (P.astride + PCHUNK - 1u) / PCHUNK;  // chunks of the longest record
   uint32_t removed_alive = 0;
-#if SWIM_PRUNE_PW  // a wave per (pair, chunk): the pair's records' headers in one round of loads, one lane each
   for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {
     const uint32_t i = u / nch, c = u % nch;
     const uint4 sp = P.sp_list[i];
@@ -2145,39 +2069,26 @@ __global__ void __launch_bounds__(256) k_gossip_pairprune(KP P) {
       len_l = P.rec_len[rec & (P.rcap - 1u)];
     }
     uint32_t removed = 0;
-    for (uint32_t j = 0; j < nr; ++j) {
-    const uint4 hdr = make_uint4(0u, 0u, (uint32_t)__shfl((int)hdr_l.z, (int)j, 64), (uint32_t)__shfl((int)hdr_l.w, (int)j, 64));
-    const uint32_t len = (uint32_t)__shfl((int)len_l, (int)j, 64);
-    if (c * PCHUNK >= len) continue;
-#else
-  for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * MAXREC * nch; u += gridDim.x * 4u) {
-    const uint32_t i = u / (MAXREC * nch), j = (u / nch) % MAXREC, c = u % nch;
-    const uint4 sp = P.sp_list[i];
-    if (j >= sp.z) continue;
-    const uint32_t rec = P.sp_recs[(size_t)i * MAXREC + j];
-    const uint4 hdr = P.rec_hdr[rec & (P.rcap - 1u)];
-    const uint32_t len = P.rec_len[rec & (P.rcap - 1u)];
-    if (c * PCHUNK >= len) continue;
-    uint32_t removed = 0;
-#endif
-    const uint32_t t = hdr.z, wbt = P.ctl->wbeg_hist[t & 255u];
-    const uint32_t* act_t = P.act_ring + (size_t)(t & 255u) * P.astride;
-    const uint32_t q1 = min(len, (c + 1u) * PCHUNK);
-    for (uint32_t q = c * PCHUNK + lane; q < q1; q += 64u) {
-      const uint32_t bits = P.rec_body[(hdr.w + q) & (P.bcap - 1u)];
-      if (!bits) continue;
-      const uint32_t wi = wbt + (act_t[q] & ACT_OFF_MASK);
-      if (wi < w_beg) continue;  // every holder has swept the word
-      const uint2 ap = P.actpos[wmod(P, wi)];  // listed this round, as this very word?
-      if (ap.x != P.round || ap.y >= n_act) continue;
-      const uint32_t ea = P.act[ap.y];
-      if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
-      const uint32_t supp = bits & state_since(P, sp.x, wmod(P, wi), t, bits);
-      if (supp) removed += slot_gossips(P, wmod(P, wi), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
+    for (uint32_t j = 0; j < nr; ++j) {  // the pair's records
+      const uint32_t t = (uint32_t)__shfl((int)hdr_l.z, (int)j, 64), body = (uint32_t)__shfl((int)hdr_l.w, (int)j, 64);
+      const uint32_t len = (uint32_t)__shfl((int)len_l, (int)j, 64);
+      if (c * PCHUNK >= len) continue;
+      const uint32_t wbt = P.ctl->wbeg_hist[t & 255u];
+      const uint32_t* act_t = P.act_ring + (size_t)(t & 255u) * P.astride;
+      const uint32_t q1 = min(len, (c + 1u) * PCHUNK);
+      for (uint32_t q = c * PCHUNK + lane; q < q1; q += 64u) {
+        const uint32_t bits = P.rec_body[(body + q) & (P.bcap - 1u)];
+        if (!bits) continue;
+        const uint32_t wi = wbt + (act_t[q] & ACT_OFF_MASK);
+        if (wi < w_beg) continue;  // every holder has swept the word
+        const uint2 ap = P.actpos[wmod(P, wi)];  // listed this round, as this very word?
+        if (ap.x != P.round || ap.y >= n_act) continue;
+        const uint32_t ea = P.act[ap.y];
+        if ((ea & ACT_OFF_MASK) != wi - w_beg || ((ea >> 26) & 3u) == WC_NONE) continue;  // nobody's window
+        const uint32_t supp = bits & state_since(P, sp.x, wmod(P, wi), t, bits);
+        if (supp) removed += slot_gossips(P, wmod(P, wi), atomicAnd(&P.pw[sp.w + ap.y], ~supp) & supp);
+      }
     }
-#if SWIM_PRUNE_PW
-    }  // the pair's records
-#endif
     if (route(P, sp.y) != NONE) {  // the send counter covers alive peers only
       removed_alive += removed;
       if (removed) atomicAdd(&P.dbg_send[2 * sp.x + 1], (unsigned long long)removed);
@@ -2224,13 +2135,9 @@ __global__ void __launch_bounds__(256) k_gossip_pairdelay(KP P) {
   add_stat(P, ST_GOSSIP_SUPP, removed_alive);
 }
 
-#ifndef SWIM_REC_ILP
 #define SWIM_REC_ILP 2
-#endif
 constexpr uint32_t REC_ILP = SWIM_REC_ILP;  // k_gossip_record's loss / delay draws per step of a lane
-#ifndef SWIM_REC_GRID
 #define SWIM_REC_GRID 1024
-#endif
 constexpr uint32_t REC_GRID = SWIM_REC_GRID;  // k_gossip_record's workgroups (4 waves each, walking the records' chunks)
 
 // word k of a delivery record: what sender entry `sreg` delivered to p this round at active
@@ -2411,28 +2318,13 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
   if (P.wlast[ws] < arrive) atomicMax(&P.wlast[ws], arrive);
 }
 
-#ifndef SWIM_PULL_WAVES
 #define SWIM_PULL_WAVES 1
-#endif
 // DQ: this handle has delayed-message rings. The delay paths get an instance of
 // their own, so the common one keeps its registers (4 waves per SIMD instead of 3).
-#ifndef SWIM_PULL_LOSS_ILP
 #define SWIM_PULL_LOSS_ILP 2
-#endif
 constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
-#ifndef SWIM_PULL_SILP
 #define SWIM_PULL_SILP 2
-#endif
 constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
-// 1: the list quad is loaded beside its lack word (one round trip per visited quad instead of two;
-// C4's schedule pull 8.02 -> 7.82 ms per period, C3 and C2 unchanged); 2: also the next step's pair
-// ahead (133 VGPRs: 3 waves per SIMD, or 20 B of scratch held to 4; slower)
-#ifndef SWIM_PULL_NOSKIP
-#define SWIM_PULL_NOSKIP 0
-#endif
-#ifndef SWIM_PULL_ACTSPEC
-#define SWIM_PULL_ACTSPEC 1
-#endif
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2562,10 +2454,6 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           hw[i] = quad ? ha[i] : (wcv[i] != WC_NONE ? hbr[wsv[i]] : 0u);
           if (wcv[i] == WC_NONE) continue;
           ++words;
-          if (SWIM_PULL_NOSKIP) {  // which window loads the quad needs, from the list alone
-            anyall |= wcv[i] == WC_ALL ? 1u : 0u;
-            anymix |= wcv[i] == WC_MIXED ? 1u : 0u;
-          }
           if (!(DQ && P.delay_on) && (hw[i] & live[i]) == live[i]) continue;  // holds every live gossip of the word
           todo |= 1u << i;
           anyall |= wcv[i] == WC_ALL ? 1u : 0u;
@@ -2679,43 +2567,20 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           }
         if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
       };
-#if SWIM_PULL_ACTSPEC == 2  // ... and the next step's pair loaded before this step's work
-      uint32_t lw_n = 0xFFFFFFFFu;
-      uint4 a_n = make_uint4(0u, 0u, 0u, 0u);
-      if (4u * lane + 256u * part < n_act) {
-        const uint32_t k1 = 4u * lane + 256u * part;
-        lw_n = lackr ? lackr[k1 >> 5] : 0xFFFFFFFFu;
-        a_n = *reinterpret_cast<const uint4*>(P.act + k1);
-      }
-#endif
       for (uint32_t kq = 4u * lane + 256u * part; kq < n_act; kq += 256u * SPLIT) {
         // the receiver's own select pass marked the sent words it lacks something in: skip the
         // rest without reading the holdings (most of them once a storm has spread; compacting the
-        // marked quads first measured no faster: the visits are latency-bound)
-#if SWIM_PULL_ACTSPEC == 2
-        const uint32_t lw = lw_n;
-        const uint4 a = a_n;
-        if (kq + 256u * SPLIT < n_act) {
-          const uint32_t k1 = kq + 256u * SPLIT;
-          lw_n = lackr ? lackr[k1 >> 5] : 0xFFFFFFFFu;
-          a_n = *reinterpret_cast<const uint4*>(P.act + k1);
-        }
-        if (!((lw >> (kq & 31u)) & 0xFu)) continue;
-#elif SWIM_PULL_ACTSPEC  // the list quad loaded beside its lack word, not after it (one round trip)
+        // marked quads first measured no faster: the visits are latency-bound). The list quad is
+        // loaded beside its lack word, not after it: one round trip per visited quad (C4's schedule
+        // pull 8.02 -> 7.82 ms per period; loading the next step's pair ahead too measured slower, §6.5)
         const uint32_t lw = lackr ? lackr[kq >> 5] : 0xFFFFFFFFu;
         const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
         if (!((lw >> (kq & 31u)) & 0xFu)) continue;
-#else
-        if (lackr && !((lackr[kq >> 5] >> (kq & 31u)) & 0xFu)) continue;
-        const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
-#endif
         uint32_t todo, anyall, anymix, ws0;
         uint32_t wcv[4], wsv[4], live[4], hw[4];
         bool quad;
         classify(kq, a, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
-        // (SWIM_PULL_NOSKIP: no branch on the holdings just loaded, so the senders' window loads
-        // issue beside them; a quad with nothing to do then costs its window loads)
-        if (!SWIM_PULL_NOSKIP && !todo) continue;
+        if (!todo) continue;
         deliver(kq, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
       }
 
@@ -2770,9 +2635,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
 // the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
 // per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
-#ifndef SWIM_PULL_LOSS_WAVES
 #define SWIM_PULL_LOSS_WAVES 6
-#endif
 __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) {
   pull_body<false, true>(P);
 }
@@ -2786,12 +2649,8 @@ __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss_
 #ifndef SWIM_APPLY_HLOG
 #define SWIM_APPLY_HLOG 14
 #endif
-#ifndef SWIM_APPLY_THREADS
 #define SWIM_APPLY_THREADS 1024
-#endif
-#ifndef SWIM_APPLY_PAIR
 #define SWIM_APPLY_PAIR 1
-#endif
 constexpr uint32_t HCAP_LOG = SWIM_APPLY_HLOG;
 constexpr uint32_t HCAP = 1u << HCAP_LOG;  // per-receiver LDS hash slots: 128 KiB of keys + values
 constexpr uint32_t HPROBE = 64;            // linear-probe bound; a key that finds no slot spills
@@ -3131,24 +2990,14 @@ constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per wor
 // 16-B entry-id loads in flight per lane on long ranges: 2 with 16-bit ids (8 per load), 4 with 32-bit
 // ids (large dictionaries: the half/half partition at 16,384 44.6 -> 40.3 ms per period; C3, on 16-bit
 // ids, 13.90 -> 14.11 at 4)
-#ifndef SWIM_AW_VILP
 #define SWIM_AW_VILP 2
-#endif
-#ifndef SWIM_AW_VILP32
 #define SWIM_AW_VILP32 4
-#endif
-#ifndef SWIM_AW_QILP
 #define SWIM_AW_QILP 2
-#endif
 constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
-#ifndef SWIM_AW_LONG
 #define SWIM_AW_LONG 256
-#endif
 // the merge pass tests AW_MC groups of 512 bitmap words (their merge marks) before it flattens their
 // blocks to merge together (fewer dependent rounds of loads per receiver than one group at a time)
-#ifndef SWIM_AW_MC
 #define SWIM_AW_MC 1
-#endif
 constexpr uint32_t AW_MC = SWIM_AW_MC;
 static_assert(AW_MC >= 1u && AW_MC <= 4u, "SWIM_AW_MC: 1..4 groups of 512 bitmap words");
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
@@ -3158,41 +3007,22 @@ constexpr uint32_t AW_LONG = SWIM_AW_LONG;
 __host__ __device__ __forceinline__ uint32_t aw_words(uint32_t dsids) { return dsids / 4u + AW_SPILL + 4u; }
 static_assert(AW_SPILL >= 1 && AW_SPILL <= 1024, "SWIM_APPLY_WSPILL out of range");
 
-// 1: a grid of as many workgroups as fit the chip, each wave walking the receiver list at a grid
-// stride; 0: a wave per possible receiver (the dispatcher hands out the list, waves past it return)
-#ifndef SWIM_AW_PERSIST
-#define SWIM_AW_PERSIST 1
-#endif
-#ifndef SWIM_AW_MINW
+// A grid of as many workgroups as fit the chip, each wave walking the receiver list at a grid stride
+// (a wave per possible receiver, the dispatcher handing out the list, measured slower: §6.5).
 #define SWIM_AW_MINW 4  // (the LDS bitmap caps the 8,192-block dictionary at 4 waves per SIMD anyway:
                         // registers beyond 128 would only lower that)
-#endif
-// SPLIT = 1: a wave per receiver. SPLIT = 4 (a build knob, off by default): the workgroup's 4 waves
-// share one receiver and one LDS bitmap, each taking every fourth group of receipt words and every
-// fourth group of bitmap words; workgroup barriers between the phases (every branch on the receiver is
-// workgroup-uniform). Measured slower on C2's 4,096 members (apply 0.70 -> 1.13 ms per period: the
-// barriers, and a 4,096-block dictionary's bitmap is two groups, so two waves merge; the parity file
-// green through it).
-#ifndef SWIM_APPLY_SPLIT_N
-#define SWIM_APPLY_SPLIT_N 0
-#endif
-constexpr uint32_t APPLY_SPLIT_N = SWIM_APPLY_SPLIT_N;  // shards of at most this many rows (and 16 per CU) apply 4 waves per receiver
-template <bool HD4, bool C16, uint32_t SPLIT = 1u>
+// A wave per receiver. (The workgroup's 4 waves sharing one receiver and one LDS bitmap measured
+// slower on C2's 4,096 members: apply 0.70 -> 1.13 ms per period, the workgroup barriers; §6.5.)
+template <bool HD4, bool C16>
 __device__ __forceinline__ void apply_b_body(const KP& P) {
-  static_assert(SPLIT == 1u || SPLIT == 4u, "apply_b_body: a wave or a workgroup per receiver");
   SWIM_GUARD(P);
   extern __shared__ uint32_t s_dyn[];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  const uint32_t part = wv % SPLIT;  // this wave's share of the receiver
-  auto bsync = [] {  // the receiver's waves (SPLIT > 1: the workgroup)
-    if (SPLIT > 1u) {
-      __syncthreads();
-    } else {
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    }
+  auto bsync = [] {  // the receiver's wave
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   };
-  uint32_t* s_bm = s_dyn + (wv / SPLIT) * aw_words(P.dsids);  // entry bitmap: all-zero between receivers
+  uint32_t* s_bm = s_dyn + wv * aw_words(P.dsids);  // entry bitmap: all-zero between receivers
   uint32_t* s_spl = s_bm + P.dsids / 4u;
   uint32_t* s_misc = s_spl + AW_SPILL;  // [0] spilled subjects
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, n_list = P.ctl->n_alist;
@@ -3224,7 +3054,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #else
 #define APPLYB_MARK(q)
 #endif
-  for (uint32_t t = lane + 64u * part; t < bw; t += 64u * SPLIT) s_bm[t] = 0u;
+  for (uint32_t t = lane; t < bw; t += 64u) s_bm[t] = 0u;
 #ifdef SWIM_APPLY_PROF
   unsigned long long t_w = 0, t_big = 0, t_short = 0, tq = 0;  // words / long ranges / short ranges
 #define APPLYB_SUB(acc)                \
@@ -3237,17 +3067,15 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
 #define APPLYB_SUB(acc)
 #endif
   APPLYB_MARK(0);
-  if (SPLIT > 1u) __syncthreads();  // the bitmap is clear
-  for (uint32_t li = (blockIdx.x * nwv + wv) / SPLIT; li < n_list; li += gridDim.x * nwv / SPLIT) {
+  for (uint32_t li = blockIdx.x * nwv + wv; li < n_list; li += gridDim.x * nwv) {
     const uint32_t p = P.alist[2 * li], total = P.alist[2 * li + 1];
     uint32_t* nbr = P.nb + lrow(P, p) * W32;
     const uint32_t nsw = (n_act + 31u) >> 5;
     const bool summ = nsw <= P.nsumw;
     const uint32_t* sumr = P.nsum + lrow(P, p) * P.nsumw;
     const uint8_t* hdrow = P.hd + lrow(P, p) * P.GC;
-    if (lane == 0 && part == 0u) {
+    if (lane == 0) {
       s_misc[0] = 0u;
-      s_misc[1] = 0u;
     }
     bsync();
     bool rowscan = false;  // the spill list overflowed: the round's claimed slots are scanned at the end
@@ -3432,9 +3260,9 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
     };
     if (!summ) {
-      for (uint32_t it0 = 64u * part; it0 < n_act; it0 += 64u * SPLIT) word(it0 + lane < n_act ? it0 + lane : NONE);
+      for (uint32_t it0 = 0; it0 < n_act; it0 += 64u) word(it0 + lane < n_act ? it0 + lane : NONE);
     } else {  // the summary's set bits, flattened across the wave
-      for (uint32_t c0 = 64u * part; c0 < nsw; c0 += 64u * SPLIT) {
+      for (uint32_t c0 = 0; c0 < nsw; c0 += 64u) {
         const uint32_t sb = c0 + lane < nsw ? sumr[c0 + lane] : 0u;
         uint32_t tot;
         const uint32_t off = wave_excl_scan((uint32_t)__popc(sb), &tot);
@@ -3474,7 +3302,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
     const uint4* mrow4 = reinterpret_cast<const uint4*>(mrow);
     const uint4* gen4 = reinterpret_cast<const uint4*>(P.d_gen);
     // AW_MC groups of 512 bitmap words are tested, then their blocks to merge flattened together
-    for (uint32_t t0 = 512u * AW_MC * part; t0 < bw; t0 += 512u * AW_MC * SPLIT) {
+    for (uint32_t t0 = 0; t0 < bw; t0 += 512u * AW_MC) {
       uint32_t bm[AW_MC];  // bit 4u + j of bm[ci]: word t0 + 512 ci + 64u + lane has set entries in its block j, not all marked
       uint32_t nzw = 0u;   // bit 8 ci + u: that word has set entries
 #pragma unroll
@@ -3572,15 +3400,14 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       for (uint32_t u = 0; u < 8u * AW_MC; ++u)
         if ((nzw >> u) & 1u) s_bm[t0 + 512u * (u >> 3) + 64u * (u & 7u) + lane] = 0u;
     }
-    if (SPLIT > 1u && __any(rowscan) && lane == 0) s_misc[1] = 1u;
     bsync();  // every merge of the receiver is done, its spill list complete
     APPLYB_MARK(2);
     const uint32_t nsp = min(s_misc[0], AW_SPILL);
-    if (SPLIT > 1u ? s_misc[1] != 0u : __any(rowscan)) {  // every spilled subject: this row's keys among the round's claimed slots
+    if (__any(rowscan)) {  // every spilled subject: this row's keys among the round's claimed slots
       __threadfence();
       const uint32_t nu = min(atomicAdd(&P.ctl->sp_n, 0u), P.spmask + 1u);
       const unsigned long long k0 = lrow(P, p) * (unsigned long long)P.W + 1ull, k1 = k0 + P.W;
-      for (uint32_t t = lane + 64u * part; t < nu; t += 64u * SPLIT) {
+      for (uint32_t t = lane; t < nu; t += 64u) {
         const uint32_t hs = P.sp_used[t];  // (another wave's entry may still be stale: keys filter it)
         const unsigned long long k = P.sp_key[hs];
         if (k < k0 || k >= k1) continue;
@@ -3589,13 +3416,13 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       }
     } else {
       if (nsp) __threadfence();
-      for (uint32_t t = lane + 64u * part; t < nsp; t += 64u * SPLIT) {
+      for (uint32_t t = lane; t < nsp; t += 64u) {
         const uint32_t hs = s_spl[t];
         apply(subj_of(P, spill_cell(P, hs)), atomicExch(&P.sp_val[hs], 0u));
       }
     }
-    if (lane == 0 && part == 0u) atomicAdd(&P.held[p], total);
-    nspills += lane == 0 && part == 0u ? s_misc[0] : 0u;
+    if (lane == 0) atomicAdd(&P.held[p], total);
+    nspills += lane == 0 ? s_misc[0] : 0u;
     bsync();  // the spill counter is reset for the next receiver
     APPLYB_MARK(3);
   }
@@ -3621,12 +3448,6 @@ __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b_
 __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16(KP P) { apply_b_body<false, true>(P); }
 __global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_h4(KP P) { apply_b_body<true, true>(P); }
 // small shards: a workgroup per receiver (16-bit ids: dictionaries of at most 8,192 blocks)
-__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_s4(KP P) {
-  apply_b_body<false, true, 4u>(P);
-}
-__global__ void __launch_bounds__(64 * AW_WAVES, SWIM_AW_MINW) k_gossip_apply_b16_h4_s4(KP P) {
-  apply_b_body<true, true, 4u>(P);
-}
 
 // hd4 handles, once a period: escape entries whose slot the row no longer holds with nibble 15
 // (swept, or rewritten with a small offset) become tombstones, so the table holds only live escapes
@@ -4468,9 +4289,7 @@ __device__ __forceinline__ void merge_row(const KP& P, uint32_t obs, const uint3
 // (sender, kind) order; each SYNC_ACK payload is j's table right after that request's merge.
 // SYNC merges at 6 waves per SIMD (80 VGPRs, 28–44 B of scratch) instead of their natural 5: the
 // fault-free steady state's merge / ack 23.9 / 17.7 -> 23.4 / 16.9 ms per 60 periods
-#ifndef SWIM_SYNC_WAVES
 #define SWIM_SYNC_WAVES 6
-#endif
 // A workgroup per listed member, over a grid of at most SY_GRID workgroups: a period's ~N/S
 // receivers (requesters), not a workgroup per member (65,536 launched workgroups took 29 us of the
 // fault-free period when ~1,800 had requests; a workgroup per 32 members serialised C3's heal merges).

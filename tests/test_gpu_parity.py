@@ -347,7 +347,10 @@ def test_refused_set_delay_leaves_the_handle_unchanged():
     crashed = scenarios.crash_ids(n, 3, 21)
     for c in (a, b):
         c.crash(crashed)
-    for _ in range(4):  # (the oracle takes ~100 s: ~3.5e7 GossipRequests per period from period 8 on)
+    # 12 periods after the crash, compared every 3. The oracle's cost grows with the storm: measured on
+    # the build container (one core), 12 periods take 67 s (3.2e8 GossipRequests) and 24 take 230 s
+    # (1.0e9), more than a third of the whole -m gpu suite's time, so the comparison stops at 12
+    for _ in range(4):
         for c in (a, b):
             c.step(3)
         assert a.digest() == b.digest()
