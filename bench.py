@@ -51,6 +51,13 @@ WORKLOADS = {
                         "through the seeds",
                    n=65536, preset="lan", loss=0.0, crash=0.10, part=120, part_group=16, gcap=1 << 18,
                    scap=8192, seeds=16),
+    # C3 on the column-allocated layout (N x K views with K = N: a subject gets a column when some row
+    # first changes its record, so the touched columns are the first ones of every row and SYNC
+    # payloads stream them)
+    "c3k": dict(desc="C3 on column-allocated views (K = N): 65,536 members, LAN defaults, 10% simultaneous crash + "
+                     "2-way partition (16-member group) for 40 periods healed via SYNC",
+                n=65536, preset="lan", loss=0.0, crash=0.10, part=40, part_group=16, gcap=1 << 17, scap=8192,
+                tracked=65536),
     "c3s": dict(desc="C3 geometry: 65,536 members, dense N x N views, LAN defaults, 0.1% simultaneous crash",
                 n=65536, preset="lan", loss=0.0, crash=0.001, part=0, gcap=1 << 16),
     "c3crash": dict(desc="65,536 members, dense, LAN defaults, 10% simultaneous crash, no partition",

@@ -216,6 +216,7 @@ struct Member {
   GossipMap gossips;                    // GPI:49 gossips
   std::unordered_map<uint32_t, std::vector<Batch>> recv;  // sender -> batches (infected sets)
   uint32_t gossip_seq = 0;              // GPI:48 gossipCounter
+  uint32_t foreign_seq = 0;             // gossips forwarded for real nodes (their own id namespace)
   uint32_t sync_fd = 0xFFFFFFFFu;       // FD-triggered SYNC target of this period (MPI:385-397)
   bool alive = true;
   // graceful leave (MPI:203-212): the gossip of its own DEAD record; the member shuts down once
@@ -474,9 +475,13 @@ void window_update(oracle_handle* h, GossipMap& g, int64_t r, int32_t spread) {
 
 // GossipProtocolImpl.spread -> createAndPutGossip (GPI:124-128,163-169,211-213): the new
 // gossip's infectionPeriod is the gossip module's *next* round (`currentPeriod`).
-void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t record, int64_t create_round) {
+// foreign: a real node's gossip the member forwards (SWIM_DELIVER_FORWARD): onGossipReq puts it under
+// its own gossipId (GPI:171-183) and the member's gossipCounter does not move; it gets an id of the
+// member's foreign namespace (0x80000000 | k) instead
+void spread_gossip(oracle_handle* h, uint32_t origin, uint32_t subject, uint32_t record, int64_t create_round,
+                   bool foreign = false) {
   Member& o = h->m[origin];
-  uint32_t seq = o.gossip_seq++;
+  uint32_t seq = foreign ? (0x80000000u | o.foreign_seq++) : o.gossip_seq++;
   const uint32_t gid = (uint32_t)h->registry.size();
   h->registry.push_back(Gossip{origin, seq, subject, record, ghash(origin, seq), create_round, 0, 0});
   gossip_reserve(h, gid + 1);
@@ -1328,7 +1333,7 @@ int oracle_deliver_records(oracle_handle* h, uint32_t obs, const uint32_t* subj,
   if (!me.alive) return SWIM_OK;
   const uint32_t tick = tick_of(h, 0), snap = me.others;
   for (uint32_t k = 0; k < n; ++k) {
-    if (fwd) spread_gossip(h, obs, subj[k], rec[k], (int64_t)h->period * h->G);
+    if (fwd) spread_gossip(h, obs, subj[k], rec[k], (int64_t)h->period * h->G, true);
     update_membership(h, obs, subj[k], rec[k], reason, 0, SWIM_DELIVER_ATTEMPT | k, tick, snap,
                       (int64_t)h->period * h->G);
   }

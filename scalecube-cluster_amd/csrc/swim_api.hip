@@ -85,6 +85,14 @@ struct swim_handle {
   uint32_t out_pairs[SWIM_MAX_WORLD] = {0};
   unsigned long long* d_digest = nullptr;
   uint32_t* d_scan = nullptr;  // k_scan_tiles sums and their exclusive scan
+  // quiet periods: the gossip rounds of a period in which no member holds a gossip are
+  // skipped (one k_quiet_rounds instead of ~15 launches per round). The test runs after the FD commit,
+  // every period while the last one was quiet and every QUIET_EVERY-th period otherwise (a host stop)
+  bool quiet_skip = true;   // SWIMHIP_QUIET=0 at swim_create: always run the rounds (tests: A/B)
+  bool last_quiet = false;
+  uint64_t quiet_periods = 0;
+  uint32_t* d_quiet = nullptr;
+  uint32_t* h_quiet = nullptr;  // pinned
   std::vector<void*> allocs;
   // library-driven exchanges (swim_shard_set_transport / swim_shard_comm_init)
   swim_transport tr{};
@@ -145,6 +153,8 @@ void free_all(swim_handle* h) {
   h->comm = nullptr;
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  if (h->h_quiet) (void)hipHostFree(h->h_quiet);
+  h->h_quiet = nullptr;
   for (auto ev : h->pool) (void)hipEventDestroy(ev);
   for (auto& pe : h->pending) {
     (void)hipEventDestroy(pe.a);
@@ -408,6 +418,36 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   return commit_sorted(h, P, nullptr, total);
 }
 
+// Quiet periods: after the FD commit, may any member hold a gossip in this period's
+// rounds (k_quiet_check)? If none may, the rounds' bookkeeping is written in one launch and the
+// period goes on at the suspicion phase: ~15 launches per round fewer, and on sharded handles 4
+// exchanges per round fewer. The test reads replicated state on sharded handles (the ring, wlast and
+// the commit counts are the same on every shard after the commit exchange), so every rank takes the
+// same branch; the exchange status rows carry the resume point (tr_status), so ranks that did not
+// would fail together instead of exchanging mismatched buffers. Handles with delayed-message rings,
+// leaves or joins in flight always run their rounds.
+constexpr uint64_t QUIET_EVERY = 8;  // periods between tests while the last test found gossips held
+int quiet_rounds(swim_handle* h, bool* quiet) {
+  *quiet = false;
+  if (!h->quiet_skip || h->base.dq || h->n_leaving || h->base.njoin) return SWIM_OK;
+  if (!h->last_quiet && h->period % QUIET_EVERY != 0) return SWIM_OK;
+  hipStream_t s = h->stream;
+  KP Q;
+  set_phase(h, Q, 1);  // the period's first gossip round
+  hipLaunchKernelGGL(k_quiet_check, dim3(1), dim3(1024), 0, s, Q, Q.round, h->d_quiet);
+  HIPC(h, hipMemcpyAsync(h->h_quiet, h->d_quiet, 4, hipMemcpyDeviceToHost, s));
+  HIPC(h, hipStreamSynchronize(s));
+  h->last_quiet = *h->h_quiet == 0u;
+  if (!h->last_quiet) return SWIM_OK;
+  timed(h, 7, "k_quiet_rounds", [&] {
+    hipLaunchKernelGGL(k_quiet_rounds, dim3(blocks_for(h->base.nloc, 256)), dim3(256), 0, s, Q, Q.round, h->G);
+    if (h->dict_on) hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, Q.dsids / 256)), dim3(256), 0, s, Q);
+  });
+  h->quiet_periods++;
+  *quiet = true;
+  return SWIM_OK;
+}
+
 // Runs the current period from h->pc. Returns SWIM_OK with x->op = SWIM_X_DONE at the end of
 // the period, or SWIM_OK with another op when an exchange must happen first (world > 1).
 int period_resume(swim_handle* h, swim_xchg* x) {
@@ -455,11 +495,14 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (commit_begin(h, P, x, &rc)) return SWIM_OK;
         if (rc) return rc;
         break;
-      case PC_FD_C:
+      case PC_FD_C: {
         if (SH && (rc = commit_end(h, P, x))) return rc;
         h->q = 0;
-        h->pc = PC_R_MAX;
+        bool quiet = false;
+        if ((rc = quiet_rounds(h, &quiet))) return rc;
+        h->pc = quiet ? PC_SUSP : PC_R_MAX;
         break;
+      }
       case PC_R_MAX:  // phases 1..G: gossip rounds
         set_phase(h, P, 1 + h->q);
         h->pc = PC_R_SEL;
@@ -731,22 +774,37 @@ int rccl_alltoallv(void* ctx, const void* send, const uint64_t* sb, void* recv, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint64_t so = 0, ro = 0;
   if (ncclGroupStart() != ncclSuccess) return -1;
-  for (uint32_t q = 0; q < h->world; ++q) {
+  bool ok = true;
+  for (uint32_t q = 0; q < h->world && ok; ++q) {
     if (sb[q] && ncclSend(static_cast<const uint8_t*>(send) + so, sb[q], ncclUint8, (int)q, h->comm, s) != ncclSuccess)
-      return -1;
-    if (rb[q] && ncclRecv(static_cast<uint8_t*>(recv) + ro, rb[q], ncclUint8, (int)q, h->comm, s) != ncclSuccess)
-      return -1;
+      ok = false;
+    if (ok && rb[q] && ncclRecv(static_cast<uint8_t*>(recv) + ro, rb[q], ncclUint8, (int)q, h->comm, s) != ncclSuccess)
+      ok = false;
     so += sb[q];
     ro += rb[q];
   }
-  return ncclGroupEnd() == ncclSuccess ? 0 : -1;
+  const bool ended = ncclGroupEnd() == ncclSuccess;  // (the group is closed on every path)
+  return ok && ended ? 0 : -1;
 }
 
 // One all-gather of n bytes per rank through the transport (send / recv: device buffers)
+// A collective that failed on this rank leaves its peers inside theirs: the library-owned communicator
+// is aborted (ncclCommAbort), so this rank's later calls fail at once instead of posting into a broken
+// group, and the peers' RCCL calls return an error or time out (RCCL has no cross-rank notification; a
+// host transport's own timeout, e.g. gloo's, ends the peers' wait there).
+int tr_broken(swim_handle* h, const char* what) {
+  if (h->comm) {
+    (void)ncclCommAbort(h->comm);
+    h->comm = nullptr;
+    h->has_tr = false;
+  }
+  return fail(h, SWIM_ERCCL, what);
+}
+
 int tr_allgather(swim_handle* h, const void* send, void* recv, uint64_t n) {
   if (!h->tr.host_staged) {
     if (h->tr.allgather(h->tr.ctx, send, recv, n, h->stream))
-      return fail(h, SWIM_ERCCL, "shard exchange: all-gather failed");
+      return tr_broken(h, "shard exchange: all-gather failed");
     return SWIM_OK;
   }
   const uint64_t W = h->world;
@@ -763,7 +821,7 @@ int tr_allgather(swim_handle* h, const void* send, void* recv, uint64_t n) {
 int tr_alltoallv(swim_handle* h, const uint64_t* sb, const uint64_t* rb) {
   if (!h->tr.host_staged) {
     if (h->tr.alltoallv(h->tr.ctx, h->xsend, sb, h->xrecv, rb, h->stream))
-      return fail(h, SWIM_ERCCL, "shard exchange: all-to-all-v failed");
+      return tr_broken(h, "shard exchange: all-to-all-v failed");
     return SWIM_OK;
   }
   uint64_t st = 0, rt = 0;
@@ -790,7 +848,8 @@ int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t
   const uint32_t W = h->world, R = 2u + W;
   std::vector<uint64_t> row(R, 0ull);
   row[0] = (uint64_t)(int64_t)code;
-  row[1] = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | x.op);
+  // (the resume point too: ranks that took different branches of a period fail here, "out of step")
+  row[1] = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | (uint64_t)(uint32_t)h->pc << 8 | x.op);
   if (!code && x.op == SWIM_X_ALLGATHER) row[2] = x.send_words;
   if (!code && x.op == SWIM_X_ALLTOALLV)
     for (uint32_t q = 0; q < W; ++q) row[2 + q] = x.send_counts[q];
@@ -1144,6 +1203,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.g_epoch, N);
   ALLOC(P.g_cursor, N);
   ALLOC(P.gseq, N);
+  ALLOC(P.fseq, N);
   ALLOC(P.sync_fd, N);
   ALLOC(P.peers, (size_t)N * c.gossip_fanout);
   ALLOC(P.npeers, N);
@@ -1268,7 +1328,11 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.stat_shards, (size_t)STAT_SHARDS * STAT_STRIDE);
   ALLOC(h->d_digest, 2);
   ALLOC(h->d_scan, 2ull * ((N + SCAN_TILE - 1) / SCAN_TILE));
+  ALLOC(h->d_quiet, 1);
 #undef ALLOC
+  if (rc == SWIM_OK && hipHostMalloc(reinterpret_cast<void**>(&h->h_quiet), 4, hipHostMallocDefault) != hipSuccess)
+    rc = fail(h, SWIM_ENOMEM, "hipHostMalloc(4 B)");
+  if (const char* e = std::getenv("SWIMHIP_QUIET")) h->quiet_skip = *e != '0';
   P.group = group;
   if (rc != SWIM_OK) {
     std::fprintf(stderr, "swim_create: %s\n", h->err.c_str());
@@ -1330,6 +1394,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   (void)hipMemsetAsync(P.g_epoch, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.g_cursor, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.gseq, 0, (size_t)N * 4, s);
+  (void)hipMemsetAsync(P.fseq, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.in_cnt, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.nb, 0, NL * (h->GC / 32) * 4, s);
   (void)hipMemsetAsync(P.g_create, 0, (size_t)h->GC * 4, s);
@@ -1994,6 +2059,7 @@ int swim_stats_get(swim_handle* h, swim_stats* out) {
   out->commit_radix = stats[ST_COMMIT_RADIX];
   out->apply_skipped = stats[ST_APPLY_SKIP];
   out->apply_bitmaps = stats[ST_APPLY_RBM];
+  out->quiet_periods = h->quiet_periods;
   out->apply_bitmap_records = stats[ST_APPLY_RBREC];
   out->escape_entries = ctl.hx_live;
   out->escape_capacity = h->base.hd4 ? (uint64_t)h->base.hxmask + 1u : 0u;

@@ -92,6 +92,12 @@ enum IfromOverflow : uint32_t {
                        // or inside the horizon
 };
 
+// the gossip-id sequence of gossips a simulated member forwards for a real node (k_deliver): a real
+// node's gossip keeps its own id in the reference (GossipProtocolImpl.onGossipReq puts it under its
+// gossipId, :171-183) and never advances the forwarding member's gossipCounter (:48, createAndPutGossip
+// :163-169); here it is re-emitted by the forwarding member under FOREIGN_SEQ | fseq[member]
+constexpr uint32_t FOREIGN_SEQ = 0x80000000u;
+
 constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
@@ -247,6 +253,8 @@ struct KP {
   uint32_t* g_epoch;
   uint32_t* g_cursor;
   uint32_t* gseq;
+  uint32_t* fseq;  // [N] gossips a member forwarded for a real node (SWIM_DELIVER_FORWARD): their own id
+                   // namespace (FOREIGN_SEQ | fseq), so the member's gossipCounter (gseq) is not advanced
   uint32_t* sync_fd;
   uint32_t* peers;   // [N][f] gossip peers chosen this round
   uint32_t* npeers;  // [N]

@@ -145,8 +145,8 @@ __global__ void k_deliver(KP P, uint32_t obs, const uint32_t* subj, const uint32
     const uint32_t snap = P.cnt[obs];
     for (uint32_t k = 0; k < n; ++k) {
       const uint32_t j = subj[k], r1 = rec[k];
-      if (fwd) {
-        emit_gossip(P, obs, j, r1, P.gseq[obs]++);
+      if (fwd) {  // (its own id namespace: the member's gossipCounter does not move, GPI:171-183)
+        emit_gossip(P, obs, j, r1, FOREIGN_SEQ | P.fseq[obs]++);
         ++created;
       }
       if (P.nxk && P.colmap[j] == NONE && r1 == BASELINE) continue;
@@ -220,6 +220,7 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
     P.cnt_delta[x] = 0;
     P.fd_epoch[x] = P.fd_cursor[x] = P.g_epoch[x] = P.g_cursor[x] = 0u;
     P.gseq[x] = 0u;
+    P.fseq[x] = 0u;
     P.sync_fd[x] = NONE;
     P.held[x] = 0u;
     P.ih_head[x] = 0u;
@@ -1527,6 +1528,75 @@ __global__ void __launch_bounds__(1024) k_gossip_prep(KP P) {
     c->n_act = base;
     c->w_beg = w_beg;
     c->wbeg_hist[P.round & 255u] = w_beg;
+  }
+}
+
+// ---- quiet periods ("Quiet periods") ----
+// After a period's FD commit: may any member still hold a gossip at the period's first round r0?
+// k_gossip_prep's own test (a word is held while wlast + sweepmax >= round) over the whole live
+// range. When none is, every gossip round of the period is a no-op for every kernel of the round:
+// nothing is listed (select returns at once, GossipProtocolImpl.java:144-146 "gossips non-empty"),
+// nobody registers with a peer, so nothing is pulled, recorded, applied, created or committed; wlast
+// and the ring only grow through those kernels, so the answer holds for every round of the period.
+// out[0] = 1: the rounds run (a word may be held, or the run has failed and prep must see it).
+__global__ void __launch_bounds__(1024) k_quiet_check(KP P, uint32_t r0, uint32_t* out) {
+  __shared__ uint32_t s_busy;
+  const Ctl* c = P.ctl;
+  if (threadIdx.x == 0) s_busy = c->overflow ? 1u : 0u;
+  __syncthreads();
+  const uint32_t hi0 = c->gcount, lo0 = c->glo;
+  const uint32_t lo1 = hi0 - lo0 > P.GC ? hi0 - P.GC : lo0;
+  bool busy = false;
+  for (uint32_t wi = (lo1 >> 5) + threadIdx.x; wi < ((hi0 + 31u) >> 5); wi += blockDim.x)
+    if (P.wlast[wmod(P, wi)] + P.sweepmax >= r0) {
+      busy = true;
+      break;
+    }
+  if (busy) s_busy = 1u;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = s_busy;
+}
+
+// What the G skipped rounds r0 .. r0 + G - 1 of a quiet period leave behind, written at once: the
+// per-round bookkeeping of k_gossip_prep listing nothing (the oldest-live pointer at the ring's end,
+// the record-pool fills and list starts of each round), select's empty peer counts, the
+// in-history heads k_gossip_inhist files per round, pull's cleared registrations and each round's
+// empty commit (k_commit of no gossips: g_prev / c_prev at the counts). The host then runs
+// k_dict_free once, as the first round's commit would have (the rounds after it free nothing more).
+__global__ void __launch_bounds__(256) k_quiet_rounds(KP P, uint32_t r0, uint32_t G) {
+  Ctl* c = P.ctl;
+  const uint32_t hi = c->gcount;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t w_beg = (hi >> 5) & ~3u;
+    c->glo = hi;
+    c->sp_n = 0u;
+    c->n_act = 0u;
+    c->w_beg = w_beg;
+    c->n_alist = c->n_inov = c->sp_cnt = c->rp_cnt = c->pw_used = 0u;
+    c->scan_lo = c->scan_hi = hi;
+    for (uint32_t q = 0; q < G; ++q) {
+      const uint32_t r = (r0 + q) & 255u;
+      c->rs_rec[r] = c->rec_cnt;
+      c->rs_body[r] = c->body_cnt;
+      c->wbeg_hist[r] = w_beg;
+    }
+    c->g_prev = hi;
+    c->c_prev = c->ccount;
+  }
+  const uint32_t m = P.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= P.row0 + P.nloc) return;
+  P.npeers[m] = 0u;
+  P.in_cnt[m] = 0u;
+  const uint32_t ihh = P.ih_head[m];
+  uint32_t* rh = P.ih_rhead + lrow(P, m) * 256u;
+  for (uint32_t q = 0; q < G; ++q) rh[(r0 + q) & 255u] = ihh;
+  if (m == P.dbg_watch) {
+    for (uint32_t q = 0; q < G; ++q) {
+      uint32_t* L = P.dbg_log + ((r0 + q) & 255u) * 8u;
+      L[0] = r0 + q;
+      L[1] = L[2] = L[3] = 0u;
+      L[4] = L[5] = L[6] = NONE;
+    }
   }
 }
 

@@ -126,6 +126,7 @@ STAT_FIELDS = [
     "apply_skipped",
     "apply_bitmaps",
     "apply_bitmap_records",
+    "quiet_periods",
 ]
 
 

@@ -195,6 +195,8 @@ class ShardedSwimCluster(SwimCluster):
 
     def step(self, periods: int = 1):
         if self._lib_x:
+            if getattr(self, "_cb_errors", None):  # a failure of an earlier step is not this step's cause
+                self._cb_errors.clear()
             try:
                 self._call("step", self._h, int(periods))
             except SwimError:
@@ -280,7 +282,7 @@ class ShardedSwimCluster(SwimCluster):
         last = np.max([p[1] for p in parts], axis=0).astype(np.uint32)
         return pres, last
 
-    _SAME = ("period", "live_gossip_slots", "live_gossip_records")
+    _SAME = ("period", "live_gossip_slots", "live_gossip_records", "quiet_periods")
 
     def stats(self) -> dict:
         parts = self._gather_objects(SwimCluster.stats(self))

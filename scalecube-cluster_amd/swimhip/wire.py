@@ -403,15 +403,19 @@ def _seen_ids(cluster, observer: int) -> dict:
     return seen.setdefault(int(observer), {})
 
 
-def _sweep_periods(cluster) -> int:
-    """Periods a received gossip stays in `gossips`: gossipPeriodsToSweep gossip rounds
-    (ClusterMath.java:99-102) at the cluster's size, rounded up to whole periods, + 1."""
+def _sweep_periods(cluster, observer: int) -> int:
+    """Periods a received gossip stays in the observer's `gossips`. sweepGossips (GossipProtocolImpl.java:
+    280-303) drops a GossipState in the first gossip round r with r > infectionPeriod + periodsToSweep,
+    periodsToSweep = gossipPeriodsToSweep(repeatMult, remoteMembers.size() + 1) (ClusterMath.java:99-102)
+    at the observer's table size. A gossip delivered before period p has infectionPeriod p * G (G gossip
+    rounds per period), so the round that drops it is p * G + sweep + 1, in period p + (sweep + 1) // G:
+    it is held until that period has run (the table size taken at delivery)."""
     from .cluster_math import gossipPeriodsToSweep
 
     g = cluster.config.gossipConfig()
     rounds_per_period = max(1, cluster.config.failureDetectorConfig().pingInterval() // g.gossipInterval())
-    sweep = gossipPeriodsToSweep(g.gossipRepeatMult(), cluster.n)
-    return -(-sweep // rounds_per_period) + 1
+    sweep = gossipPeriodsToSweep(g.gossipRepeatMult(), len(cluster.members(observer)))
+    return (sweep + 1) // rounds_per_period + 1
 
 
 def deliver(cluster, observer: int, msg: Message, directory: Directory, sync_group: str = "default") -> int:
@@ -445,7 +449,7 @@ def deliver(cluster, observer: int, msg: Message, directory: Directory, sync_gro
         for g in data.gossips:
             if g.gossipId in seen:
                 continue
-            seen[g.gossipId] = now + _sweep_periods(cluster)
+            seen[g.gossipId] = now + _sweep_periods(cluster, observer)
             if g.message.qualifier == MEMBERSHIP_GOSSIP and isinstance(g.message.data, MembershipRecord):
                 recs.append(g.message.data)
         subj, rec = decoded_records(recs, directory)

@@ -1,12 +1,20 @@
-"""C4's node run rehearsed on one GPU: BASELINE configs[3]'s schedule (LAN, 1 %
-loss, 0.1 % simultaneous crash after a 5-period warmup) at 32,768 members, dense views row-sharded
-over 8 ranks (8 processes sharing cuda:0, gloo, the library-driven exchanges), against the unsharded
-handle on rank 0: view and deadline digests, every parity counter and the presence vectors equal
-every 4 periods through the storm the 1 % loss starts (false suspicions re-spread by SYNC,
-MembershipProtocolImpl.java:649-656; one GossipRequest per gossip, each lost independently,
-GossipProtocolImpl.java:225-239 / NetworkEmulator.java:166-180), and no buffer overflows."""
+"""C4's and C5's node runs rehearsed on one GPU: the schedules of
+BASELINE configs[3] and [4], row-sharded over 8 ranks (8 processes sharing cuda:0, gloo, the
+library-driven exchanges), against the unsharded handle on rank 0: view and deadline digests, every
+parity counter and the presence vectors equal every few periods, and no buffer overflows.
+
+* C4 (LAN, 1 % loss, 0.1 % simultaneous crash after a 5-period warmup), dense views: at 32,768 members
+  for 24 periods, and at 65,536 members (the largest dense N for which 8 shards plus the unsharded
+  handle fit one MI355X's 288 GB) through 44 storm periods. The 1 % loss starts a storm (false
+  suspicions re-spread by SYNC, MembershipProtocolImpl.java:649-656; one GossipRequest per gossip,
+  each lost independently, GossipProtocolImpl.java:225-239 / NetworkEmulator.java:166-180).
+* C5 (LAN, N x K views with K = 256, 256 simultaneous crashes = concurrent churn): at 131,072 members
+  through 100 periods, past the first suspicion timeouts (5 x bit_length(131,071) = 85 periods of
+  suspicion, MembershipProtocolImpl.java:620-647, then the DEAD gossips, GossipProtocolImpl.java:171-183).
+"""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -14,10 +22,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-N = 32768
-WORLD = 8
 SEED = 41
-WARMUP, PERIODS, EVERY = 5, 24, 4
 
 
 def _free_port():
@@ -26,7 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port):
+def _worker(rank, world, port, n, kw, loss, n_crash, warmup, periods, every, min_timeouts):
     import scenarios
     from swimhip import ClusterConfig, SwimCluster
     from swimhip.sharded import ShardedSwimCluster
@@ -37,36 +42,58 @@ def _worker(rank, world, port):
     torch.cuda.set_device(0)
     try:
         cfg = ClusterConfig.defaultLanConfig()
-        kw = dict(gossip_capacity=1 << 18, sync_capacity=2048)
-        a = ShardedSwimCluster(cfg, N, SEED, **kw)
-        b = SwimCluster(cfg, N, SEED, **kw) if rank == 0 else None
-        crashed = scenarios.crash_ids(N, N // 1000, SEED)
+        a = ShardedSwimCluster(cfg, n, SEED, **kw)
+        b = SwimCluster(cfg, n, SEED, **kw) if rank == 0 else None
+        crashed = scenarios.crash_ids(n, n_crash, SEED)
+        t0 = time.perf_counter()
         for c in (a, b):
             if c is not None:
-                c.set_loss(1.0)
-                c.step(WARMUP)
+                if loss:
+                    c.set_loss(loss)
+                c.step(warmup)
                 c.crash(crashed)
-        for t in range(PERIODS // EVERY):
-            a.step(EVERY)
+        for t in range(periods // every):
+            a.step(every)
             if b is not None:
-                b.step(EVERY)
+                b.step(every)
             da, sa, pa = a.digest(), a.stats(), a.presence()  # (collective)
             if rank == 0:
                 db, sb, pb = b.digest(), b.stats(), b.presence()
+                p = warmup + every * (t + 1)
                 bad = {k: (sa[k], sb[k]) for k in scenarios.PARITY_KEYS if sa[k] != sb[k]}
-                assert not bad, f"period {WARMUP + EVERY * (t + 1)}: counters differ {bad}"
-                assert da == db, f"period {WARMUP + EVERY * (t + 1)}: digests differ"
+                assert not bad, f"period {p}: counters differ {bad}"
+                assert da == db, f"period {p}: digests differ"
                 assert np.array_equal(pa[0], pb[0]) and np.array_equal(pa[1], pb[1])
                 assert sa["overflow"] == 0 and sb["overflow"] == 0
-                print(f"period {WARMUP + EVERY * (t + 1)}: equal; gossips {sb['gossips_created']}, live slots "
-                      f"{sb['live_gossip_slots']}, removed {sb['events_removed']}", flush=True)
+                print(f"period {p}: equal; gossips {sb['gossips_created']}, live slots {sb['live_gossip_slots']}, "
+                      f"timeouts {sb['suspicion_timeouts']}, removed {sb['events_removed']}, "
+                      f"{time.perf_counter() - t0:.1f} s", flush=True)
         if rank == 0:
             s = b.stats()
-            assert s["gossips_created"] > 0 and s["suspicion_timeouts"] >= 0
+            assert s["gossips_created"] > 0 and s["suspicion_timeouts"] >= min_timeouts
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
 def test_c4_schedule_32768_world8_matches_unsharded():
-    mp.spawn(_worker, args=(WORLD, _free_port()), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(8, _free_port(), 32768, dict(gossip_capacity=1 << 18, sync_capacity=2048), 1.0, 32, 5,
+                            24, 4, 0), nprocs=8, join=True)
+
+
+@pytest.mark.gpu
+def test_c4_schedule_65536_world8_matches_unsharded():
+    """C4's schedule at 65,536 members: 8 shards of 8,192 rows plus the unsharded handle (a 2^19-slot
+    ring each, 2x the ~2.6e5 live one-gossip slots of the storm's peak at this N),
+    compared every 4 periods through 44 storm periods."""
+    mp.spawn(_worker, args=(8, _free_port(), 65536, dict(gossip_capacity=1 << 19, sync_capacity=4096), 1.0, 66, 5,
+                            44, 4, 0), nprocs=8, join=True)
+
+
+@pytest.mark.gpu
+def test_c5_schedule_131072_world8_matches_unsharded():
+    """C5's schedule at 131,072 members (N x K, K = 256, 256 simultaneous crashes) over 8 shards,
+    compared every 5 periods through 100 periods: the crashed members' suspicion timeouts fire (every
+    alive observer removes all 256) within the window."""
+    mp.spawn(_worker, args=(8, _free_port(), 1 << 17, dict(gossip_capacity=1 << 17, tracked_subjects=256), 0.0,
+                            256, 3, 100, 5, 1), nprocs=8, join=True)

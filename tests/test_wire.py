@@ -159,14 +159,18 @@ def test_gossip_request_is_forwarded_once_per_id():
     c.step(2)
     gossip = wire.membership_gossip_request(d, 9, 0, wire.MembershipRecord(d[7], "SUSPECT", 0))
     before = c.stats()["gossips_created"]
+    seq0 = c.debug_member_state()["gossip_seq"].copy()
     assert wire.deliver(c, 3, gossip, d) == 1
     assert c.stats()["gossips_created"] == before + 1  # the forwarded copy
+    # the forward keeps the real node's id namespace: member 3's gossipCounter (GPI:48) does not move, so
+    # the ids of the gossips it creates itself later are the reference's
+    assert np.array_equal(c.debug_member_state()["gossip_seq"], seq0)
     assert c.view(3)[7] == nat.pack(0, nat.SUSPECT)
     assert wire.deliver(c, 3, gossip, d) == 0  # a repeat of a held id
     assert c.stats()["gossips_created"] == before + 1
     c.step(1)  # the forward reaches the other simulated members (10 rounds per local period)
     assert sum(1 for i in range(n) if c.view(i)[7] in (nat.pack(0, nat.SUSPECT), nat.pack(1, nat.ALIVE))) == n
-    c.step(wire._sweep_periods(c))
+    c.step(wire._sweep_periods(c, 3))
     assert wire.deliver(c, 3, gossip, d) == 1  # swept: new again
 
 
@@ -222,8 +226,10 @@ def test_delivered_records_match_oracle(tracked):
         c.step(2)
         assert wire.deliver(c, 12, sync, d) == n      # ALIVE inc 2 about 12 itself: refuted with inc 3
         assert wire.deliver(c, 3, sync, d) == n       # 3 refutes its SUSPECT
+        seq30 = c.debug_member_state()["gossip_seq"][30]
         assert wire.deliver(c, 30, gossip, d) == 1    # MEMBERSHIP_GOSSIP: applied and forwarded
         assert wire.deliver(c, 30, gossip, d) == 0    # the same id again: dropped
+        assert c.debug_member_state()["gossip_seq"][30] == seq30  # (a foreign id: the counter stays)
     for _ in range(4):
         for c in (a, b):
             c.step(3)
