@@ -122,7 +122,7 @@ typedef struct swim_config {
                                view. More than K such subjects -> SWIM_EOVERFLOW */
   uint32_t n_initial;       /* members started (converged) at create: ids [0, n_initial); 0 = all
                                N. Ids [n_initial, N) are spare slots, absent from every view, for
-                               swim_join / swim_restart (dense, unsharded handles only)          */
+                               swim_join / swim_restart (dense handles, sharded or not)          */
   int32_t device;           /* HIP device ordinal the handle lives on                     */
   uint32_t shard_rank;      /* observer-row shard of this handle (0 .. shard_world-1)     */
   uint32_t shard_world;     /* shards of the cluster (0 or 1 = unsharded); see swim_shard_step */
@@ -257,7 +257,9 @@ int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n);
  * (MembershipProtocolImpl.java:130-139), and in that period's SYNC phase makes the initial SYNC to
  * every seed address (start0, :222-257); the first SYNC_ACK that comes back (lowest seed address
  * whose round trip is delivered) is merged with reason INITIAL_SYNC (not re-spread, :649-656).
- * Periodic doSync follows the usual stagger from the next period on. Dense, unsharded handles. */
+ * Periodic doSync follows the usual stagger from the next period on. Dense handles; a sharded handle
+ * takes the same call on every rank (an initial SYNC to a seed on another shard travels in the SYNC
+ * exchange). */
 int swim_join(swim_handle* h, const uint32_t* ids, uint32_t n);
 /* Restart on the same address (MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses,
  * :453-520): stopped member old_ids[k]'s address is taken by spare slot new_ids[k], a NEW member id
@@ -265,7 +267,7 @@ int swim_join(swim_handle* h, const uint32_t* ids, uint32_t n);
  * DEST_GONE, so the prober's FD emits DEAD for the old id (FailureDetectorImpl.java:231-235,383);
  * a metadata request for the old id fails (MetadataStoreImpl.java:216-223); gossip and SYNC are
  * handled by the new member, which ignores records of other ids at its own address
- * (MembershipProtocolImpl.java:499-505). Dense, unsharded handles. */
+ * (MembershipProtocolImpl.java:499-505). Dense handles, sharded or not (as swim_join). */
 int swim_restart(swim_handle* h, const uint32_t* old_ids, const uint32_t* new_ids, uint32_t n);
 
 /* GossipProtocol.spread (GossipProtocol.java:12-29, GossipProtocolImpl.java:124-128): member

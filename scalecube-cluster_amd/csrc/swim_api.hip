@@ -949,7 +949,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   *out = nullptr;
   const swim_config& c = *cfg;
   if (c.n_members < 2 || c.n_members > (1u << 20) || c.mode > 1 || c.n_initial > c.n_members ||
-      (c.n_initial && c.n_initial < c.n_members && (c.mode != 0 || c.shard_world > 1)) ||
+      (c.n_initial && c.n_initial < c.n_members && c.mode != 0) ||
       (c.mode == 1 && (c.tracked_subjects < 1 || c.tracked_subjects > c.n_members)) ||
       c.ping_interval_ms <= 0 ||
       c.gossip_interval_ms <= 0 || c.gossip_fanout < 1 || c.gossip_fanout > MAXF || c.ping_req_members < 0 ||
@@ -1197,6 +1197,8 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   ALLOC(P.joining, N);
   ALLOC(P.jslot, N);
   ALLOC(P.jwin, N);
+  ALLOC(P.jsend, N);
+  ALLOC(P.jack_ref, N);
   ALLOC(group, N);
   ALLOC(P.fd_epoch, N);
   ALLOC(P.fd_cursor, N);
@@ -1372,15 +1374,13 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     (void)hipMemsetAsync(P.track_req, 0, (size_t)N * 4, s);
   }
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.cnt, (size_t)N, n0 - 1);
-  // presence is per shard: observers of this shard holding the subject (all but the subject itself)
-  if (n0 == N) {
-    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.pres, (size_t)N, P.nloc);
-    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P.pres + P.row0, (size_t)P.nloc,
-                       P.nloc - 1);
-  } else {  // unsharded
-    (void)hipMemsetAsync(P.pres, 0, (size_t)N * 4, s);
-    hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(n0, 256)), dim3(256), 0, s, P.pres, (size_t)n0, n0 - 1);
-  }
+  // presence is per shard: observers of this shard holding the subject (all but the subject itself).
+  // The started members of this shard's rows are [row0, min(n0, row0 + nloc)); a subject of them is
+  // held by all but itself, any other started subject by all of them, a spare slot by none
+  const uint32_t ls = n0 > P.row0 ? std::min(n0, P.row0 + P.nloc) - P.row0 : 0u;  // started local rows
+  (void)hipMemsetAsync(P.pres, 0, (size_t)N * 4, s);
+  hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(n0, 256)), dim3(256), 0, s, P.pres, (size_t)n0, ls);
+  if (ls) hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(ls, 256)), dim3(256), 0, s, P.pres + P.row0, (size_t)ls, ls - 1);
   hipLaunchKernelGGL(k_fill_u32, dim3(blocks_for(N, 256)), dim3(256), 0, s, P.sync_fd, (size_t)N, NONE);
   (void)hipMemsetAsync(P.cnt_delta, 0, (size_t)N * 4, s);
   (void)hipMemsetAsync(P.alive, 1, n0, s);
@@ -1431,7 +1431,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
   hipLaunchKernelGGL(k_fill_u32, dim3(64), dim3(256), 0, s, reinterpret_cast<uint32_t*>(P.actpos), (size_t)h->GC / 16,
                      NONE);
   {  // every started member of this shard starts with others = n0 - 1; n0 members alive
-    const uint32_t all = n0 == N ? P.nloc : n0, alive = n0 == N ? P.nloc : n0;  // of this shard
+    const uint32_t all = ls, alive = ls;  // of this shard
     (void)hipMemcpyAsync(&P.ctl->bl_hist[bitlen(n0)], &all, 4, hipMemcpyHostToDevice, s);
     (void)hipMemcpyAsync(&P.ctl->alive_count, &alive, 4, hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
@@ -1672,7 +1672,9 @@ int start_member(swim_handle* h, uint32_t x, uint32_t a) {
 }
 
 int join_checks(swim_handle* h, uint32_t n) {
-  if (h->sharded || h->base.nxk) return fail(h, SWIM_EINVAL, "join / restart: dense, unsharded handles only");
+  // (N x K views hold BASELINE for every untracked subject in every row: a joiner's table, which knows
+  // only itself, is not one. Sharded handles: every rank makes the same call)
+  if (h->base.nxk) return fail(h, SWIM_EINVAL, "join / restart: dense handles only");
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "join / restart: a period is in flight");
   const uint64_t seeds = std::min<uint64_t>(h->cfg.n_seeds, h->N);
   if ((uint64_t)(h->base.njoin + n) * std::max<uint64_t>(1, seeds) > h->scap)

@@ -98,6 +98,10 @@ enum IfromOverflow : uint32_t {
 // :163-169); here it is re-emitted by the forwarding member under FOREIGN_SEQ | fseq[member]
 constexpr uint32_t FOREIGN_SEQ = 0x80000000u;
 
+// the request word of a SYNC exchange record that carries a joiner's initial SYNC (MembershipProtocolImpl
+// .start0, :222-257) to a seed on another shard: JOIN_REQ | joiner (periodic / FD requests are 2i + kind)
+constexpr uint32_t JOIN_REQ = 0x40000000u;
+
 constexpr uint32_t BASELINE = 1u;  // SWIM_PACK(0, SWIM_ALIVE): every view's record at the start
 
 constexpr uint32_t STAT_SHARDS = 64;  // power of two
@@ -146,6 +150,8 @@ struct Ctl {
   uint32_t wbeg_hist[256];  // w_beg of each round's active list (act_ring)
   uint32_t xg_cnt[SWIM_MAX_WORLD];  // this round's (sender, remote peer) pairs per peer shard
   uint32_t xs_cnt[SWIM_MAX_WORLD];  // this period's SYNC requests per remote receiver shard
+  uint32_t js_n;        // initial SYNCs of local joiners bound for other shards this period (jsend)
+  uint32_t xr_n;        // SYNC requests received from other shards this period (k_sync_unpack)
   uint32_t sp_n;        // spill-table slots claimed this round (sp_used): cleared by k_finalize, reset by k_gossip_prep
   uint32_t ntouched;    // dense SYNC rows: touched columns listed by k_tlist for this period's SYNC
   uint32_t rb_next;     // slot entry bitmaps handed out (mod rb_cap)
@@ -206,6 +212,10 @@ struct KP {
   uint8_t* joining;   // [N]
   uint32_t* jslot;    // [N] a joiner's SYNC staging slot (its table, one payload for every seed)
   uint32_t* jwin;     // [N] the seed member whose SYNC_ACK the joiner merges (first round trip), or NONE
+  // sharded joins: initial SYNCs whose seed lives on another shard travel in the SYNC exchange as
+  // records [JOIN_REQ | joiner, seed, joiner's table]; the seed's SYNC_ACK comes back in the same slot
+  uint2* jsend;       // [world * nloc] {joiner, seed} of this period's initial SYNCs bound for other shards
+  uint32_t* jack_ref; // [N] requester side: record index of the SYNC_ACK of a joiner's remote initial SYNC
   // state
   uint32_t* view;
   uint16_t* dl;  // [W cells][nloc observers] suspicion deadline (dl_enc; 0 = none), subject-major

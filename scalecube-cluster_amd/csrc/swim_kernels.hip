@@ -206,15 +206,20 @@ __global__ void k_iota_u32(uint32_t* p, uint32_t n, uint32_t n_id) {
 // swim_join / swim_restart: spare slot x starts at address a (ClusterImpl.start, ClusterImpl.java:
 // 170-227) with a table holding only itself ALIVE inc 0 (MembershipProtocolImpl.java:138-142) and
 // fresh protocol state; a restart on another member's address links x into that address's movers.
+// Sharded handles launch it on every shard: the row (table, deadlines, histories, marks) and the shard's
+// alive tallies only where it lives, liveness and addresses everywhere (they are replicated).
 __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
-  for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
-    P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
-    P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
-    if (P.meta_view) P.meta_view[lrow(P, x) * P.W + c] = 0u;
+  const bool mine = is_local(P, x);
+  if (mine) {
+    for (uint32_t c = threadIdx.x; c < P.W; c += blockDim.x) {
+      P.view[lrow(P, x) * P.W + c] = c == x ? BASELINE : SWIM_ABSENT;
+      P.dl[(size_t)c * P.nloc + lrow(P, x)] = 0u;
+      if (P.meta_view) P.meta_view[lrow(P, x) * P.W + c] = 0u;
+    }
+    for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) P.ih_rhead[lrow(P, x) * 256u + t] = 0u;
+    if (P.dmark)  // a fresh table: no merge marks
+      for (uint32_t t = threadIdx.x; t < P.dsids; t += blockDim.x) P.dmark[lrow(P, x) * P.dsids + t] = 0u;
   }
-  for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) P.ih_rhead[lrow(P, x) * 256u + t] = 0u;
-  if (P.dmark)  // a fresh table: no merge marks
-    for (uint32_t t = threadIdx.x; t < P.dsids; t += blockDim.x) P.dmark[lrow(P, x) * P.dsids + t] = 0u;
   if (threadIdx.x == 0) {
     P.cnt[x] = 0u;
     P.cnt_delta[x] = 0;
@@ -232,8 +237,10 @@ __global__ void k_join_one(KP P, uint32_t x, uint32_t a) {
     }
     P.addr[x] = a;
     P.occ[a] = x;
-    atomicAdd(&P.ctl->bl_hist[bitlen(1u)], 1u);
-    atomicAdd(&P.ctl->alive_count, 1u);
+    if (mine) {
+      atomicAdd(&P.ctl->bl_hist[bitlen(1u)], 1u);
+      atomicAdd(&P.ctl->alive_count, 1u);
+    }
   }
 }
 
@@ -3712,11 +3719,13 @@ __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
     if (!xrec_locate(P, P.ctl->xs_cnt, g, &dst, &i)) break;
     const uint32_t q = P.xs_pend[(size_t)dst * 2u * P.nloc + i];
     uint32_t* out = P.xsend + (size_t)g * sync_rec_words(P);  // a row of W cells (N x K: columns; tmode: touched)
+    // a joiner's initial SYNC (JOIN_REQ | jsend index): [JOIN_REQ | joiner, seed, table]
+    const uint2 js = (q & JOIN_REQ) ? P.jsend[q & ~JOIN_REQ] : make_uint2(q >> 1, 0u);
     if (threadIdx.x == 0) {
-      out[0] = q;
-      out[1] = P.req_to[q];
+      out[0] = (q & JOIN_REQ) ? (JOIN_REQ | js.x) : q;
+      out[1] = (q & JOIN_REQ) ? js.y : P.req_to[q];
     }
-    const uint32_t* row = P.view + lrow(P, q >> 1) * P.W;
+    const uint32_t* row = P.view + lrow(P, js.x) * P.W;
     if (tlisted(P))
       for (uint32_t c = threadIdx.x; c < P.ctl->ntouched; c += blockDim.x) out[2 + c] = row[P.tlist[c]];
     else
@@ -3728,9 +3737,10 @@ __global__ void __launch_bounds__(256) k_sync_pack(KP P, uint32_t n_rec) {
 __global__ void k_sync_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) P.ctl->xr_n = n_rec;
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
-    P.rs_ref[rec[0]] = g;
+    if (!(rec[0] & JOIN_REQ)) P.rs_ref[rec[0]] = g;  // (a joiner's record is found by its seed's merge)
     recv_one(P, rec[1]);
   }
 }
@@ -3741,7 +3751,8 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
   if (g < n_rec) {
     const uint32_t* rec = P.xrecv + (size_t)g * sync_rec_words(P);
     const uint32_t to = rec[1];
-    P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = 4u * (rec[0] >> 1) + (rec[0] & 1u);
+    const uint32_t e = (rec[0] & JOIN_REQ) ? 4u * (rec[0] & ~JOIN_REQ) + 2u : 4u * (rec[0] >> 1) + (rec[0] & 1u);
+    P.bucket[P.recv_off[to] + atomicAdd(&P.recv_fill[to], 1u)] = e;
   }
 }
 
@@ -3749,7 +3760,14 @@ __global__ void k_sync_scatter_remote(KP P, uint32_t n_rec) {
 __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
   SWIM_GUARD(P);
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n_rec) P.ack_ref[P.xrecv[(size_t)g * sync_rec_words(P)]] = g;
+  if (g < n_rec) {
+    const uint32_t q = P.xrecv[(size_t)g * sync_rec_words(P)];
+    if (q == NONE) return;  // a joiner's initial SYNC whose seed is not the one it takes the SYNC_ACK of
+    if (q & JOIN_REQ)
+      P.jack_ref[q & ~JOIN_REQ] = g;
+    else
+      P.ack_ref[q] = g;
+  }
 }
 
 // Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
@@ -3808,6 +3826,7 @@ __global__ void __launch_bounds__(1024) k_due(KP P) {
   const uint32_t nc = ncells(P);
   if (threadIdx.x == 0) {  // this period's SYNC counters (k_sync_select on), in place of host memsets
     P.ctl->stage_count = 0u;
+    P.ctl->js_n = 0u;
   }
   if (threadIdx.x < SWIM_MAX_WORLD) P.ctl->xs_cnt[threadIdx.x] = 0u;
   if (threadIdx.x < SY_STRIPES) {
@@ -4088,20 +4107,40 @@ __global__ void k_sync_select(KP P) {
 // seed address but the own one, all carrying the joiner's table (one staging slot); the joiner will
 // merge only the first SYNC_ACK to come back (take(1), :244-247), canonically the lowest seed address
 // whose round trip is delivered (jwin). Thread per member; launched only when some member joins.
+// Sharded handles: every shard works out every joiner's jwin (the seeds' shards need it: only jwin's merge
+// keeps a SYNC_ACK); the joiner's own shard stages its table for the seeds on that shard and sends it
+// to each seed on another shard in the SYNC exchange (jsend, k_sync_pack), whose SYNC_ACK comes back
+// in the same record.
 __global__ void k_join_select(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t sent = 0, dlv = 0;
   if (i < P.N && P.joining[i] && P.alive[i]) {
+    const bool mine = is_local(P, i);
     P.jwin[i] = NONE;
     P.jslot[i] = NONE;
     const uint32_t nseeds = P.n_seeds < P.N ? P.n_seeds : P.N, own = addr_of(P, i);
     uint32_t slot = NONE;
     for (uint32_t s = 0; s < nseeds; ++s) {
       if (s == own) continue;
-      ++sent;
+      sent += mine ? 1u : 0u;
       if (!delivered(P, K_SYNC, i, s, 2u, P.tick)) continue;
-      ++dlv;
+      dlv += mine ? 1u : 0u;
+      const uint32_t rcv = route(P, s);
+      if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
+      if (!mine) continue;
+      if (!is_local(P, rcv)) {  // the table travels to the seed's shard
+        const uint32_t dst = rcv / P.nloc;
+        const uint32_t js = atomicAdd(&P.ctl->js_n, 1u);
+        const uint32_t o = atomicAdd(&P.ctl->xs_cnt[dst], 1u);
+        if (js >= P.N || o >= 2u * P.nloc) {
+          atomicOr(&P.ctl->overflow, OV_SYNC);
+          break;
+        }
+        P.jsend[js] = make_uint2(i, rcv);
+        P.xs_pend[(size_t)dst * 2u * P.nloc + o] = JOIN_REQ | js;
+        continue;
+      }
       if (slot == NONE) {
         slot = atomicAdd(&P.ctl->stage_count, 1u);
         if (slot >= P.scap) {
@@ -4111,15 +4150,13 @@ __global__ void k_join_select(KP P) {
         P.stage_req[slot] = 2 * i;
         P.jslot[i] = slot;
       }
-      const uint32_t rcv = route(P, s);
       recv_one(P, rcv);
-      if (P.jwin[i] == NONE && delivered(P, K_SYNC_ACK, rcv, i, 2u, P.tick + 1u)) P.jwin[i] = rcv;
     }
   }
   // a joiner whose initial SYNC_ACK comes back is k_sync_ack's work too (k_sync_ack's own test; once:
   // not when k_sync_select listed it for a request of its own)
-  if (i >= P.row0 && i < P.row0 + P.nloc && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap &&
-      P.req_stage[2 * i] == NONE && P.req_stage[2 * i + 1] == NONE)
+  if (i >= P.row0 && i < P.row0 + P.nloc && P.joining[i] && P.jwin[i] != NONE &&
+      (P.jslot[i] < P.scap || !is_local(P, P.jwin[i])) && P.req_stage[2 * i] == NONE && P.req_stage[2 * i + 1] == NONE)
     sy_push(P.ctl->sy_acnt, P.sy_alist, P.sy_cap, i - P.row0, i);
   add_stat(P, ST_SYNCS_SENT, sent);
   add_stat(P, ST_SYNCS_DELIVERED, dlv);
@@ -4130,11 +4167,12 @@ __global__ void k_join_select(KP P) {
 __global__ void k_join_scatter(KP P) {
   SWIM_GUARD(P);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < P.N && P.joining[i] && P.alive[i] && P.jslot[i] != NONE && P.jslot[i] < P.scap) {
+  if (i < P.N && P.joining[i] && P.alive[i] && is_local(P, i) && P.jslot[i] != NONE && P.jslot[i] < P.scap) {
     const uint32_t nseeds = P.n_seeds < P.N ? P.n_seeds : P.N, own = addr_of(P, i);
     for (uint32_t s = 0; s < nseeds; ++s) {
       if (s == own || !delivered(P, K_SYNC, i, s, 2u, P.tick)) continue;
       const uint32_t rcv = route(P, s);
+      if (!is_local(P, rcv)) continue;  // (k_sync_scatter_remote on the seed's shard)
       P.bucket[P.recv_off[rcv] + atomicAdd(&P.recv_fill[rcv], 1u)] = 4u * i + 2u;
     }
   }
@@ -4416,9 +4454,30 @@ __device__ __forceinline__ void sync_merge_one(const KP& P, uint32_t j, uint32_t
     const uint32_t* src;
     uint32_t* ack;
     if (kind == 2u) {  // a joiner's initial SYNC; only the seed it will take the SYNC_ACK of keeps one
-      const uint32_t slot = P.jslot[from];
-      src = P.stage_sync + (size_t)slot * P.W;
-      ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
+      if (is_local(P, from)) {
+        const uint32_t slot = P.jslot[from];
+        src = P.stage_sync + (size_t)slot * P.W;
+        ack = P.jwin[from] == j ? P.stage_ack + (size_t)slot * P.W : nullptr;
+      } else {  // from another shard: its record [JOIN_REQ | from, j, table] among this period's received ones
+        __shared__ uint32_t s_jg;
+        const size_t rw = sync_rec_words(P);
+        if (threadIdx.x == 0) s_jg = NONE;
+        __syncthreads();
+        for (uint32_t g = threadIdx.x; g < P.ctl->xr_n; g += blockDim.x)
+          if (P.xrecv[(size_t)g * rw] == (JOIN_REQ | from) && P.xrecv[(size_t)g * rw + 1] == j) s_jg = g;
+        __syncthreads();
+        const uint32_t g = s_jg;
+        if (g == NONE) {  // (invariant: k_sync_scatter_remote listed it from that record)
+          if (threadIdx.x == 0) atomicOr(&P.ctl->overflow, OV_BUG);
+          continue;
+        }
+        src = P.xrecv + (size_t)g * rw + 2;
+        ack = P.jwin[from] == j ? P.xsend + (size_t)g * rw + 2 : nullptr;
+        if (threadIdx.x == 0) {  // the record goes back to the joiner's shard in the SYNC_ACK exchange
+          P.xsend[(size_t)g * rw] = P.jwin[from] == j ? (JOIN_REQ | from) : NONE;
+          P.xsend[(size_t)g * rw + 1] = j;
+        }
+      }
       merge_row(P, j, src, ack, 0x80000000u | from, SWIM_R_SYNC, snap, seq, T, created, s_lds4);
       continue;
     }
@@ -4464,7 +4523,7 @@ __device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* 
     to[n] = t;
     ++n;
   }
-  if (P.njoin && P.joining[i] && P.jwin[i] != NONE && P.jslot[i] < P.scap) {  // checked in k_join_select
+  if (P.njoin && P.joining[i] && P.jwin[i] != NONE && (P.jslot[i] < P.scap || !is_local(P, P.jwin[i]))) {  // as k_join_select
     kd[n] = 2u;
     to[n] = P.jwin[i];
     ++n;
@@ -4487,7 +4546,8 @@ __device__ __forceinline__ void sync_ack_one(const KP& P, uint32_t i, uint32_t* 
     const uint32_t* src;
     uint32_t attempt, reason = SWIM_R_SYNC;
     if (kd[k] == 2u) {  // syncMembership(onStart = true): reason INITIAL_SYNC (MPI:463-473)
-      src = P.stage_ack + (size_t)P.jslot[i] * P.W;
+      src = is_local(P, to[k]) ? P.stage_ack + (size_t)P.jslot[i] * P.W
+                               : P.xrecv + (size_t)P.jack_ref[i] * sync_rec_words(P) + 2;  // (the seed's shard)
       attempt = 0x80000000u | to[k];
       reason = SWIM_R_INITIAL_SYNC;
     } else {

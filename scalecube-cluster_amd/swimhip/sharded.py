@@ -243,6 +243,18 @@ class ShardedSwimCluster(SwimCluster):
         self._same_args("crash", ids)
         super().crash(ids)
 
+    def join(self, ids):
+        """Joins on a sharded handle: every rank makes the same call; the joiner's row
+        lives on its shard, its initial SYNCs to seeds on other shards travel in the SYNC exchange."""
+        ids = list(ids)
+        self._same_args("join", ids)
+        super().join(ids)
+
+    def restart(self, old_ids, new_ids):
+        old_ids, new_ids = list(old_ids), list(new_ids)
+        self._same_args("restart", old_ids + new_ids)
+        super().restart(old_ids, new_ids)
+
     def update_metadata(self, ids):
         ids = list(ids)
         self._same_args("update_metadata", ids)

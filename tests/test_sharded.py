@@ -133,6 +133,20 @@ def test_shard_lifecycle_and_delays_match_unsharded(world, names):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,names", [(2, ["local40_restart_join"]),
+                                         (4, ["local40_restart_join", "lan288_restart_join_loss5"])])
+def test_shard_joins_and_restarts_match_unsharded(world, names):
+    """Joins and restarts on sharded handles (round 6): spare slots on every shard, the
+    joiner's row on its own shard, liveness and addresses replicated; an initial SYNC to a seed on
+    another shard travels in the SYNC exchange as [JOIN_REQ | joiner, seed, table] and the seed it
+    takes the SYNC_ACK of answers in the same record (MembershipProtocolImpl.start0, :222-257); a
+    restarted member takes an address whose old id's pings answer DEST_GONE (FailureDetectorImpl.java:
+    231-235). Crashes, restarts on the same addresses and joins through the seeds, with 5 % loss on the
+    LAN one, bit-exact with the unsharded handle every period."""
+    mp.spawn(_parity_worker, args=(world, _free_port(), names), nprocs=world, join=True)
+
+
+@pytest.mark.gpu
 def test_host_driven_exchanges_match_unsharded():
     """The host-driven protocol (swim_shard_step: the host performs each exchange the library
     describes, as a Java host with its own collectives would) against the unsharded handle; every
