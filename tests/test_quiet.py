@@ -33,14 +33,30 @@ def _make(flag):
     return make
 
 
+def _solo(name, make):
+    cfg, n, seed, script, kw = scenarios.scenario(name)
+    c = make(cfg, n, seed, event_capacity=1 << 20, **kw)
+    for _ in script(c):
+        pass
+    return c.stats()
+
+
 @pytest.mark.parametrize("name", ["c1_local32_crash", "lan256_loss5_crash3", "local128_partition_heal",
                                   "local40_restart_join", "local64_update_metadata", "local64_user_gossips_loss10",
                                   "local32_leave2"])
 def test_quiet_skip_matches_full_rounds(name):
+    """Every parity counter, event, digest and table equal period by period (run_pair). The kernels' own
+    work counters are compared too, except those that differ between two runs of the always-running
+    handle itself (their counts depend on the order of atomics: merge-mark skips, spill claims, sender
+    chunks), which a third run finds."""
     a, b = scenarios.run_pair(name, _make("1"), _make("0"))
     sa, sb = a.stats(), b.stats()
-    assert {k: sa[k] for k in KEYS} == {k: sb[k] for k in KEYS}
-    assert sb["quiet_periods"] == 0
+    sc = _solo(name, _make("0"))
+    nondet = {k for k in KEYS if sb[k] != sc[k]}
+    assert not nondet & set(scenarios.PARITY_KEYS)
+    assert {k: sa[k] for k in KEYS if k not in nondet} == {k: sb[k] for k in KEYS if k not in nondet}, sorted(nondet)
+    print(name, "run-to-run work counters:", sorted(nondet), "quiet periods:", sa["quiet_periods"])
+    assert sb["quiet_periods"] == 0 and sc["quiet_periods"] == 0
 
 
 @pytest.mark.parametrize("tracked", [0, 256])
@@ -70,7 +86,9 @@ def test_quiet_stretches_around_a_storm(tracked):
             busy_seen += 1
         elif busy_seen:
             quiet_after += 1
-        assert {k: sa[k] for k in KEYS} == {k: sb[k] for k in KEYS}, f"period {t}"
+        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}, f"period {t}"
+        for k in ("gossip_scanned", "gossip_window_words", "gossips_created", "sweep_cells", "merge_cells"):
+            assert sa[k] == sb[k], (t, k)  # a skipped round that was not empty would list or send something
         assert a.digest() == b.digest(), f"period {t}"
         assert [e.key() for e in a.events()] == [e.key() for e in b.events()], f"period {t}"
     assert busy_seen > 10 and quiet_after > 0 and sb["quiet_periods"] == 0
