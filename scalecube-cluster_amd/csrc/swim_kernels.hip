@@ -1626,6 +1626,9 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 // entries flattened across the wave, more waves in flight beat more loads per wave (C3 select 63.9
 // -> 55.3 ms per 20 periods, C4's schedule 94.9 -> 87.9)
 #define SWIM_SEL_BATCH 1
+#ifndef SWIM_SEL_PF
+#define SWIM_SEL_PF 0
+#endif
 #define SWIM_SEL_WAVES 6
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
@@ -1726,12 +1729,24 @@ __device__ __forceinline__ void select_body(const KP& P) {
     // load each, all issued together (bytes in flight). Words whose class the member's own age
     // bounds settle are finished in a fully unrolled pass (no dynamically indexed register
     // arrays, so nothing goes to scratch); the few left MIXED are finished one by one from a mask.
+#if SWIM_SEL_PF
+    // the next step's list quad is loaded while this step's holdings are classified (the list is the
+    // same for every member: only the holdings load depends on it)
+    static_assert(SEL_BATCH == 1u, "SWIM_SEL_PF: one list quad per lane per step");
+    uint4 a_pf = 4u * lane < n_act ? *reinterpret_cast<const uint4*>(P.act + 4u * lane) : make_uint4(0u, 0u, 0u, 0u);
+#endif
     for (uint32_t k0 = 0; k0 < n_act; k0 += 256u * SEL_BATCH) {
       uint32_t ev[4 * SEL_BATCH], wv[4 * SEL_BATCH];
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
         const uint32_t kq = k0 + 256u * j + 4u * lane;
+#if SWIM_SEL_PF
+        const uint4 a = a_pf;
+        const uint32_t kn = kq + 256u;
+        a_pf = kn < n_act ? *reinterpret_cast<const uint4*>(P.act + kn) : make_uint4(0u, 0u, 0u, 0u);
+#else
         const uint4 a = kq < n_act ? *reinterpret_cast<const uint4*>(P.act + kq) : make_uint4(0u, 0u, 0u, 0u);
+#endif
         ev[4 * j] = a.x;
         ev[4 * j + 1] = a.y;
         ev[4 * j + 2] = a.z;
@@ -3081,6 +3096,12 @@ constexpr uint32_t AW_DIRECT = SWIM_AW_DIRECT;
 // blocks to merge together (fewer dependent rounds of loads per receiver than one group at a time)
 #define SWIM_AW_MC 1
 constexpr uint32_t AW_MC = SWIM_AW_MC;
+// bitmap words whose merge marks and block generations one step of the merge pass loads together
+#ifndef SWIM_AW_MW
+#define SWIM_AW_MW 2
+#endif
+constexpr uint32_t AW_MW = SWIM_AW_MW;
+static_assert(AW_MW == 1u || AW_MW == 2u || AW_MW == 4u || AW_MW == 8u, "SWIM_AW_MW: 1, 2, 4 or 8 words per step");
 static_assert(AW_MC >= 1u && AW_MC <= 4u, "SWIM_AW_MC: 1..4 groups of 512 bitmap words");
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
@@ -3407,19 +3428,19 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
       for (uint32_t ci = 0; ci < AW_MC; ++ci) {
       bm[ci] = 0u;
 #pragma unroll
-      for (uint32_t h2 = 0; h2 < 4u; ++h2) {  // (two words in flight per step: registers)
-        uint32_t wv[2];
-        uint4 mv[2], gv[2];
+      for (uint32_t h2 = 0; h2 < 8u / AW_MW; ++h2) {  // (AW_MW words in flight per step: registers)
+        uint32_t wv[AW_MW];
+        uint4 mv[AW_MW], gv[AW_MW];
 #pragma unroll
-        for (uint32_t uu = 0; uu < 2u; ++uu) {
-          const uint32_t t = t0 + 512u * ci + 64u * (2u * h2 + uu) + lane;
+        for (uint32_t uu = 0; uu < AW_MW; ++uu) {
+          const uint32_t t = t0 + 512u * ci + 64u * (AW_MW * h2 + uu) + lane;
           wv[uu] = t < bw ? s_bm[t] : 0u;
           mv[uu] = wv[uu] ? mrow4[t] : make_uint4(0u, 0u, 0u, 0u);
           gv[uu] = wv[uu] ? gen4[t] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
-        for (uint32_t uu = 0; uu < 2u; ++uu) {
-          const uint32_t u = 2u * h2 + uu;
+        for (uint32_t uu = 0; uu < AW_MW; ++uu) {
+          const uint32_t u = AW_MW * h2 + uu;
           if (wv[uu]) nzw |= 1u << (8u * ci + u);
           const uint32_t mk[4] = {mv[uu].x, mv[uu].y, mv[uu].z, mv[uu].w};
           const uint32_t gg[4] = {gv[uu].x, gv[uu].y, gv[uu].z, gv[uu].w};

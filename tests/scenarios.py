@@ -266,6 +266,13 @@ SCENARIOS_EXTRA = {
     # C5's shape (BASELINE configs[4]: N x K views, concurrent crashes, LAN, no loss: gossip batches)
     # at 4,096 members with 64 crashes, past the first suspicion timeouts (65 periods at b = 13)
     "nxk4096_c5_shape": (ClusterConfig.defaultLanConfig(), 4096, 19, lambda c: _lan_loss(c, 64, 70, 0.0, t0=3)),
+    # rings that are not powers of two (ids mod GC, C4's 5,128 x 1,024 slots; tools/probe_ring.py sized
+    # them): 20 % loss over 120 periods issues ~14,000 one-gossip slots into 3,072 (the ring wraps ~4
+    # times at ~560 live); C2-like loss at 1,024 members keeps ~15,100 of 17,408 slots live at its peak
+    "local100_loss20_ring3k": (ClusterConfig.defaultLocalConfig(), 100, 3, lambda c: _lan_loss(c, 2, 120, 20.0),
+                               {"gossip_capacity": 3 * 1024}),
+    "lan1024_loss5_ring17k": (ClusterConfig.defaultLanConfig(), 1024, 7, lambda c: _lan_loss(c, 10, 30, 5.0),
+                              {"gossip_capacity": 17 * 1024}),
 }
 
 

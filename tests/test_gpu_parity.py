@@ -22,6 +22,20 @@ def test_scenario_parity(name):
 # ring slot per gossip and the LDS-hash apply (gossip_batching off) must match the oracle too
 
 
+@pytest.mark.parametrize("name,wraps", [("local100_loss20_ring3k", 4), ("lan1024_loss5_ring17k", 1)])
+def test_non_power_of_two_ring_matches_oracle(name, wraps):
+    """Rings of any multiple of 1,024 slots (C4's shards use 5,128 x 1,024): gossip ids map to
+    slots and bitmap words mod GC (gmod / wmod) once the ring is not a power of two. Scenarios that issue
+    several rings' worth of one-gossip slots (20 % loss over 120 periods into 3,072 slots), or keep the
+    ring nearly full (C2-like loss at 1,024 members in 17,408 slots): bit-exact with the oracle every
+    period, no overflow."""
+    a, b = scenarios.run_pair(name, SwimCluster, OracleCluster)
+    s = a.stats()
+    gcap = scenarios.scenario(name)[4]["gossip_capacity"]
+    assert gcap & (gcap - 1) and s["overflow"] == 0
+    assert s["gossips_created"] > wraps * gcap, s["gossips_created"]
+
+
 @pytest.mark.parametrize("name", list(scenarios.SCENARIOS))
 def test_scenario_parity_unbatched(name):
     """Handles without the record dictionary (gossip_batching off): one gossip per ring slot and the

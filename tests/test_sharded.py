@@ -147,6 +147,13 @@ def test_shard_joins_and_restarts_match_unsharded(world, names):
 
 
 @pytest.mark.gpu
+def test_non_power_of_two_ring_shards_match_unsharded():
+    """A 3,072-slot ring (not a power of two: ids mod GC) wrapping ~4 times, over 2 shards: every commit
+    exchange assigns the same ids on both, bit-exact with the unsharded handle every period."""
+    mp.spawn(_parity_worker, args=(2, _free_port(), ["local100_loss20_ring3k"]), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
 def test_host_driven_exchanges_match_unsharded():
     """The host-driven protocol (swim_shard_step: the host performs each exchange the library
     describes, as a Java host with its own collectives would) against the unsharded handle; every
