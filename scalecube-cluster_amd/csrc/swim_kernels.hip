@@ -3086,11 +3086,6 @@ constexpr uint32_t AW_WAVES = 4;                  // receivers in flight per wor
 #define SWIM_AW_VILP32 4
 #define SWIM_AW_QILP 2
 constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flight per lane (short ranges)
-// short ranges of at most this many 16-B id groups are walked by their own lane (no owner search)
-#ifndef SWIM_AW_DIRECT
-#define SWIM_AW_DIRECT 2
-#endif
-constexpr uint32_t AW_DIRECT = SWIM_AW_DIRECT;
 #define SWIM_AW_LONG 256
 // the merge pass tests AW_MC groups of 512 bitmap words (their merge marks) before it flattens their
 // blocks to merge together (fewer dependent rounds of loads per receiver than one group at a time)
@@ -3330,27 +3325,14 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
           }
         }
         APPLYB_SUB(t_big);
-        // short ranges (single gossips, small batches). A range of at most AW_DIRECT aligned 16-B groups
-        // of entry ids (most run tops: ~7 records on average in C3's storm) is walked by its own lane,
-        // its groups' loads issued together; longer ones have their groups flattened across the lanes,
-        // one group per lane per load (one owner search per group)
+        // short ranges (single gossips, small batches): their aligned 16-B groups of entry ids
+        // flattened across the lanes, one group per lane per load (one owner search per group). (Walking
+        // ranges of at most one / two / three groups by their own lane instead, without the owner
+        // search, measured slower: C3 apply 6.41 -> 6.47 / 6.60 / 6.98 ms per period, §6.6: the lanes'
+        // ranges are uneven.)
         {
           const bool sh = len != 0u && len < AW_LONG;
-          const uint32_t nq0 = sh ? ((cr.x & (IDG - 1u)) + len + IDG - 1u) / IDG : 0u;
-          if (__any(nq0 != 0u && nq0 <= AW_DIRECT)) {
-            const bool direct = nq0 != 0u && nq0 <= AW_DIRECT;
-            const uint32_t qb0 = cr.x & ~(IDG - 1u);
-            uint4 v[AW_DIRECT];
-#pragma unroll
-            for (uint32_t u = 0; u < AW_DIRECT; ++u)
-              v[u] = direct && u < nq0 ? id_load(qb0 + IDG * u) : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-            for (uint32_t u = 0; u < AW_DIRECT; ++u)
-#pragma unroll
-              for (uint32_t k = 0; k < IDG; ++k)
-                if (direct && (qb0 + IDG * u + k - cr.x) < len) record(qb0 + IDG * u + k, id_at(v[u], k));
-          }
-          const uint32_t nq = nq0 > AW_DIRECT ? nq0 : 0u;
+          const uint32_t nq = sh ? ((cr.x & (IDG - 1u)) + len + IDG - 1u) / IDG : 0u;
           uint32_t qtot;
           const uint32_t qoff = wave_excl_scan(nq, &qtot);
           for (uint32_t e0 = 0; e0 < qtot; e0 += 64u * AW_QILP) {
