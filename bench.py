@@ -35,10 +35,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # the metric is quoted on that fits one GPU: a 10 % simultaneous crash plus a 2-way partition from
 # t0 to t0+40 periods (< the 85-period suspicion timeout, so it heals by refutation and SYNC), LAN
 # defaults, no loss; t0 = the end of the warmup. The partition cuts a 16-member group (ids that are
-# multiples of N/16) from the rest. A half/half cut is not simulable under the reference's rules at
-# this N by any implementation: on heal every SYNC/SYNC_ACK re-spreads each accepted SUSPECT record
-# as a new gossip (MembershipProtocolImpl.java:649-656), ~0.47 N^2 gossips (oracle: 25.7k / 112k /
-# 491k at N = 256 / 512 / 1,024), i.e. ~2e9 gossips held by 65,536 members each.
+# multiples of N/16) from the rest. SURVEY §8(d)'s half/half cut by id parity is the workload
+# c3half65k: on heal every SYNC/SYNC_ACK re-spreads each accepted SUSPECT record as a new gossip
+# (MembershipProtocolImpl.java:649-656), ~0.47 N^2 gossips over the heal (oracle: 25.7k / 112k / 491k at
+# N = 256 / 512 / 1,024); it runs on one MI355X at 236 ms per period of the driver's window (180.6 GiB,
+# 1.1e7 gossips live at its end), 17x the 16-member cut's period.
 WORKLOADS = {
     "c3": dict(desc="C3: 65,536 members, dense N x N views, LAN defaults, 10% simultaneous crash + 2-way "
                     "partition (16-member group) for 40 periods healed via SYNC",
