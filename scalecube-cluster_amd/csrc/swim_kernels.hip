@@ -2417,6 +2417,10 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
 #define SWIM_PULL_SILP 2
 constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
+#ifndef SWIM_PULL_FLAT
+#define SWIM_PULL_FLAT 0
+#endif
+constexpr bool PULL_FLAT = SWIM_PULL_FLAT != 0;  // the lossy instance's draws flattened across the wave
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2438,6 +2442,8 @@ __device__ __forceinline__ void pull_body(const KP& P) {
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
   __shared__ uint32_t s_rcpt[4 / SPLIT];  // SPLIT > 1: the receiver's receipts over its waves
+  constexpr bool FLAT = LOSS && !DQ && PULL_FLAT;
+  __shared__ uint32_t s_u[FLAT ? 4 : 1][FLAT ? 256 : 1];  // FLAT: the delivered bits of a sender's pass, by (lane, word)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t part = (threadIdx.x >> 6) % SPLIT;  // this wave's share of the receiver's list quads
   const uint32_t p = P.row0 + blockIdx.x * (4u / SPLIT) + (threadIdx.x >> 6) / SPLIT;
@@ -2659,6 +2665,120 @@ __device__ __forceinline__ void pull_body(const KP& P) {
           }
         if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
       };
+      // FLAT (the lossy instance): the loss draws of a sender's messages flattened across the wave, one
+      // (word, gossip) per lane per step, instead of each lane drawing its own quad's candidates in a loop
+      // (the wave waited for the lane with the most). Every lane takes part in every step (wave-uniform
+      // loops; a lane without a quad to visit contributes no draws); a sender's delivered bits meet in LDS
+      // (s_u) and return to the quads' lanes before the next sender, whose candidates exclude them, as in
+      // deliver (the same draws: NetworkEmulator.evaluateLoss per message, one per gossip until delivered).
+      auto deliver_flat = [&](uint32_t kq, const uint32_t (&wcv)[4], const uint32_t (&wsv)[4], const uint32_t (&live)[4],
+                              const uint32_t (&hw)[4], uint32_t todo, uint32_t anyall, uint32_t anymix, bool quad,
+                              uint32_t ws0) {
+        uint32_t* su = s_u[FLAT ? (threadIdx.x >> 6) : 0];
+        uint32_t u[4] = {0u, 0u, 0u, 0u}, prev[4] = {0u, 0u, 0u, 0u};
+        if (!first_chunk && todo) {
+          const uint4 p4 = *reinterpret_cast<const uint4*>(nbr + DBG_IDX(kq, W32 - 3u, "pull nbr4"));
+          prev[0] = p4.x;
+          prev[1] = p4.y;
+          prev[2] = p4.z;
+          prev[3] = p4.w;
+        }
+        for (uint32_t q0 = 0; q0 < cdeg; ++q0) {  // (wave-uniform)
+          const uint32_t en = snd[q0], sid = s_sid[threadIdx.x >> 6][q0];
+          const bool rch = ((reach >> q0) & 1ull) != 0ull;
+          uint4 wa = make_uint4(0u, 0u, 0u, 0u), wm = make_uint4(0u, 0u, 0u, 0u);
+          if (todo && (en & SPAIR)) {
+            wm = *reinterpret_cast<const uint4*>(P.pw + DBG_IDX((size_t)s_pwo[threadIdx.x >> 6][q0] + kq, P.pwcap - 3u, "pull pw"));
+          } else if (todo && !(en & XREC) && quad) {
+            if (anyall) wa = *reinterpret_cast<const uint4*>(P.hb + DBG_IDX(lrow(P, en) * W32 + ws0, (size_t)P.nloc * W32 - 3u, "pull hb4"));
+            if (anymix) wm = *reinterpret_cast<const uint4*>(P.wb + DBG_IDX(lrow(P, en) * W32 + DBG_IDX(kq, W32 - 3u, "pull wb4 kq"), (size_t)P.nloc * W32 - 3u, "pull wb4"));
+          }
+          const uint32_t waa[4] = {wa.x, wa.y, wa.z, wa.w}, wma[4] = {wm.x, wm.y, wm.z, wm.w};
+          uint32_t cm[4], cnt = 0u;
+#pragma unroll
+          for (uint32_t i = 0; i < 4u; ++i) {
+            uint32_t v = 0u;
+            if ((todo >> i) & 1u) {
+              if (en & XREC)
+                v = remote_window(P, en & ~XREC, kq + i);
+              else if (en & SPAIR)
+                v = wma[i];
+              else if (quad)
+                v = wcv[i] == WC_ALL ? waa[i] & live[i] : wma[i];
+              else
+                v = wcv[i] == WC_ALL ? P.hb[DBG_IDX(lrow(P, en) * W32 + wsv[i], (size_t)P.nloc * W32, "pull hb")] & live[i]
+                                     : P.wb[DBG_IDX(lrow(P, en) * W32 + DBG_IDX(kq + i, W32, "pull wb kq"), (size_t)P.nloc * W32, "pull wb")];
+            }
+            if (v) ++probes;
+            cm[i] = rch ? v & ~hw[i] & ~u[i] & ~prev[i] : 0u;
+            cnt += (uint32_t)__popc(cm[i]);
+          }
+          if (P.loss_mode == 1u) {
+            uint32_t tot;
+            const uint32_t off = wave_excl_scan(cnt, &tot);
+            if (tot) {  // (wave-uniform)
+#pragma unroll
+              for (uint32_t i = 0; i < 4u; ++i) su[4u * lane + i] = 0u;
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+              for (uint32_t e0 = 0; e0 < tot; e0 += 64u) {
+                const uint32_t q = e0 + lane;
+                const uint32_t o = wave_owner(off, q);  // (every lane shuffles)
+                const uint32_t c0 = __shfl(cm[0], (int)o, 64), c1 = __shfl(cm[1], (int)o, 64);
+                const uint32_t c2 = __shfl(cm[2], (int)o, 64), c3 = __shfl(cm[3], (int)o, 64);
+                const uint32_t w0 = __shfl(wsv[0], (int)o, 64), w1 = __shfl(wsv[1], (int)o, 64);
+                const uint32_t w2 = __shfl(wsv[2], (int)o, 64), w3 = __shfl(wsv[3], (int)o, 64);
+                const uint32_t oo = __shfl(off, (int)o, 64);
+                if (q < tot) {
+                  uint32_t k = q - oo, i = 0u, c = c0, ws = w0;
+                  const uint32_t n0 = (uint32_t)__popc(c0), n1 = (uint32_t)__popc(c1), n2 = (uint32_t)__popc(c2);
+                  if (k >= n0) {
+                    k -= n0, i = 1u, c = c1, ws = w1;
+                    if (k >= n1) {
+                      k -= n1, i = 2u, c = c2, ws = w2;
+                      if (k >= n2) k -= n2, i = 3u, c = c3, ws = w3;
+                    }
+                  }
+                  const uint32_t b = kth_set_bit(c, k);
+                  if (draw1(P.seed, K_GOSSIP, sid, p, P.g_hash[ws * 32u + b], P.tick) >= P.loss_thr)
+                    atomicOr(&su[4u * o + i], 1u << b);
+                }
+              }
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+              for (uint32_t i = 0; i < 4u; ++i) cm[i] = su[4u * lane + i];
+              __builtin_amdgcn_wave_barrier();  // (su is cleared by the next pass)
+            }
+          }
+#pragma unroll
+          for (uint32_t i = 0; i < 4u; ++i) u[i] |= cm[i];
+        }
+        uint32_t sbits = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i)
+          if (u[i]) {
+            nbr[DBG_IDX(kq + i, W32, "pull nbr")] = prev[i] | u[i];
+            receipts += (uint32_t)__popc(u[i]);
+            sbits |= 1u << ((kq + i) & 31u);
+          }
+        if (sbits && nsw <= P.nsumw) atomicOr(&sum[kq >> 5], sbits);
+      };
+      if constexpr (FLAT) {
+        for (uint32_t kq0 = 256u * part; kq0 < n_act; kq0 += 256u * SPLIT) {  // (wave-uniform)
+          const uint32_t kq = kq0 + 4u * lane;
+          uint32_t todo = 0u, anyall = 0u, anymix = 0u, ws0 = 0u;
+          uint32_t wcv[4] = {WC_NONE, WC_NONE, WC_NONE, WC_NONE}, wsv[4] = {0u, 0u, 0u, 0u};
+          uint32_t live[4] = {0u, 0u, 0u, 0u}, hw[4] = {0u, 0u, 0u, 0u};
+          bool quad = false;
+          if (kq < n_act) {
+            const uint32_t lw = lackr ? lackr[kq >> 5] : 0xFFFFFFFFu;
+            const uint4 a = *reinterpret_cast<const uint4*>(P.act + kq);
+            if ((lw >> (kq & 31u)) & 0xFu) classify(kq, a, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
+          }
+          if (__any(todo != 0u)) deliver_flat(kq, wcv, wsv, live, hw, todo, anyall, anymix, quad, ws0);
+        }
+      } else
       for (uint32_t kq = 4u * lane + 256u * part; kq < n_act; kq += 256u * SPLIT) {
         // the receiver's own select pass marked the sent words it lacks something in: skip the
         // rest without reading the holdings (most of them once a storm has spread; compacting the
@@ -2727,7 +2847,9 @@ __device__ __forceinline__ void pull_body(const KP& P) {
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
 // the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
 // per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
+#ifndef SWIM_PULL_LOSS_WAVES
 #define SWIM_PULL_LOSS_WAVES 6
+#endif
 __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) {
   pull_body<false, true>(P);
 }
