@@ -1626,9 +1626,6 @@ __device__ __forceinline__ void leave_swept(const KP& P, uint32_t m, uint32_t ws
 // entries flattened across the wave, more waves in flight beat more loads per wave (C3 select 63.9
 // -> 55.3 ms per 20 periods, C4's schedule 94.9 -> 87.9)
 #define SWIM_SEL_BATCH 1
-#ifndef SWIM_SEL_PF
-#define SWIM_SEL_PF 0
-#endif
 #define SWIM_SEL_WAVES 6
 constexpr uint32_t SEL_BATCH = SWIM_SEL_BATCH;  // list quads per lane per step in k_gossip_select
 
@@ -1729,24 +1726,12 @@ __device__ __forceinline__ void select_body(const KP& P) {
     // load each, all issued together (bytes in flight). Words whose class the member's own age
     // bounds settle are finished in a fully unrolled pass (no dynamically indexed register
     // arrays, so nothing goes to scratch); the few left MIXED are finished one by one from a mask.
-#if SWIM_SEL_PF
-    // the next step's list quad is loaded while this step's holdings are classified (the list is the
-    // same for every member: only the holdings load depends on it)
-    static_assert(SEL_BATCH == 1u, "SWIM_SEL_PF: one list quad per lane per step");
-    uint4 a_pf = 4u * lane < n_act ? *reinterpret_cast<const uint4*>(P.act + 4u * lane) : make_uint4(0u, 0u, 0u, 0u);
-#endif
     for (uint32_t k0 = 0; k0 < n_act; k0 += 256u * SEL_BATCH) {
       uint32_t ev[4 * SEL_BATCH], wv[4 * SEL_BATCH];
 #pragma unroll
       for (uint32_t j = 0; j < SEL_BATCH; ++j) {
         const uint32_t kq = k0 + 256u * j + 4u * lane;
-#if SWIM_SEL_PF
-        const uint4 a = a_pf;
-        const uint32_t kn = kq + 256u;
-        a_pf = kn < n_act ? *reinterpret_cast<const uint4*>(P.act + kn) : make_uint4(0u, 0u, 0u, 0u);
-#else
         const uint4 a = kq < n_act ? *reinterpret_cast<const uint4*>(P.act + kq) : make_uint4(0u, 0u, 0u, 0u);
-#endif
         ev[4 * j] = a.x;
         ev[4 * j + 1] = a.y;
         ev[4 * j + 2] = a.z;
@@ -2417,10 +2402,7 @@ __device__ __forceinline__ void dq_push(const KP& P, uint32_t p, uint32_t sender
 constexpr uint32_t PULL_LOSS_ILP = SWIM_PULL_LOSS_ILP;  // loss draws per step of a lane (id-hash loads in flight)
 #define SWIM_PULL_SILP 2
 constexpr uint32_t PULL_SILP = SWIM_PULL_SILP;  // senders whose window loads a lane issues together
-#ifndef SWIM_PULL_FLAT
-#define SWIM_PULL_FLAT 0
-#endif
-constexpr bool PULL_FLAT = SWIM_PULL_FLAT != 0;  // the lossy instance's draws flattened across the wave
+
 
 // DQ: message delays are or were on (dq ring); LOSS: the instance the host launches while a
 // probabilistic loss is set, whose draws keep several id-hash loads in flight (more registers: the
@@ -2442,7 +2424,10 @@ __device__ __forceinline__ void pull_body(const KP& P) {
   __shared__ uint32_t s_sid[4][64];  // ... and their member ids
   __shared__ uint32_t s_pwo[4][64];  // ... and, for pruned pairs, their window offset in pw
   __shared__ uint32_t s_rcpt[4 / SPLIT];  // SPLIT > 1: the receiver's receipts over its waves
-  constexpr bool FLAT = LOSS && !DQ && PULL_FLAT;
+  // the lossy instance with a wave per receiver (shards of more than 4,096 rows: C4's) draws flattened
+  // across the wave (deliver_flat): C4's schedule at 65,536 pull 7.85 -> 7.40 ms per period; the split
+  // instance of small shards keeps each lane's own draws (C2's pull 0.77 -> 0.83 flattened, §6.6)
+  constexpr bool FLAT = LOSS && !DQ && SPLIT == 1u;
   __shared__ uint32_t s_u[FLAT ? 4 : 1][FLAT ? 256 : 1];  // FLAT: the delivered bits of a sender's pass, by (lane, word)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t part = (threadIdx.x >> 6) % SPLIT;  // this wave's share of the receiver's list quads
@@ -2847,9 +2832,7 @@ __device__ __forceinline__ void pull_body(const KP& P) {
 __global__ void __launch_bounds__(256, SWIM_PULL_WAVES) k_gossip_pull(KP P) { pull_body<false, false>(P); }
 // the lossy instance at 6 waves per SIMD (80 VGPRs, spilling): C4's schedule pull 170.8 -> 155.4 ms
 // per 20 periods; the lossless one loses at any occupancy above its natural 4 (C3 58.2 -> 60.9)
-#ifndef SWIM_PULL_LOSS_WAVES
 #define SWIM_PULL_LOSS_WAVES 6
-#endif
 __global__ void __launch_bounds__(256, SWIM_PULL_LOSS_WAVES) k_gossip_pull_loss(KP P) {
   pull_body<false, true>(P);
 }
@@ -3213,12 +3196,9 @@ constexpr uint32_t AW_QILP = SWIM_AW_QILP;        // 16-B entry-id loads in flig
 // blocks to merge together (fewer dependent rounds of loads per receiver than one group at a time)
 #define SWIM_AW_MC 1
 constexpr uint32_t AW_MC = SWIM_AW_MC;
-// bitmap words whose merge marks and block generations one step of the merge pass loads together
-#ifndef SWIM_AW_MW
-#define SWIM_AW_MW 2
-#endif
-constexpr uint32_t AW_MW = SWIM_AW_MW;
-static_assert(AW_MW == 1u || AW_MW == 2u || AW_MW == 4u || AW_MW == 8u, "SWIM_AW_MW: 1, 2, 4 or 8 words per step");
+// bitmap words whose merge marks and block generations one step of the merge pass loads together (4
+// measured no faster: C3 13.74 / 13.74 against 13.69 / 13.81 ms per period, with 48 B of scratch, §6.6)
+constexpr uint32_t AW_MW = 2;
 static_assert(AW_MC >= 1u && AW_MC <= 4u, "SWIM_AW_MC: 1..4 groups of 512 bitmap words");
 // record ranges of at least AW_LONG records are walked one at a time by the whole wave; shorter ones
 // are flattened into one stream of 16-B quads across the wave
