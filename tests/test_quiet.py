@@ -1,9 +1,9 @@
 """Quiet periods: the library skips the gossip rounds of a period in which no member
 holds a gossip (k_quiet_check after the FD commit; one k_quiet_rounds launch instead of ~15 per round).
-A/B against handles created with SWIMHIP_QUIET=0, which always run their rounds: every counter (the
-work counters of the byte model included), event, digest, membership and deadline table equal, period
-by period, through quiet stretches, storms, joins and restarts, and the return to quiet. The oracle
-parity file runs with the skip on as well (it is the default)."""
+A/B against handles created with SWIMHIP_QUIET=0, which always run their rounds: every parity counter,
+event, digest, membership and deadline table equal, period by period, and the protocol-level work counters
+that are exact run to run, through quiet stretches, storms, joins and restarts, and the return to quiet.
+The oracle parity file runs with the skip on as well (it is the default)."""
 import os
 
 import numpy as np
@@ -11,12 +11,8 @@ import pytest
 
 import scenarios
 from swimhip import ClusterConfig, SwimCluster
-from swimhip import _native as nat
 
 pytestmark = pytest.mark.gpu
-
-# every counter except the skip's own count
-KEYS = [k for k in nat.STAT_FIELDS if k != "quiet_periods"]
 
 
 def _make(flag):
@@ -33,31 +29,25 @@ def _make(flag):
     return make
 
 
-def _solo(name, make):
-    cfg, n, seed, script, kw = scenarios.scenario(name)
-    c = make(cfg, n, seed, event_capacity=1 << 20, **kw)
-    for _ in script(c):
-        pass
-    return c.stats()
+# protocol-level counters beyond the parity keys: exact run to run. (The kernels' own work counters are
+# not: gossips with equal commit sort keys take ring slots in the order their stage entries were claimed
+# by atomics, slot order being unobservable, and run tops, record ranges, list words,
+# pull probes and merge-mark skips follow the slots; two runs of the same always-running handle differ in
+# them.)
+EXACT = list(scenarios.PARITY_KEYS) + ["sweep_cells", "merge_cells", "ack_cells"]
 
 
 @pytest.mark.parametrize("name", ["c1_local32_crash", "lan256_loss5_crash3", "local128_partition_heal",
                                   "local40_restart_join", "local64_update_metadata", "local64_user_gossips_loss10",
                                   "local32_leave2"])
 def test_quiet_skip_matches_full_rounds(name):
-    """Every parity counter, event, digest and table equal period by period (run_pair). The kernels' own
-    work counters are compared too, except those that differ between two runs of the always-running
-    handle itself, which a third run finds: gossips with equal commit sort keys take ring slots in the
-    order their stage entries were claimed by atomics (slot order is unobservable), and
-    run tops, record ranges, list words and merge-mark skips follow the slots."""
+    """Every parity counter, event, digest and table equal period by period (run_pair), and the exact
+    protocol-level counters at the end; the skip taken (fault-free periods before the faults)."""
     a, b = scenarios.run_pair(name, _make("1"), _make("0"))
     sa, sb = a.stats(), b.stats()
-    sc = _solo(name, _make("0"))
-    nondet = {k for k in KEYS if sb[k] != sc[k]}
-    assert not nondet & set(scenarios.PARITY_KEYS)
-    assert {k: sa[k] for k in KEYS if k not in nondet} == {k: sb[k] for k in KEYS if k not in nondet}, sorted(nondet)
-    print(name, "run-to-run work counters:", sorted(nondet), "quiet periods:", sa["quiet_periods"])
-    assert sb["quiet_periods"] == 0 and sc["quiet_periods"] == 0
+    assert {k: sa[k] for k in EXACT} == {k: sb[k] for k in EXACT}
+    assert sb["quiet_periods"] == 0
+    print(name, "quiet periods:", sa["quiet_periods"], "of", sa["period"])
 
 
 @pytest.mark.parametrize("tracked", [0, 256])
@@ -87,10 +77,7 @@ def test_quiet_stretches_around_a_storm(tracked):
             busy_seen += 1
         elif busy_seen:
             quiet_after += 1
-        assert {k: sa[k] for k in scenarios.PARITY_KEYS} == {k: sb[k] for k in scenarios.PARITY_KEYS}, f"period {t}"
-        for k in ("gossips_created", "gossip_sends", "sweep_cells", "merge_cells", "ack_cells"):
-            assert sa[k] == sb[k], (t, k)  # (the kernels' other work counters follow slot order, which ties
-            # of equal sort keys leave to the order of atomics: they differ run to run, see above)
+        assert {k: sa[k] for k in EXACT} == {k: sb[k] for k in EXACT}, f"period {t}"
         assert a.digest() == b.digest(), f"period {t}"
         assert [e.key() for e in a.events()] == [e.key() for e in b.events()], f"period {t}"
     assert busy_seen > 10 and quiet_after > 0 and sb["quiet_periods"] == 0
