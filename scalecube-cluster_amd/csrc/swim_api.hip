@@ -89,6 +89,9 @@ struct swim_handle {
   // skipped (one k_quiet_rounds instead of ~15 launches per round). The test runs after the FD commit,
   // every period while the last one was quiet and every QUIET_EVERY-th period otherwise (a host stop)
   bool quiet_skip = true;   // SWIMHIP_QUIET=0 at swim_create: always run the rounds (tests: A/B)
+  // gossips the host calls between periods may have staged (leave, spread, metadata updates, delivered
+  // records): with the FD phase's own (one per member) they bound the FD commit's batch
+  uint64_t host_staged = 0;
   bool last_quiet = false;
   uint64_t quiet_periods = 0;
   uint32_t* d_quiet = nullptr;
@@ -492,7 +495,14 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         // change is visible from the first gossip round on, as at the end of every other phase
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_FD_C;
-        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        {  // the phase's batch is bounded: at most two FD gossips per member (a SUSPECT, then a DEAD of a
+           // DEST_GONE ack, MPI:376-404) plus what the host calls since the last period staged. A bound
+           // within CS_FUSE tiles sorts a storm's batch in one k_rs_fused launch (or in k_commit's LDS
+           // sort) instead of the eleven-launch radix chain sized for the stage's capacity
+          const uint64_t fd_bound = std::min<uint64_t>(2ull * nloc + h->host_staged, NONE - 1u);
+          h->host_staged = 0;
+          if (commit_begin(h, P, x, &rc, (uint32_t)fd_bound)) return SWIM_OK;
+        }
         if (rc) return rc;
         break;
       case PC_FD_C: {
@@ -1654,6 +1664,7 @@ int swim_leave(swim_handle* h, const uint32_t* ids, uint32_t n) {
       track_commit(h, h->base);
     }
     hipLaunchKernelGGL(k_leave, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+    h->host_staged += 1;
   }
   h->n_leaving += n;
   HIPC(h, hipStreamSynchronize(h->stream));
@@ -1776,6 +1787,7 @@ int swim_update_metadata(swim_handle* h, const uint32_t* ids, uint32_t n) {
       track_commit(h, h->base);
     }
     hipLaunchKernelGGL(k_update_meta, dim3(1), dim3(64), 0, h->stream, h->base, ids[k]);
+    h->host_staged += 1;
   }
   HIPC(h, hipStreamSynchronize(h->stream));
   HIPC(h, hipGetLastError());
@@ -1786,6 +1798,7 @@ int swim_spread(swim_handle* h, uint32_t origin, uint32_t tag) {
   if (!h || origin >= h->N) return SWIM_EINVAL;
   if (h->pc != PC_FD) return fail(h, SWIM_EINVAL, "swim_spread: a period is in flight");
   hipLaunchKernelGGL(k_spread, dim3(1), dim3(64), 0, h->stream, h->base, origin, tag);
+  h->host_staged += 1;
   HIPC(h, hipStreamSynchronize(h->stream));
   HIPC(h, hipGetLastError());
   return SWIM_OK;
@@ -1822,6 +1835,7 @@ int swim_deliver_records(swim_handle* h, uint32_t observer, const uint32_t* subj
     track_commit(h, P);
   }
   hipLaunchKernelGGL(k_deliver, dim3(1), dim3(64), 0, s, P, observer, h->deliver_buf, h->deliver_buf + n, n, reason);
+  h->host_staged += 2ull * n;  // (a forwarded copy and a spread per record at most)
   hipLaunchKernelGGL(k_finalize, dim3(blocks_for(P.nloc, 256)), dim3(256), 0, s, P);
   HIPC(h, hipStreamSynchronize(s));
   HIPC(h, hipGetLastError());
