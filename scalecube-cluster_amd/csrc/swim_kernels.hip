@@ -2263,65 +2263,12 @@ __device__ __forceinline__ uint32_t delivered_word(const KP& P, uint32_t sreg, u
 // addToInfected(sender) for every gossip delivered (GossipProtocolImpl.java:181), one word per
 // position of this round's active list (kept in act_ring for the record's lifetime). Runs before
 // k_gossip_apply changes any holdings; PCHUNK positions per wave.
-#ifndef SWIM_REC_FLAT
-#define SWIM_REC_FLAT 0
-#endif
 __global__ void __launch_bounds__(256) k_gossip_record(KP P) {
   SWIM_GUARD(P);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n = P.ctl->rp_cnt < P.spcap ? P.ctl->rp_cnt : P.spcap;
   const uint32_t n_act = P.ctl->n_act, w_beg = P.ctl->w_beg, lo = P.ctl->scan_lo, hi = P.ctl->scan_hi;
   const uint32_t nch = (n_act + PCHUNK - 1u) / PCHUNK;
-#if SWIM_REC_FLAT
-  // lossy / delayed deliveries: a step's 64 positions' window words, then their messages' draws
-  // flattened across the wave (one per lane per step) and the delivered bits met in LDS
-  if (P.loss_mode == 1u || P.delay_on) {
-    __shared__ uint32_t s_dw[4][64];
-    uint32_t* dw = s_dw[threadIdx.x >> 6];
-    for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {  // (wave-uniform)
-      const uint4 rp = P.rp_list[u / nch];  // {in_list entry, receiver, record, sender id}
-      const uint32_t off = P.rec_hdr[rp.z & (P.rcap - 1u)].w;
-      const uint32_t k1 = min(n_act, (u % nch + 1u) * PCHUNK);
-      for (uint32_t k0 = (u % nch) * PCHUNK; k0 < k1; k0 += 64u) {
-        const uint32_t k = k0 + lane;
-        uint32_t v = 0u, ws = 0u;
-        if (k < k1) {
-          const uint32_t ea = P.act[k];
-          if (((ea >> 26) & 3u) != WC_NONE) {
-            if (rp.x & XREC)
-              v = remote_window(P, rp.x & ~XREC, k);
-            else if (rp.x & SPAIR)
-              v = P.pw[P.sp_list[rp.x & ~SPAIR].w + k];
-            else
-              v = own_window(P, rp.x, k, w_beg, lo, hi);
-            ws = wmod(P, w_beg + (ea & ACT_OFF_MASK));
-          }
-        }
-        dw[lane] = 0u;
-        uint32_t tot;
-        const uint32_t qoff = wave_excl_scan((uint32_t)__popc(v), &tot);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        for (uint32_t e0 = 0; e0 < tot; e0 += 64u) {
-          const uint32_t q = e0 + lane;
-          const uint32_t o = wave_owner(qoff, q);  // (every lane shuffles)
-          const uint32_t vo = __shfl(v, (int)o, 64), wo = __shfl(ws, (int)o, 64), oo = __shfl(qoff, (int)o, 64);
-          if (q < tot) {
-            const uint32_t b = kth_set_bit(vo, q - oo);
-            const u32x4 d = draw4(P.seed, K_GOSSIP, rp.w, rp.y, P.g_hash[wo * 32u + b], P.tick);
-            const bool lost = (P.loss_mode == 1u && d.x < P.loss_thr) || (P.delay_on && delay_of_draw(P, d.y) >= P.gint);
-            if (!lost) atomicOr(&dw[o], 1u << b);
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        if (k < k1) P.rec_body[(off + k) & (P.bcap - 1u)] = dw[lane];
-        __builtin_amdgcn_wave_barrier();  // (dw is cleared by the next step)
-      }
-    }
-    return;
-  }
-#endif
   for (uint32_t u = blockIdx.x * 4u + (threadIdx.x >> 6); u < n * nch; u += gridDim.x * 4u) {
     const uint4 rp = P.rp_list[u / nch];  // {in_list entry, receiver, record, sender id}
     const uint32_t off = P.rec_hdr[rp.z & (P.rcap - 1u)].w;
