@@ -222,3 +222,17 @@ def test_c4_schedule_fullsize_properties(workload):
     keys = list(scenarios.PARITY_KEYS) + ["live_gossip_slots", "live_gossip_records", "not_converged"]
     assert {k: st[k] for k in keys} == {k: st2[k] for k in keys}
     assert {k: mid[k] for k in keys} == {k: mid2[k] for k in keys}
+
+
+def test_c3_schedule_8192_matches_oracle():
+    """C3's schedule (10 % crash + the 16-member partition, LAN) at 8,192 members against the CPU oracle:
+    digests, parity counters and events every 4 periods through 24 periods from the crash, then every
+    view and deadline row (tools/parity_c3_8k.py; ~45 s, ~23 GB of oracle state on the host). The largest
+    full-table comparison of the suite; C3 at 65,536 itself is checked by the invariants above."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import parity_c3_8k
+
+    parity_c3_8k.main(8192, 24, 4)

@@ -1,8 +1,9 @@
 """C3's schedule (LAN, 10 % simultaneous crash + the 16-member partition, bench.py's c3) at 8,192 members,
 the GPU handle against the CPU oracle: digests, every parity counter and the MembershipEvent stream every 4
 periods through 24 periods from the crash, every view and deadline row at the end. The oracle needs ~2
-minutes and ~23 GB here, so this runs as a one-off on the GPU box (tools/sessions/r06/o.sh), not in the
-suite, whose largest full-table comparison is 4,096 members. Prints one JSON line."""
+minutes and ~23 GB in the build container (43 s on the GPU box's host): tests/test_gpu_fullsize.py runs it;
+`python tools/parity_c3_8k.py 16384` is the one-off at 16,384 members (~90 GB of oracle state).
+Prints one JSON line."""
 import json
 import os
 import sys
@@ -50,4 +51,4 @@ def main(n=8192, periods=24, every=4):
 
 
 if __name__ == "__main__":
-    main()
+    main(*(int(a) for a in sys.argv[1:3]))
