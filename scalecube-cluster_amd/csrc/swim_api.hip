@@ -93,6 +93,7 @@ struct swim_handle {
   // records): with the FD phase's own (one per member) they bound the FD commit's batch
   uint64_t host_staged = 0;
   bool last_quiet = false;
+  bool period_quiet = false;  // this period's rounds were skipped
   uint64_t quiet_periods = 0;
   uint32_t* d_quiet = nullptr;
   uint32_t* h_quiet = nullptr;  // pinned
@@ -283,7 +284,8 @@ uint64_t commit_tail(const swim_handle* h) { return h->GC / 32 + 2ull + (h->base
 
 // Order the phase's gossips by (subject, record) and commit them: one k_commit launch. stg != nullptr: the local stage, counted on the device (no host round trip); otherwise
 // the n gathered gossips already in h->ck[0] / h->cv[0].
-int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, uint32_t bound = NONE) {
+int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, uint32_t bound = NONE,
+                  bool fused = false) {
   hipStream_t s = h->stream;
   KP P = P0;
   if (P.batch_commit && !h->base.batched) {  // from now on the ring may hold batch slots
@@ -307,7 +309,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
   C.radix = big ? tiles : 0u;
   timed(h, 7, "k_commit", [&] {
     hipLaunchKernelGGL(k_commit, dim3(1), dim3(CS_THREADS), 0, s, P, stg, n, C);
-    if (big && (tiles <= CS_FUSE || SWIM_RS_FUSE_ALL)) {
+    if (big && (tiles <= CS_FUSE || fused || SWIM_RS_FUSE_ALL)) {
       hipLaunchKernelGGL(k_rs_fused, dim3(std::min(tiles, CS_FUSE)), dim3(CS_THREADS), 0, s, P, stg, n, C);
     } else if (big) {
       hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(CS_THREADS), 0, s, P, stg, n, C);
@@ -343,10 +345,10 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
 // reported at the next swim_sync; k_gossip_prep lists nothing once it is set, so a run never
 // feeds a wrapped ring to the gossip kernels). Sharded: the host all-gathers every shard's stage
 // first (returns true: exchange pending); all shards then sort the same batch.
-bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t bound = NONE) {
+bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t bound = NONE, bool fused = false) {
   hipStream_t s = h->stream;
   if (!h->sharded) {
-    *rc = commit_sorted(h, P, P.stg, 0u, bound);
+    *rc = commit_sorted(h, P, P.stg, 0u, bound, fused);
     return false;
   }
   // {overflow, stg_count, n_stop} in one copy: a sharded run stops at the first phase whose
@@ -432,6 +434,7 @@ int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
 constexpr uint64_t QUIET_EVERY = 8;  // periods between tests while the last test found gossips held
 int quiet_rounds(swim_handle* h, bool* quiet) {
   *quiet = false;
+  h->period_quiet = false;
   if (!h->quiet_skip || h->base.dq || h->n_leaving || h->base.njoin) return SWIM_OK;
   if (!h->last_quiet && h->period % QUIET_EVERY != 0) return SWIM_OK;
   hipStream_t s = h->stream;
@@ -447,6 +450,7 @@ int quiet_rounds(swim_handle* h, bool* quiet) {
     if (h->dict_on) hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, Q.dsids / 256)), dim3(256), 0, s, Q);
   });
   h->quiet_periods++;
+  h->period_quiet = true;
   *quiet = true;
   return SWIM_OK;
 }
@@ -724,7 +728,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         timed(h, 5, "k_sync_ack", [&] { hipLaunchKernelGGL(k_sync_ack, dim3(std::min(nloc, SY_GRID)), dim3(256), 0, s, P); });
         timed(h, 7, "k_finalize", [&] { hipLaunchKernelGGL(k_finalize, dim3(gL), dim3(256), 0, s, P); });
         h->pc = PC_END;  // the SYNC and SYNC_ACK gossips (both created at round (t+1)G)
-        if (commit_begin(h, P, x, &rc)) return SWIM_OK;
+        // (no host-side bound: SYNC merges re-spread what they accept. After a quiet period's rounds the
+        // batch is small or empty, so it is sorted by the single-launch chain, k_rs_fused, which walks
+        // any number of tiles on its CS_FUSE workgroups, instead of the eleven launches sized for the
+        // stage's capacity: steady65k ten launches fewer per period)
+        if (commit_begin(h, P, x, &rc, NONE, h->period_quiet)) return SWIM_OK;
         if (rc) return rc;
         break;
       case PC_END: {
