@@ -194,7 +194,8 @@ MAJOR_CLASSES = ["k_gossip_select", "k_gossip_pull", "k_gossip_apply", "k_susp_s
 KERNEL_NAMES = {"k_gossip_apply": ["k_gossip_apply", "k_gossip_apply_b", "k_gossip_apply_h4", "k_gossip_apply_b_h4",
                                    "k_gossip_apply_b16", "k_gossip_apply_b16_h4"],
                 "k_gossip_select": ["k_gossip_select", "k_gossip_select_h4"],
-                "k_gossip_pull": ["k_gossip_pull", "k_gossip_pull_loss", "k_gossip_pull_dq"],
+                "k_gossip_pull": ["k_gossip_pull", "k_gossip_pull_loss", "k_gossip_pull_dq", "k_gossip_pull_s4",
+                                  "k_gossip_pull_loss_s4"],
                 "k_gossip_pairwin": ["k_gossip_pairfill", "k_gossip_pairprune", "k_gossip_pairdelay"]}
 
 
