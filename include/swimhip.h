@@ -200,7 +200,8 @@ typedef struct swim_stats {
                                  instead of walking their ids; 0 in the oracle */
   uint64_t apply_bitmap_records; /* the records of those ranges (their ids were not read)          */
   uint64_t quiet_periods;     /* periods whose gossip rounds were skipped: no member held a gossip
-                                 (quiet periods); 0 in the oracle                 */
+                                 (quiet periods; SWIMHIP_QUIET=0 in the environment
+                                 at swim_create runs every round, for A/B tests); 0 in the oracle */
 } swim_stats;
 
 typedef struct swim_handle swim_handle;
