@@ -8,9 +8,9 @@ parity counter and the presence vectors equal every few periods, and no buffer o
   handle fit one MI355X's 288 GB) through 44 storm periods. The 1 % loss starts a storm (false
   suspicions re-spread by SYNC, MembershipProtocolImpl.java:649-656; one GossipRequest per gossip,
   each lost independently, GossipProtocolImpl.java:225-239 / NetworkEmulator.java:166-180).
-* C5 (LAN, N x K views with K = 256, 256 simultaneous crashes = concurrent churn): at 131,072 members
-  through 100 periods, past the first suspicion timeouts (5 x bit_length(131,071) = 85 periods of
-  suspicion, MembershipProtocolImpl.java:620-647, then the DEAD gossips, GossipProtocolImpl.java:171-183).
+* C5 (LAN, N x K views with K = 256, 256 simultaneous crashes = concurrent churn): at 262,144 members
+  through 110 periods, past the suspicion timeouts (5 x bit_length(262,143) = 90 periods of suspicion,
+  MembershipProtocolImpl.java:620-647, then the removals; GossipProtocolImpl.java:171-183).
 """
 import os
 import socket
@@ -91,9 +91,11 @@ def test_c4_schedule_65536_world8_matches_unsharded():
 
 
 @pytest.mark.gpu
-def test_c5_schedule_131072_world8_matches_unsharded():
-    """C5's schedule at 131,072 members (N x K, K = 256, 256 simultaneous crashes) over 8 shards,
-    compared every 5 periods through 100 periods: the crashed members' suspicion timeouts fire (every
-    alive observer removes all 256) within the window."""
-    mp.spawn(_worker, args=(8, _free_port(), 1 << 17, dict(gossip_capacity=1 << 17, tracked_subjects=256), 0.0,
-                            256, 3, 100, 5, 1), nprocs=8, join=True)
+def test_c5_schedule_262144_world8_matches_unsharded():
+    """C5's schedule at 262,144 members - a quarter of BASELINE configs[4]'s 2^20 - (N x K, K = 256, 256
+    simultaneous crashes) over 8 shards, compared every 10 periods through 110 periods: the crashed
+    members' suspicion timeouts fire (every alive observer removes all 256: 67,043,328 removals) within
+    the window. The ring has 80 x 1,024 slots (not a power of two), 1.85x this storm's ~44,300 live batch
+    slots: two copies of the cluster with 2^18 slots do not fit one GPU. ~25 s."""
+    mp.spawn(_worker, args=(8, _free_port(), 1 << 18, dict(gossip_capacity=80 * 1024, tracked_subjects=256), 0.0,
+                            256, 3, 110, 10, 1), nprocs=8, join=True)

@@ -9,5 +9,5 @@ timeout -k 10 560 python -u -m pytest tests/test_c4_rehearsal.py -m gpu -x -v -s
    --timeout-method thread -k "65536" --durations 5 > $out/pytest_c4_65536.log 2>&1
 rc=$?; echo "c4 65536 rc=$rc" >> $out/status.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 560 python -u -m pytest tests/test_c4_rehearsal.py -m gpu -x -v -s -p no:cacheprovider --timeout 540 \
-   --timeout-method thread -k "131072" --durations 5 > $out/pytest_c5_131072.log 2>&1
-rc=$?; echo "c5 131072 rc=$rc" >> $out/status.log; exit $rc
+   --timeout-method thread -k "262144" --durations 5 > $out/pytest_c5_262144.log 2>&1
+rc=$?; echo "c5 262144 rc=$rc" >> $out/status.log; exit $rc
