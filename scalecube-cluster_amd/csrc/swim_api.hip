@@ -102,7 +102,11 @@ struct swim_handle {
   swim_transport tr{};
   bool has_tr = false;
   ncclComm_t comm = nullptr;
-  uint64_t* d_status = nullptr;  // [(1 + world) * (2 + world)]: this rank's status row, then all ranks'
+  uint64_t* d_status = nullptr;  // [(1 + world) * (XS_CNT + world)]: this rank's status row, then all ranks'
+  uint32_t xpend = 0;              // XsKind whose k_xstatus row awaits xpost
+  uint64_t xrow[XS_CNT + SWIM_MAX_WORLD] = {0};  // host-driven exchanges: this rank's row, read back
+  uint64_t xhead[2] = {0, 0};       // the status row's host half {code, op}
+  uint32_t chead[4] = {0, 0, 0, 0};  // a commit block's header
   std::vector<uint8_t> hsend, hrecv;  // host staging of a host_staged transport
   std::string err;
   // timing
@@ -264,12 +268,6 @@ void track_commit(swim_handle* h, const KP& P) {
   hipLaunchKernelGGL(k_colorder, dim3(1), dim3(256), 0, h->stream, P);
 }
 
-int read_ctl(swim_handle* h, Ctl* c) {
-  HIPC(h, hipMemcpyAsync(c, h->base.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->stream));
-  HIPC(h, hipStreamSynchronize(h->stream));
-  return SWIM_OK;
-}
-
 void xchg_clear(swim_xchg* x, uint32_t op, uint32_t world) {
   std::memset(x, 0, sizeof *x);
   x->op = op;
@@ -341,50 +339,134 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
   return SWIM_OK;
 }
 
+// The end of a pack before an exchange. A host that performs the exchange itself (swim_shard_step) reads
+// the send buffer once swim_shard_step returns, so the stream is synchronized here; the library's own
+// transports are ordered on the stream already (RCCL enqueues on it; a host-staged transport copies the
+// buffer out and synchronizes before its callback), so they skip this host stop (round 6: 7 of a
+// period's ~2 x (4 + 4G) host stops at G = 5 are these).
+hipError_t xorder(swim_handle* h) { return h->has_tr ? hipSuccess : hipStreamSynchronize(h->stream); }
+
+// An exchange's device-side failure, on the rank whose state raised it (the others report "rank q failed")
+int xown_fail(swim_handle* h, uint32_t kind) {
+  switch (kind) {
+    case XS_COMMIT:
+    case XS_DONE: {
+      const int rc = check_overflow(h);
+      return rc ? rc : fail(h, SWIM_EOVERFLOW, "simulator buffer overflow");
+    }
+    case XS_SEL: return fail(h, SWIM_EOVERFLOW, "active list too long for sharded need bitmaps");
+    case XS_WIN: return fail(h, SWIM_EOVERFLOW, "gossip exchange buffer too small");
+    case XS_SYNC: return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
+    default: return fail(h, SWIM_EINVAL, "shard exchange: unknown status kind");
+  }
+}
+
+// The host half of an exchange whose counts k_xstatus wrote into `row` (this rank's status row, after the
+// status all-gather, or read back by xready): pack the send buffer and set this rank's send counts.
+int xpost(swim_handle* h, swim_xchg* x, const uint64_t* row) {
+  const uint32_t kind = h->xpend, W = h->world;
+  h->xpend = XS_NONE;
+  hipStream_t s = h->stream;
+  KP& P = h->cur;
+  P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
+  switch (kind) {
+    case XS_COMMIT: {
+      // Once any member left (n_leaving: the same on every rank, swim_leave is collective), each block
+      // starts with a header {gossips, stopped members, 0, 0} and carries the members this shard
+      // stopped (k_leave_stop) after its gossips: liveness is replicated. Block layout:
+      //   [header (leaves only) | gossips 4n | stopped (leaves only) | wlast W32 | bhi | 32 - blo]
+      const uint32_t n = (uint32_t)row[XS_A0], ns = (uint32_t)row[XS_A1];
+      const uint32_t hdr = h->n_leaving ? 4u : 0u;
+      uint32_t* xs = P.xsend;
+      if (hdr) {
+        h->chead[0] = n;
+        h->chead[1] = ns;
+        HIPC(h, hipMemcpyAsync(xs, h->chead, 16, hipMemcpyHostToDevice, s));
+      }
+      if (n) HIPC(h, hipMemcpyAsync(xs + hdr, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s));
+      if (ns) HIPC(h, hipMemcpyAsync(xs + hdr + 4u * n, P.stop_list, (size_t)ns * 4, hipMemcpyDeviceToDevice, s));
+      HIPC(h, hipMemsetAsync(&P.ctl->stg_count, 0, 8, s));  // stg_count and n_stop
+      hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, P, hdr + 4u * n + ns);
+      x->send_words = row[XS_CNT];
+      break;
+    }
+    case XS_TRACK:  // (k_track_pack ran before k_xstatus)
+      x->send_words = row[XS_CNT];
+      return SWIM_OK;
+    case XS_SEL: {  // (1) registrations with receivers on other shards
+      h->nneed = ((uint32_t)row[XS_A0] + 31u) / 32u;
+      uint32_t n_rec = 0;
+      for (uint32_t q = 0; q < W; ++q) {
+        x->send_counts[q] = row[XS_CNT + q];
+        h->out_pairs[q] = (uint32_t)(row[XS_CNT + q] / 2);
+        n_rec += h->out_pairs[q];
+      }
+      h->n_out_pairs = n_rec;
+      if (n_rec) hipLaunchKernelGGL(k_gossip_pack_pairs, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
+      break;
+    }
+    case XS_WIN:  // (3) the needed window words
+      for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = row[XS_CNT + q];
+      P.nneed = h->nneed;
+      hipLaunchKernelGGL(k_gossip_pack_sparse, dim3(std::min<uint32_t>(h->n_out_pairs, 8192)), dim3(256), 0, s, P,
+                         h->n_out_pairs, h->nneed);
+      break;
+    case XS_SYNC: {  // tables of requesters whose receiver lives on another shard
+      h->sync_rl = (uint32_t)row[XS_A0];  // (the same on every shard: tbits are merged)
+      const uint32_t n_rec = (uint32_t)row[XS_A1];
+      for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = row[XS_CNT + q];
+      if (n_rec) hipLaunchKernelGGL(k_sync_pack, dim3(std::min<uint32_t>(n_rec, 4096)), dim3(256), 0, s, P, n_rec);
+      break;
+    }
+    case XS_DONE:
+      resolve_timing(h);
+      return SWIM_OK;
+    default:
+      return fail(h, SWIM_EINVAL, "shard exchange: unknown status kind");
+  }
+  HIPC(h, xorder(h));
+  return SWIM_OK;
+}
+
+// An exchange whose counts are on the device: k_xstatus writes them, and what this
+// shard's state says is wrong, into this rank's status row. With a transport the row rides the status
+// all-gather, one host stop for both, and tr_period runs xpost after it; a host that performs the
+// exchanges itself (swim_shard_step) reads the row back here and goes on at once. x->op is set.
+int xready(swim_handle* h, const KP& P, swim_xchg* x, XsArgs a) {
+  a.world = h->world;
+  hipLaunchKernelGGL(k_xstatus, dim3(1), dim3(64), 0, h->stream, (const Ctl*)P.ctl, (const uint32_t*)P.woff,
+                     h->d_status, a);
+  h->xpend = a.kind;
+  if (h->has_tr) return SWIM_OK;
+  HIPC(h, hipMemcpyAsync(h->xrow, h->d_status, 8ull * (XS_CNT + h->world), hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipStreamSynchronize(h->stream));
+  if (h->xrow[XS_ERR]) {
+    h->xpend = XS_NONE;
+    return xown_fail(h, a.kind);
+  }
+  return xpost(h, x, h->xrow);
+}
+
 // Commit the phase's staged gossips. Unsharded: in place, sized on the device (overflow is
 // reported at the next swim_sync; k_gossip_prep lists nothing once it is set, so a run never
 // feeds a wrapped ring to the gossip kernels). Sharded: the host all-gathers every shard's stage
 // first (returns true: exchange pending); all shards then sort the same batch.
 bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t bound = NONE, bool fused = false) {
-  hipStream_t s = h->stream;
   if (!h->sharded) {
     *rc = commit_sorted(h, P, P.stg, 0u, bound, fused);
     return false;
   }
-  // {overflow, stg_count, n_stop} in one copy: a sharded run stops at the first phase whose
-  // buffers overflowed; the hosts share the error with every rank before the next collective
-  // (swimhip/sharded.py, status all-gather).
-  static_assert(offsetof(Ctl, stg_count) == offsetof(Ctl, overflow) + 4, "Ctl layout");
-  static_assert(offsetof(Ctl, n_stop) == offsetof(Ctl, overflow) + 8, "Ctl layout");
-  uint32_t ovn[3] = {0u, 0u, 0u};
-  HIPC_RC(h, rc, hipMemcpyAsync(ovn, &P.ctl->overflow, 12, hipMemcpyDeviceToHost, s));
-  HIPC_RC(h, rc, hipStreamSynchronize(s));
-  if (ovn[0]) {
-    *rc = check_overflow(h);
-    return false;
-  }
-  const uint32_t n = std::min(ovn[1], P.stg_cap);  // beyond: OV_GOSSIP already raised
-  // Once any member left (n_leaving: the same on every rank, swim_leave is collective), each block
-  // starts with a header {gossips, stopped members, 0, 0} and carries the members this shard
-  // stopped (k_leave_stop) after its gossips: liveness is replicated. Block layout:
-  //   [header (leaves only) | gossips 4n | stopped (leaves only) | wlast W32 | bhi | 32 - blo]
-  const uint32_t ns = h->n_leaving ? std::min(ovn[2], P.nloc) : 0u;
-  const uint32_t hdr = h->n_leaving ? 4u : 0u;
-  uint32_t* xs = reinterpret_cast<uint32_t*>(h->xsend);
-  if (hdr) {
-    const uint32_t head[4] = {n, ns, 0u, 0u};
-    HIPC_RC(h, rc, hipMemcpyAsync(xs, head, 16, hipMemcpyHostToDevice, s));
-  }
-  if (n) (void)hipMemcpyAsync(xs + hdr, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s);
-  if (ns) (void)hipMemcpyAsync(xs + hdr + 4u * n, P.stop_list, (size_t)ns * 4, hipMemcpyDeviceToDevice, s);
-  HIPC_RC(h, rc, hipMemsetAsync(&P.ctl->stg_count, 0, 8, s));  // stg_count and n_stop
-  KP Q = P;
-  Q.xsend = xs;
-  hipLaunchKernelGGL(k_round_max_pack, dim3(64), dim3(256), 0, s, Q, hdr + 4u * n + ns);
-  HIPC_RC(h, rc, hipStreamSynchronize(s));
+  // {overflow, stg_count, n_stop} go into the status row (k_xstatus): a sharded run stops at the first
+  // phase whose buffers overflowed, every rank at the same exchange; the block is packed after (xpost)
+  XsArgs a{};
+  a.kind = XS_COMMIT;
+  a.cap = P.stg_cap;
+  a.hdr = h->n_leaving ? 4u : 0u;
+  a.nloc = h->n_leaving ? P.nloc : 0u;
+  a.tail = commit_tail(h);
   xchg_clear(x, SWIM_X_ALLGATHER, h->world);
-  x->send_words = hdr + 4ull * n + ns + commit_tail(h);
-  return true;
+  *rc = xready(h, P, x, a);
+  return *rc == SWIM_OK;
 }
 
 int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
@@ -473,14 +555,13 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (P.nxk) {  // N x K: columns for the subjects this FD phase changes first
           timed(h, 0, "k_fd_track", [&] { hipLaunchKernelGGL(k_fd_track, dim3(gL), dim3(256), 0, s, P); });
           if (SH) {  // every shard's requests to every shard: all allocate the same columns
-            Ctl c;
-            if ((rc = read_ctl(h, &c))) return rc;
             P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
             hipLaunchKernelGGL(k_track_pack, dim3(1), dim3(256), 0, s, P);
-            HIPC(h, hipStreamSynchronize(s));
             xchg_clear(x, SWIM_X_ALLGATHER, W);
-            x->send_words = std::min(c.ntrack, P.tcap);
-            return SWIM_OK;
+            XsArgs a{};
+            a.kind = XS_TRACK;
+            a.cap = P.tcap;
+            return xready(h, P, x, a);
           }
           track_commit(h, P);
         }
@@ -535,23 +616,11 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (P.dq)  // rings exist once a delay was set; messages in flight arrive even after it is reset
           timed(h, 10, "k_gossip_pairdelay", [&] { hipLaunchKernelGGL(k_gossip_pairdelay, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_R_NEED;
-        if (SH) {  // (1) registrations with receivers on other shards
-          Ctl c;
-          if ((rc = read_ctl(h, &c))) return rc;
-          if (c.n_act > 32u * 1024u) return fail(h, SWIM_EOVERFLOW, "active list too long for sharded need bitmaps");
-          h->nneed = (c.n_act + 31u) / 32u;
-          uint32_t n_rec = 0;
+        if (SH) {  // (1) registrations with receivers on other shards (packed by xpost)
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
-          for (uint32_t q = 0; q < W; ++q) {
-            x->send_counts[q] = 2ull * c.xg_cnt[q];
-            h->out_pairs[q] = c.xg_cnt[q];
-            n_rec += c.xg_cnt[q];
-          }
-          h->n_out_pairs = n_rec;
-          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-          if (n_rec) hipLaunchKernelGGL(k_gossip_pack_pairs, dim3(blocks_for(n_rec, 256)), dim3(256), 0, s, P, n_rec);
-          HIPC(h, hipStreamSynchronize(s));
-          return SWIM_OK;
+          XsArgs a{};
+          a.kind = XS_SEL;
+          return xready(h, P, x, a);
         }
         h->pc = PC_R_PULL;
         break;
@@ -576,7 +645,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         }
         xchg_clear(x, SWIM_X_ALLTOALLV, W);
         for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
-        HIPC(h, hipStreamSynchronize(s));
+        HIPC(h, xorder(h));
         h->pc = PC_R_WIN;
         return SWIM_OK;
       }
@@ -586,23 +655,16 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
         P.nneed = h->nneed;
         xchg_clear(x, SWIM_X_ALLTOALLV, W);
-        if (n_out) {
+        h->pc = PC_R_PULL;
+        if (n_out) {  // per-peer volumes from the scanned word counts (k_xstatus), packed by xpost
           hipLaunchKernelGGL(k_gossip_wcount, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, P, n_out, h->nneed);
           hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(CS_THREADS), 0, s, P.wcnt, P.woff, n_out + 1);
-          std::vector<uint32_t> woff(n_out + 1);
-          HIPC(h, hipMemcpyAsync(woff.data(), P.woff, 4ull * (n_out + 1), hipMemcpyDeviceToHost, s));
-          HIPC(h, hipStreamSynchronize(s));
-          if (woff[n_out] > h->xsend_words) return fail(h, SWIM_EOVERFLOW, "gossip exchange buffer too small");
-          uint32_t g = 0;
-          for (uint32_t q = 0; q < W; ++q) {
-            x->send_counts[q] = woff[g + h->out_pairs[q]] - woff[g];
-            g += h->out_pairs[q];
-          }
-          hipLaunchKernelGGL(k_gossip_pack_sparse, dim3(std::min<uint32_t>(n_out, 8192)), dim3(256), 0, s, P, n_out,
-                             h->nneed);
+          XsArgs a{};
+          a.kind = XS_WIN;
+          a.cap = (uint32_t)std::min<uint64_t>(h->xsend_words, NONE);
+          for (uint32_t q = 0; q < W; ++q) a.bnd[q + 1] = a.bnd[q] + h->out_pairs[q];
+          return xready(h, P, x, a);
         }
-        HIPC(h, hipStreamSynchronize(s));
-        h->pc = PC_R_PULL;
         return SWIM_OK;
       }
       case PC_R_PULL:
@@ -664,21 +726,15 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         if (P.njoin) hipLaunchKernelGGL(k_join_select, dim3(blocks_for(N, 256)), dim3(256), 0, s, P);
         timed(h, 6, "k_sync_snapshot", [&] { hipLaunchKernelGGL(k_sync_snapshot, dim3(1024), dim3(256), 0, s, P); });
         h->pc = PC_SYNC_REQ;
-        if (SH) {  // tables of requesters whose receiver lives on another shard
-          Ctl c;
-          if ((rc = read_ctl(h, &c))) return rc;
-          RL = (P.tmode && c.ntouched < N) ? c.ntouched : P.W;  // (the same on every shard: tbits are merged)
-          uint32_t n_rec = 0;
+        if (SH) {  // tables of requesters whose receiver lives on another shard (row cells RL: k_xstatus)
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
-          for (uint32_t q = 0; q < W; ++q) {
-            x->send_counts[q] = (uint64_t)c.xs_cnt[q] * (RL + 2u);
-            n_rec += c.xs_cnt[q];
-          }
-          if (n_rec > h->scap) return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity");
-          P.xsend = reinterpret_cast<uint32_t*>(h->xsend);
-          if (n_rec) hipLaunchKernelGGL(k_sync_pack, dim3(std::min<uint32_t>(n_rec, 4096)), dim3(256), 0, s, P, n_rec);
-          HIPC(h, hipStreamSynchronize(s));
-          return SWIM_OK;
+          XsArgs a{};
+          a.kind = XS_SYNC;
+          a.cap = h->scap;
+          a.tmode = P.tmode;
+          a.N = N;
+          a.rl_dense = P.W;
+          return xready(h, P, x, a);
         }
         break;
       case PC_SYNC_REQ: {
@@ -711,7 +767,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           for (uint32_t q = 0; q < W; ++q) back[q] = x->recv_counts[q];
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
           for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
-          HIPC(h, hipStreamSynchronize(s));
+          HIPC(h, xorder(h));
           return SWIM_OK;
         }
         break;
@@ -863,15 +919,23 @@ int tr_alltoallv(swim_handle* h, const uint64_t* sb, const uint64_t* rb) {
 // never a hang. The leave count rides along because it sets the layout of every commit block (a
 // {gossips, stopped} header once any member left): ranks that disagree fail instead of misreading.
 int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t>* rows) {
-  const uint32_t W = h->world, R = 2u + W;
-  std::vector<uint64_t> row(R, 0ull);
-  row[0] = (uint64_t)(int64_t)code;
+  const uint32_t W = h->world, R = XS_CNT + W;
   // (the resume point too: ranks that took different branches of a period fail here, "out of step")
-  row[1] = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | (uint64_t)(uint32_t)h->pc << 8 | x.op);
-  if (!code && x.op == SWIM_X_ALLGATHER) row[2] = x.send_words;
-  if (!code && x.op == SWIM_X_ALLTOALLV)
-    for (uint32_t q = 0; q < W; ++q) row[2 + q] = x.send_counts[q];
-  HIPC(h, hipMemcpyAsync(h->d_status, row.data(), 8ull * R, hipMemcpyHostToDevice, h->stream));
+  const uint64_t op = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | (uint64_t)(uint32_t)h->pc << 8 | x.op);
+  if (!code && h->xpend) {  // k_xstatus wrote the rest of the row
+    h->xhead[0] = 0;
+    h->xhead[1] = op;
+    HIPC(h, hipMemcpyAsync(h->d_status, h->xhead, 16, hipMemcpyHostToDevice, h->stream));
+  } else {
+    h->xpend = XS_NONE;
+    std::vector<uint64_t> row(R, 0ull);
+    row[0] = (uint64_t)(int64_t)code;
+    row[1] = op;
+    if (!code && x.op == SWIM_X_ALLGATHER) row[XS_CNT] = x.send_words;
+    if (!code && x.op == SWIM_X_ALLTOALLV)
+      for (uint32_t q = 0; q < W; ++q) row[XS_CNT + q] = x.send_counts[q];
+    HIPC(h, hipMemcpyAsync(h->d_status, row.data(), 8ull * R, hipMemcpyHostToDevice, h->stream));
+  }
   int rc = tr_allgather(h, h->d_status, h->d_status + R, 8ull * R);
   if (rc) return rc;
   rows->resize((size_t)W * R);
@@ -883,53 +947,63 @@ int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t
 // One period of a sharded handle with a transport: period_resume up to each exchange, the status
 // all-gather, the collective, resume.
 int tr_period(swim_handle* h) {
-  const uint32_t W = h->world, R = 2u + W;
+  const uint32_t W = h->world, R = XS_CNT + W;
   std::vector<uint64_t> rows;
   swim_xchg x;  // carries each exchange's receive counts into the resumed period
   xchg_clear(&x, SWIM_X_DONE, W);
   for (;;) {
+    h->xpend = XS_NONE;
     int rc = period_resume(h, &x);
-    if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow check joins the status
-      HIPC(h, hipStreamSynchronize(h->stream));
-      resolve_timing(h);
-      rc = check_overflow(h);
+    if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow flag joins the status
+      XsArgs a{};
+      a.kind = XS_DONE;
+      rc = xready(h, h->cur, &x, a);
     }
     const std::string mine = rc ? h->err : std::string();
+    const uint32_t kind = h->xpend;
     const int src = tr_status(h, rc, x, &rows);
     if (src) return src;
-    for (uint32_t q = 0; q < W; ++q)
-      if (rows[(size_t)q * R]) {
+    if (!rc && kind && rows[(size_t)h->rank * R + XS_ERR]) {
+      h->xpend = XS_NONE;
+      return xown_fail(h, kind);
+    }
+    for (uint32_t q = 0; q < W; ++q) {
+      const uint64_t e = rows[(size_t)q * R] ? rows[(size_t)q * R] : rows[(size_t)q * R + XS_ERR];
+      if (e) {
+        h->xpend = XS_NONE;
         if (rc) return fail(h, rc, mine);
-        return fail(h, (int)(int64_t)rows[(size_t)q * R], "shard exchange: rank " + std::to_string(q) + " failed");
+        return fail(h, (int)(int64_t)e, "shard exchange: rank " + std::to_string(q) + " failed");
       }
+    }
     for (uint32_t q = 1; q < W; ++q) {
       if ((rows[(size_t)q * R + 1] >> 32) != (rows[1] >> 32))
         return fail(h, SWIM_EINVAL, "shard exchange: ranks disagree on swim_leave calls (rank " + std::to_string(q) + ")");
       if (rows[(size_t)q * R + 1] != rows[1]) return fail(h, SWIM_EINVAL, "shard exchange: ranks out of step");
     }
+    if (h->xpend && (rc = xpost(h, &x, &rows[(size_t)h->rank * R]))) return rc;
     if (x.op == SWIM_X_DONE) return SWIM_OK;
     if (x.op == SWIM_X_ALLGATHER) {
       uint64_t m = 0;
-      for (uint32_t q = 0; q < W; ++q) m = std::max(m, rows[(size_t)q * R + 2]);
+      for (uint32_t q = 0; q < W; ++q) m = std::max(m, rows[(size_t)q * R + XS_CNT]);
       if (m * W > h->xrecv_words) return fail(h, SWIM_EOVERFLOW, "shard exchange: all-gather over the receive buffer");
       if (m && (rc = tr_allgather(h, h->xsend, h->xrecv, 4ull * m))) return rc;
-      for (uint32_t q = 0; q < W; ++q) x.recv_counts[q] = rows[(size_t)q * R + 2];
+      for (uint32_t q = 0; q < W; ++q) x.recv_counts[q] = rows[(size_t)q * R + XS_CNT];
       x.recv_stride = m;
     } else if (x.op == SWIM_X_ALLTOALLV) {
       uint64_t sb[SWIM_MAX_WORLD], rb[SWIM_MAX_WORLD], vol = 0;
       for (uint32_t r = 0; r < W; ++r) {  // every rank checks every rank's volumes: all fail together
         uint64_t out = 0, in = 0;
         for (uint32_t q = 0; q < W; ++q) {
-          out += rows[(size_t)r * R + 2 + q];
-          in += rows[(size_t)q * R + 2 + r];
+          out += rows[(size_t)r * R + XS_CNT + q];
+          in += rows[(size_t)q * R + XS_CNT + r];
         }
         if (out > h->xsend_words || in > h->xrecv_words)
           return fail(h, SWIM_EOVERFLOW, "shard exchange over the buffer capacity on rank " + std::to_string(r));
         vol += out;
       }
       for (uint32_t q = 0; q < W; ++q) {
-        sb[q] = 4ull * rows[(size_t)h->rank * R + 2 + q];
-        rb[q] = 4ull * rows[(size_t)q * R + 2 + h->rank];
+        sb[q] = 4ull * rows[(size_t)h->rank * R + XS_CNT + q];
+        rb[q] = 4ull * rows[(size_t)q * R + XS_CNT + h->rank];
         x.recv_counts[q] = rb[q] / 4;
       }
       if (vol && (rc = tr_alltoallv(h, sb, rb))) return rc;
@@ -942,7 +1016,7 @@ int tr_period(swim_handle* h) {
 
 // exchange buffers and the status rows of a handle that drives its own exchanges
 int tr_buffers(swim_handle* h) {
-  const uint32_t W = h->world, R = 2u + W;
+  const uint32_t W = h->world, R = XS_CNT + W;
   int rc = SWIM_OK;
   if (!h->d_status && (rc = dalloc(h, &h->d_status, (size_t)(1 + W) * R))) return rc;
   if (!h->xsend) {
@@ -2286,6 +2360,7 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev) {
   swim_shard_buffer_words(h, &sw, &rw);
   h->xsend_words = sw;
   h->xrecv_words = rw;
+  if (!h->d_status) return dalloc(h, &h->d_status, (size_t)(1 + h->world) * (XS_CNT + h->world));
   return SWIM_OK;
 }
 

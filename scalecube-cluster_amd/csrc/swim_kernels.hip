@@ -3896,6 +3896,73 @@ __global__ void k_sync_ack_unpack(KP P, uint32_t n_rec) {
   }
 }
 
+// The device half of a library-driven exchange's status row: the counts an exchange
+// needs are in Ctl, so they go into the row the status all-gather carries instead of to the host first
+// (one host stop per exchange, not two). row[XS_ERR]: an error this shard's state raises (every rank sees
+// it and fails at the same exchange); row[XS_A0], row[XS_A1]: what the host needs afterwards;
+// row[XS_CNT + q]: words to rank q (an all-gather: row[XS_CNT] alone).
+enum XsKind : uint32_t { XS_NONE = 0, XS_COMMIT, XS_TRACK, XS_SEL, XS_WIN, XS_SYNC, XS_DONE };
+constexpr uint32_t XS_ERR = 2, XS_A0 = 3, XS_A1 = 4, XS_CNT = 5;
+struct XsArgs {
+  uint32_t kind, world;
+  uint32_t cap;      // COMMIT: stage capacity; TRACK: track capacity; WIN: send words; SYNC: sync_capacity
+  uint32_t hdr;      // COMMIT: block header words (leaves)
+  uint32_t nloc;     // COMMIT: stopped-member clamp (leaves), else 0
+  uint32_t rl_dense; // SYNC: row cells without touched columns
+  uint32_t tmode, N;
+  uint64_t tail;     // COMMIT: words after the gossips and stopped members
+  uint32_t bnd[SWIM_MAX_WORLD + 1];  // WIN: the out pairs' first index per peer shard
+};
+__global__ void k_xstatus(const Ctl* c, const uint32_t* woff, uint64_t* row, XsArgs a) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint64_t err = 0, a0 = 0, a1 = 0;
+  for (uint32_t q = 0; q < a.world; ++q) row[XS_CNT + q] = 0;
+  switch (a.kind) {
+    case XS_COMMIT: {
+      const uint32_t n = c->stg_count < a.cap ? c->stg_count : a.cap;  // beyond: OV_GOSSIP already raised
+      const uint32_t ns = c->n_stop < a.nloc ? c->n_stop : a.nloc;
+      err = c->overflow ? SWIM_EOVERFLOW : 0;
+      a0 = n;
+      a1 = ns;
+      row[XS_CNT] = a.hdr + 4ull * n + ns + a.tail;
+      break;
+    }
+    case XS_TRACK:
+      row[XS_CNT] = c->ntrack < a.cap ? c->ntrack : a.cap;
+      break;
+    case XS_SEL:
+      err = c->n_act > 32u * 1024u ? SWIM_EOVERFLOW : 0;
+      a0 = c->n_act;
+      for (uint32_t q = 0; q < a.world; ++q) {
+        row[XS_CNT + q] = 2ull * c->xg_cnt[q];
+        a1 += c->xg_cnt[q];
+      }
+      break;
+    case XS_WIN: {
+      const uint32_t n_out = a.bnd[a.world];
+      err = woff[n_out] > a.cap ? SWIM_EOVERFLOW : 0;
+      for (uint32_t q = 0; q < a.world; ++q) row[XS_CNT + q] = woff[a.bnd[q + 1]] - woff[a.bnd[q]];
+      break;
+    }
+    case XS_SYNC: {
+      const uint32_t rl = (a.tmode && c->ntouched < a.N) ? c->ntouched : a.rl_dense;
+      for (uint32_t q = 0; q < a.world; ++q) {
+        row[XS_CNT + q] = (uint64_t)c->xs_cnt[q] * (rl + 2u);
+        a1 += c->xs_cnt[q];
+      }
+      err = a1 > a.cap ? SWIM_EOVERFLOW : 0;
+      a0 = rl;
+      break;
+    }
+    case XS_DONE:
+      err = c->overflow ? SWIM_EOVERFLOW : 0;
+      break;
+  }
+  row[XS_ERR] = err;
+  row[XS_A0] = a0;
+  row[XS_A1] = a1;
+}
+
 // Every commit exchange also carries the shard's per-word gossip liveness (wlast) and its
 // bit-length bounds after the words of its staged gossips: [gossips | wlast | bhi | 32 - blo]
 __global__ void k_round_max_pack(KP P, uint32_t off) {
