@@ -103,10 +103,19 @@ struct swim_handle {
   bool has_tr = false;
   ncclComm_t comm = nullptr;
   uint64_t* d_status = nullptr;  // [(1 + world) * (XS_CNT + world)]: this rank's status row, then all ranks'
-  uint32_t xpend = 0;              // XsKind whose k_xstatus row awaits xpost
-  uint64_t xrow[XS_CNT + SWIM_MAX_WORLD] = {0};  // host-driven exchanges: this rank's row, read back
-  uint64_t xhead[2] = {0, 0};       // the status row's host half {code, op}
-  uint32_t chead[4] = {0, 0, 0, 0};  // a commit block's header
+  uint32_t xpend = 0;  // XsKind whose k_xstatus row awaits xpost
+  // Pinned host words of the exchanges (sharded handles): small copies from pageable memory go through
+  // a staging buffer and wait for it, so every copy of a period's exchanges is pinned
+  struct XPin {
+    uint64_t head[2];                                      // the status row's host half {code, op}
+    uint32_t chead[4];                                     // a commit block's header
+    uint32_t offs[SWIM_MAX_WORLD];                         // commit blocks' tail offsets
+    uint32_t cnt[SWIM_MAX_WORLD];                          // N x K track counts
+    uint32_t bhead[2];                                     // a received commit block's header
+    uint64_t xrow[XS_CNT + SWIM_MAX_WORLD];                // host-driven exchanges: this rank's row
+    uint64_t rows[SWIM_MAX_WORLD * (XS_CNT + SWIM_MAX_WORLD)];  // the gathered status rows
+  };
+  XPin* xp = nullptr;
   std::vector<uint8_t> hsend, hrecv;  // host staging of a host_staged transport
   std::string err;
   // timing
@@ -163,6 +172,8 @@ void free_all(swim_handle* h) {
   h->allocs.clear();
   if (h->h_quiet) (void)hipHostFree(h->h_quiet);
   h->h_quiet = nullptr;
+  if (h->xp) (void)hipHostFree(h->xp);
+  h->xp = nullptr;
   for (auto ev : h->pool) (void)hipEventDestroy(ev);
   for (auto& pe : h->pending) {
     (void)hipEventDestroy(pe.a);
@@ -379,9 +390,10 @@ int xpost(swim_handle* h, swim_xchg* x, const uint64_t* row) {
       const uint32_t hdr = h->n_leaving ? 4u : 0u;
       uint32_t* xs = P.xsend;
       if (hdr) {
-        h->chead[0] = n;
-        h->chead[1] = ns;
-        HIPC(h, hipMemcpyAsync(xs, h->chead, 16, hipMemcpyHostToDevice, s));
+        h->xp->chead[0] = n;
+        h->xp->chead[1] = ns;
+        h->xp->chead[2] = h->xp->chead[3] = 0u;
+        HIPC(h, hipMemcpyAsync(xs, h->xp->chead, 16, hipMemcpyHostToDevice, s));
       }
       if (n) HIPC(h, hipMemcpyAsync(xs + hdr, P.stg, (size_t)n * 16, hipMemcpyDeviceToDevice, s));
       if (ns) HIPC(h, hipMemcpyAsync(xs + hdr + 4u * n, P.stop_list, (size_t)ns * 4, hipMemcpyDeviceToDevice, s));
@@ -433,18 +445,20 @@ int xpost(swim_handle* h, swim_xchg* x, const uint64_t* row) {
 // all-gather, one host stop for both, and tr_period runs xpost after it; a host that performs the
 // exchanges itself (swim_shard_step) reads the row back here and goes on at once. x->op is set.
 int xready(swim_handle* h, const KP& P, swim_xchg* x, XsArgs a) {
+  if (!h->d_status || !h->xp || !h->xsend) return fail(h, SWIM_EINVAL, "sharded handle: swim_shard_attach or a transport first");
   a.world = h->world;
   hipLaunchKernelGGL(k_xstatus, dim3(1), dim3(64), 0, h->stream, (const Ctl*)P.ctl, (const uint32_t*)P.woff,
                      h->d_status, a);
   h->xpend = a.kind;
   if (h->has_tr) return SWIM_OK;
-  HIPC(h, hipMemcpyAsync(h->xrow, h->d_status, 8ull * (XS_CNT + h->world), hipMemcpyDeviceToHost, h->stream));
+  uint64_t* row = h->xp->xrow;
+  HIPC(h, hipMemcpyAsync(row, h->d_status, 8ull * (XS_CNT + h->world), hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
-  if (h->xrow[XS_ERR]) {
+  if (row[XS_ERR]) {
     h->xpend = XS_NONE;
     return xown_fail(h, a.kind);
   }
-  return xpost(h, x, h->xrow);
+  return xpost(h, x, row);
 }
 
 // Commit the phase's staged gossips. Unsharded: in place, sized on the device (overflow is
@@ -472,13 +486,13 @@ bool commit_begin(swim_handle* h, const KP& P, swim_xchg* x, int* rc, uint32_t b
 int commit_end(swim_handle* h, const KP& P, const swim_xchg* x) {
   hipStream_t s = h->stream;
   const uint32_t* xr = reinterpret_cast<const uint32_t*>(h->xrecv);
-  uint32_t total = 0, offs[SWIM_MAX_WORLD];
+  uint32_t total = 0, *offs = h->xp->offs;
   const uint64_t tail = commit_tail(h);  // wlast + bounds (+ touched columns) after each shard's gossips
   for (uint32_t q = 0; q < h->world; ++q) {
     const uint32_t* blk = xr + q * x->recv_stride;
     uint32_t c = 0, ns = 0, hdr = 0;
     if (h->n_leaving) {  // the block's header: gossips and stopped members
-      uint32_t head[2];
+      uint32_t* head = h->xp->bhead;
       HIPC(h, hipMemcpyAsync(head, blk, 8, hipMemcpyDeviceToHost, s));
       HIPC(h, hipStreamSynchronize(s));
       c = head[0];
@@ -568,7 +582,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         break;
       case PC_FD_TRACK:
         if (P.nxk && SH) {
-          uint32_t cnt[SWIM_MAX_WORLD];
+          uint32_t* cnt = h->xp->cnt;
           for (uint32_t q = 0; q < W; ++q) cnt[q] = (uint32_t)x->recv_counts[q];
           HIPC(h, hipMemcpyAsync(h->d_xcounts, cnt, 4ull * W, hipMemcpyHostToDevice, s));
           P.xrecv = reinterpret_cast<const uint32_t*>(h->xrecv);
@@ -922,25 +936,26 @@ int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t
   const uint32_t W = h->world, R = XS_CNT + W;
   // (the resume point too: ranks that took different branches of a period fail here, "out of step")
   const uint64_t op = code ? ~0ull : ((uint64_t)h->n_leaving << 32 | (uint64_t)(uint32_t)h->pc << 8 | x.op);
+  uint64_t* row = h->xp->xrow;  // (free here: xready's read-back serves host-driven exchanges only)
   if (!code && h->xpend) {  // k_xstatus wrote the rest of the row
-    h->xhead[0] = 0;
-    h->xhead[1] = op;
-    HIPC(h, hipMemcpyAsync(h->d_status, h->xhead, 16, hipMemcpyHostToDevice, h->stream));
+    h->xp->head[0] = 0;
+    h->xp->head[1] = op;
+    HIPC(h, hipMemcpyAsync(h->d_status, h->xp->head, 16, hipMemcpyHostToDevice, h->stream));
   } else {
     h->xpend = XS_NONE;
-    std::vector<uint64_t> row(R, 0ull);
+    for (uint32_t i = 0; i < R; ++i) row[i] = 0ull;
     row[0] = (uint64_t)(int64_t)code;
     row[1] = op;
     if (!code && x.op == SWIM_X_ALLGATHER) row[XS_CNT] = x.send_words;
     if (!code && x.op == SWIM_X_ALLTOALLV)
       for (uint32_t q = 0; q < W; ++q) row[XS_CNT + q] = x.send_counts[q];
-    HIPC(h, hipMemcpyAsync(h->d_status, row.data(), 8ull * R, hipMemcpyHostToDevice, h->stream));
+    HIPC(h, hipMemcpyAsync(h->d_status, row, 8ull * R, hipMemcpyHostToDevice, h->stream));
   }
   int rc = tr_allgather(h, h->d_status, h->d_status + R, 8ull * R);
   if (rc) return rc;
-  rows->resize((size_t)W * R);
-  HIPC(h, hipMemcpyAsync(rows->data(), h->d_status + R, 8ull * W * R, hipMemcpyDeviceToHost, h->stream));
+  HIPC(h, hipMemcpyAsync(h->xp->rows, h->d_status + R, 8ull * W * R, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  rows->assign(h->xp->rows, h->xp->rows + (size_t)W * R);
   return SWIM_OK;
 }
 
@@ -1014,11 +1029,22 @@ int tr_period(swim_handle* h) {
   }
 }
 
-// exchange buffers and the status rows of a handle that drives its own exchanges
-int tr_buffers(swim_handle* h) {
+// the status rows (device) and the exchanges' pinned host words of a sharded handle
+int status_buffers(swim_handle* h) {
   const uint32_t W = h->world, R = XS_CNT + W;
   int rc = SWIM_OK;
   if (!h->d_status && (rc = dalloc(h, &h->d_status, (size_t)(1 + W) * R))) return rc;
+  if (!h->xp && hipHostMalloc(reinterpret_cast<void**>(&h->xp), sizeof(swim_handle::XPin), hipHostMallocDefault) != hipSuccess) {
+    h->xp = nullptr;
+    return fail(h, SWIM_ENOMEM, "hipHostMalloc(exchange words)");
+  }
+  return SWIM_OK;
+}
+
+// exchange buffers and the status rows of a handle that drives its own exchanges
+int tr_buffers(swim_handle* h) {
+  int rc = status_buffers(h);
+  if (rc) return rc;
   if (!h->xsend) {
     uint64_t sw = 0, rw = 0;
     if ((rc = swim_shard_buffer_words(h, &sw, &rw))) return rc;
@@ -2360,8 +2386,7 @@ int swim_shard_attach(swim_handle* h, void* send_dev, void* recv_dev) {
   swim_shard_buffer_words(h, &sw, &rw);
   h->xsend_words = sw;
   h->xrecv_words = rw;
-  if (!h->d_status) return dalloc(h, &h->d_status, (size_t)(1 + h->world) * (XS_CNT + h->world));
-  return SWIM_OK;
+  return status_buffers(h);
 }
 
 int swim_shard_set_transport(swim_handle* h, const swim_transport* t) {
