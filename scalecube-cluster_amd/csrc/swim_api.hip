@@ -23,6 +23,7 @@ namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 constexpr uint32_t RB_CAP = 2048;  // slot entry bitmaps (k_slot_bm)
+constexpr uint32_t SLOT_IDS_GRID = 64;  // k_slot_ids' workgroups (a grid stride over the commit's new slots)
 constexpr uint32_t RB_GRID = 256;  // k_slot_bm's workgroups (a grid stride over the commit's new slots)
 #ifndef SWIM_RS_FUSE_ALL
 #define SWIM_RS_FUSE_ALL 0  // (tests: every radix sort in one launch of CS_FUSE workgroups at most)
@@ -343,6 +344,7 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
       hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
       hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, P.dsids / 256)), dim3(256), 0, s, P);
+      if (P.cid16) hipLaunchKernelGGL(k_slot_ids, dim3(SLOT_IDS_GRID), dim3(256), 0, s, P);
       // the entry bitmaps of this commit's long batch ranges (dsids bytes of LDS per workgroup)
       if (P.batched && P.rb_cap) hipLaunchKernelGGL(k_slot_bm, dim3(RB_GRID), dim3(256), P.dsids, s, P);
     }
@@ -1338,6 +1340,7 @@ int swim_create(const swim_config* cfg, swim_handle** out) {
     P.cid16 = (P.dsids * DICT_WAYS <= 65536u) ? 1u : 0u;
     if (P.cid16) {
       ALLOC(P.c_id16, h->CC);
+      ALLOC(P.g_sid, h->GC);
     } else {
       ALLOC(P.c_id, h->CC);
     }

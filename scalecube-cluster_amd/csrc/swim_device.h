@@ -273,6 +273,8 @@ struct KP {
   // gossip (loss set, or batching off). Its records live in the record ring c_sr / c_hash at
   // absolute indices [g_cref.x, g_cref.y).
   uint2* g_cref;      // [GC] record range of each slot (absolute indices into c_sr, mod CC)
+  uint2* g_sid;       // [GC] 16-bit entry ids: the ids of a slot whose range holds at most SID_INLINE
+                      // records, copied from c_id16 after its commit (k_slot_ids), read beside g_cref
   // slot entry bitmaps: a long record range's dictionary entries as one bitmap
   // (dsids / 4 words), built once at its commit, ORed by a receiver instead of walking the ids
   uint32_t* rb_bits;  // [rb_cap][dsids / 4]
