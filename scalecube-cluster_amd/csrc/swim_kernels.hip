@@ -898,6 +898,7 @@ __global__ void __launch_bounds__(256) k_slot_bm(KP P) {
 // record's id never changes while its slot is live (k_dict_entries writes it once, at the commit).
 // C3 apply 6.45 -> 6.09 / 6.14 ms per period (13.90 -> 13.51 / 13.59 per period), C2 3.60 -> 3.53, C4's
 // schedule at 65,536 (c4d65) 19.53 -> 19.03 / 19.01
+// (8 ids per slot in 16 B measured slower: C3 13.82 against 13.54 / 13.68, c4d65 19.19 against 19.01 / 19.00)
 constexpr uint32_t SID_INLINE = 4;
 __global__ void __launch_bounds__(256) k_slot_ids(KP P) {
   const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount;
@@ -3387,7 +3388,7 @@ __device__ __forceinline__ void apply_b_body(const KP& P) {
         const bool inl = C16 && len != 0u && len <= SID_INLINE;
         if (inl) {
 #pragma unroll
-          for (uint32_t k = 0; k < 4u; ++k)
+          for (uint32_t k = 0; k < SID_INLINE; ++k)
             if (k < len) record(cr.x + k, ((k < 2u ? si.x : si.y) >> (16u * (k & 1u))) & 0xFFFFu);
         }
 #ifdef SWIM_APPLY_PROF
