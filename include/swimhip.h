@@ -339,7 +339,8 @@ int swim_shard_step(swim_handle* h, swim_xchg* x);
 /* Library-driven exchanges. With a transport attached, swim_step / swim_step_async advance a sharded
  * handle through whole periods: at each exchange the library gathers every rank's status row (error
  * code, op, send counts: one small all-gather and one host stop, so an error any rank detects fails
- * every rank together), then moves the data itself (an all-gather padded to the largest block, or an
+ * every rank together; the counts and the errors the device state raises are written into the row on
+ * the device, so the status read is the exchange's only host stop), then moves the data itself (an all-gather padded to the largest block, or an
  * all-to-all-v) and resumes. The handle allocates its exchange buffers unless swim_shard_attach gave
  * some. Either the library's own RCCL communicator over xGMI (swim_shard_comm_init: rank 0 makes a
  * unique id with swim_rccl_unique_id and the host hands it to every rank; the collectives run on the
