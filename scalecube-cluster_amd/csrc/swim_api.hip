@@ -23,7 +23,7 @@ namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 constexpr uint32_t RB_CAP = 2048;  // slot entry bitmaps (k_slot_bm)
-constexpr uint32_t SLOT_IDS_GRID = 64;  // k_slot_ids' workgroups (a grid stride over the commit's new slots)
+constexpr uint32_t SLOT_IDS_GRID = 64;  // k_dict_free's least workgroups while it copies short slots' entry ids
 constexpr uint32_t RB_GRID = 256;  // k_slot_bm's workgroups (a grid stride over the commit's new slots)
 #ifndef SWIM_RS_FUSE_ALL
 #define SWIM_RS_FUSE_ALL 0  // (tests: every radix sort in one launch of CS_FUSE workgroups at most)
@@ -336,15 +336,17 @@ int commit_sorted(swim_handle* h, const KP& P0, const uint4* stg, uint32_t n, ui
       hipLaunchKernelGGL(k_rs_fin, dim3(1), dim3(1), 0, s, P, stg, n, C);
     }
     // batch slots: the gossips per bitmap word of the words this commit wrote (counter weights)
-    if (P.batched) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P, 0u);
+    // (with the dictionary on, in k_dict_claim's launch)
+    if (P.batched && !h->dict_on) hipLaunchKernelGGL(k_commit_wsum, dim3(64), dim3(256), 0, s, P, 0u);
     // the record dictionary of the batched apply: every commit while batching is
     // enabled, so records committed before the first batch have their entries too. (One launch with
-    // grid barriers between the steps measured slower: 38 us against ~4 per launch, §6.5.)
+    // grid barriers between the steps measured slower: 38 us against ~4 per launch, §6.5.) The short
+    // slots' entry ids (16-bit ids) are copied in k_dict_free's launch, after the entries.
     if (h->dict_on) {
-      hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(k_dict_claim, dim3(DICT_GRID), dim3(256), 0, s, P, P.batched);
       hipLaunchKernelGGL(k_dict_entries, dim3(DICT_GRID), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, P.dsids / 256)), dim3(256), 0, s, P);
-      if (P.cid16) hipLaunchKernelGGL(k_slot_ids, dim3(SLOT_IDS_GRID), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(P.cid16 ? SLOT_IDS_GRID : 1u, P.dsids / 256)), dim3(256), 0,
+                         s, P, P.cid16);
       // the entry bitmaps of this commit's long batch ranges (dsids bytes of LDS per workgroup)
       if (P.batched && P.rb_cap) hipLaunchKernelGGL(k_slot_bm, dim3(RB_GRID), dim3(256), P.dsids, s, P);
     }
@@ -545,7 +547,7 @@ int quiet_rounds(swim_handle* h, bool* quiet) {
   if (!h->last_quiet) return SWIM_OK;
   timed(h, 7, "k_quiet_rounds", [&] {
     hipLaunchKernelGGL(k_quiet_rounds, dim3(blocks_for(h->base.nloc, 256)), dim3(256), 0, s, Q, Q.round, h->G);
-    if (h->dict_on) hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, Q.dsids / 256)), dim3(256), 0, s, Q);
+    if (h->dict_on) hipLaunchKernelGGL(k_dict_free, dim3(std::max<uint32_t>(1, Q.dsids / 256)), dim3(256), 0, s, Q, 0u);
   });
   h->quiet_periods++;
   h->period_quiet = true;

@@ -900,7 +900,7 @@ __global__ void __launch_bounds__(256) k_slot_bm(KP P) {
 // schedule at 65,536 (c4d65) 19.53 -> 19.03 / 19.01
 // (8 ids per slot in 16 B measured slower: C3 13.82 against 13.54 / 13.68, c4d65 19.19 against 19.01 / 19.00)
 constexpr uint32_t SID_INLINE = 4;
-__global__ void __launch_bounds__(256) k_slot_ids(KP P) {
+__device__ __forceinline__ void slot_ids_body(const KP& P) {
   const uint32_t g0 = P.ctl->g_prev, g1 = P.ctl->gcount;
   for (uint32_t g = g0 + blockIdx.x * blockDim.x + threadIdx.x; (int32_t)(g1 - g) > 0; g += gridDim.x * blockDim.x) {
     const uint32_t sl = gmod(P, g);
@@ -913,9 +913,17 @@ __global__ void __launch_bounds__(256) k_slot_ids(KP P) {
   }
 }
 
-__global__ void k_dict_claim(KP P) { dict_claim_body(P); }
+// (launches after a commit: the batch slots' word counts ride the claim, the short slots' entry ids the
+// free; neither depends on the other's step)
+__global__ void k_dict_claim(KP P, uint32_t wsum) {
+  if (wsum) commit_wsum_body(P, 0u);
+  dict_claim_body(P);
+}
 __global__ void k_dict_entries(KP P) { dict_entries_body(P); }
-__global__ void k_dict_free(KP P) { dict_free_body(P); }
+__global__ void k_dict_free(KP P, uint32_t sids) {
+  dict_free_body(P);
+  if (sids) slot_ids_body(P);
+}
 
 
 // Exclusive prefix sum of n words in one workgroup (sharded exchange offsets)
