@@ -315,3 +315,28 @@ def test_leave_on_one_rank_fails_every_rank():
     others did not fails every rank with SWIM_EINVAL at the next exchange, instead of one rank
     reading another's header as gossips."""
     mp.spawn(_leave_mismatch_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+
+@pytest.mark.gpu
+def test_unattached_shard_fails_loudly():
+    """A sharded handle (rank 0 of 2) with neither a transport nor exchange buffers: swim_step refuses it
+    (no transport), and swim_shard_step refuses it (no buffers), each with SWIM_EINVAL and before any
+    kernel of the period runs; stepping it again fails the same way (xready repeats the check at every
+    exchange of a period that did start)."""
+    import ctypes
+
+    from swimhip import ClusterConfig, SwimCluster
+
+    c = SwimCluster(ClusterConfig.defaultLocalConfig(), 64, 3, _shard=(0, 2))
+    try:
+        for _ in range(2):
+            with pytest.raises(SwimError) as ei:
+                c.step(1)
+            assert ei.value.code == nat.SWIM_EINVAL and "attach a transport" in str(ei.value)
+            x = nat.SwimXchg()
+            with pytest.raises(SwimError) as ei:
+                c._call("shard_step", c._h, ctypes.byref(x))
+            assert ei.value.code == nat.SWIM_EINVAL and "swim_shard_attach first" in str(ei.value)
+    finally:
+        c.close()
