@@ -38,6 +38,9 @@ def _worker(rank, world, port, n, kw, loss, n_crash, warmup, periods, every, min
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # nine processes on one GPU: one hardware queue each (HIP's default is 4 per process), so the card's
+    # queues are not oversubscribed (set before this process's first HIP call)
+    os.environ["GPU_MAX_HW_QUEUES"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:

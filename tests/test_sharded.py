@@ -23,6 +23,8 @@ def _free_port():
 def _init(rank, world, port, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if backend == "gloo" and world > 1:  # ranks sharing one GPU: one hardware queue each (HIP's default: 4)
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
     if backend == "nccl":
         torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
