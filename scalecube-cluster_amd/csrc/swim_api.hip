@@ -23,6 +23,8 @@ namespace {
 
 constexpr int NCLASS = 12;  // timing classes, see swim_kernel_time
 constexpr uint32_t RB_CAP = 2048;  // slot entry bitmaps (k_slot_bm)
+// exchanges whose every count follows from the status rows of the exchange before them (tr_period)
+enum XKnown : uint32_t { XK_NONE = 0, XK_NEED, XK_ACK };
 constexpr uint32_t SLOT_IDS_GRID = 64;  // k_dict_free's least workgroups while it copies short slots' entry ids
 constexpr uint32_t RB_GRID = 256;  // k_slot_bm's workgroups (a grid stride over the commit's new slots)
 #ifndef SWIM_RS_FUSE_ALL
@@ -105,6 +107,7 @@ struct swim_handle {
   ncclComm_t comm = nullptr;
   uint64_t* d_status = nullptr;  // [(1 + world) * (XS_CNT + world)]: this rank's status row, then all ranks'
   uint32_t xpend = 0;  // XsKind whose k_xstatus row awaits xpost
+  uint32_t xknown = 0;  // XK_*: the exchange period_resume returned has counts the last status rows give
   // Pinned host words of the exchanges (sharded handles): small copies from pageable memory go through
   // a staging buffer and wait for it, so every copy of a period's exchanges is pinned
   struct XPin {
@@ -665,6 +668,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
         for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
         HIPC(h, xorder(h));
         h->pc = PC_R_WIN;
+        h->xknown = XK_NEED;
         return SWIM_OK;
       }
       case PC_R_WIN: {  // (3) sender side: ship the needed window words
@@ -786,6 +790,7 @@ int period_resume(swim_handle* h, swim_xchg* x) {
           xchg_clear(x, SWIM_X_ALLTOALLV, W);
           for (uint32_t q = 0; q < W; ++q) x->send_counts[q] = back[q];
           HIPC(h, xorder(h));
+          h->xknown = XK_ACK;
           return SWIM_OK;
         }
         break;
@@ -901,9 +906,9 @@ int tr_allgather(swim_handle* h, const void* send, void* recv, uint64_t n) {
   }
   const uint64_t W = h->world;
   if (h->hsend.size() < n) h->hsend.resize(n);
-  if (h->hrecv.size() < W * n) h->hrecv.resize(W * n);
   HIPC(h, hipMemcpyAsync(h->hsend.data(), send, n, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  if (h->hrecv.size() < W * n) h->hrecv.resize(W * n);  // (after the last copy out of it has completed)
   if (h->tr.allgather(h->tr.ctx, h->hsend.data(), h->hrecv.data(), n, nullptr))
     return fail(h, SWIM_ERCCL, "shard exchange: all-gather failed");
   HIPC(h, hipMemcpyAsync(recv, h->hrecv.data(), W * n, hipMemcpyHostToDevice, h->stream));
@@ -922,9 +927,10 @@ int tr_alltoallv(swim_handle* h, const uint64_t* sb, const uint64_t* rb) {
     rt += rb[q];
   }
   if (h->hsend.size() < st) h->hsend.resize(st);
-  if (h->hrecv.size() < rt) h->hrecv.resize(rt);
   if (st) HIPC(h, hipMemcpyAsync(h->hsend.data(), h->xsend, st, hipMemcpyDeviceToHost, h->stream));
   HIPC(h, hipStreamSynchronize(h->stream));
+  // (grown only now: the last exchange's copy to the device out of it has completed)
+  if (h->hrecv.size() < rt) h->hrecv.resize(rt);
   if (h->tr.alltoallv(h->tr.ctx, h->hsend.data(), sb, h->hrecv.data(), rb, nullptr))
     return fail(h, SWIM_ERCCL, "shard exchange: all-to-all-v failed");
   if (rt) HIPC(h, hipMemcpyAsync(h->xrecv, h->hrecv.data(), rt, hipMemcpyHostToDevice, h->stream));
@@ -963,6 +969,22 @@ int tr_status(swim_handle* h, int code, const swim_xchg& x, std::vector<uint64_t
   return SWIM_OK;
 }
 
+// The rows of an exchange whose counts the last status rows give (tr_period): XK_NEED after the
+// registrations (rank a sends rank b one need bitmap of nneed_a words per pair b registered with a:
+// rows[b][XS_CNT + a] / 2 pairs, nneed_a from a's active-list length, rows[a][XS_A0]); XK_ACK after the
+// SYNC requests (rank a sends rank b back what it received from b: the transposed counts).
+void known_rows(swim_handle* h, uint32_t known, std::vector<uint64_t>* rows) {
+  const uint32_t W = h->world, R = XS_CNT + W;
+  std::vector<uint64_t>& v = *rows;
+  std::vector<uint64_t> cnt((size_t)W * W);
+  for (uint32_t a = 0; a < W; ++a)
+    for (uint32_t b = 0; b < W; ++b)
+      cnt[(size_t)a * W + b] = known == XK_NEED ? v[(size_t)b * R + XS_CNT + a] / 2 * ((v[(size_t)a * R + XS_A0] + 31u) / 32u)
+                                                : v[(size_t)b * R + XS_CNT + a];
+  for (uint32_t a = 0; a < W; ++a)
+    for (uint32_t b = 0; b < W; ++b) v[(size_t)a * R + XS_CNT + b] = cnt[(size_t)a * W + b];
+}
+
 // One period of a sharded handle with a transport: period_resume up to each exchange, the status
 // all-gather, the collective, resume.
 int tr_period(swim_handle* h) {
@@ -972,34 +994,51 @@ int tr_period(swim_handle* h) {
   xchg_clear(&x, SWIM_X_DONE, W);
   for (;;) {
     h->xpend = XS_NONE;
+    h->xknown = XK_NONE;
     int rc = period_resume(h, &x);
-    if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow flag joins the status
-      XsArgs a{};
-      a.kind = XS_DONE;
-      rc = xready(h, h->cur, &x, a);
-    }
-    const std::string mine = rc ? h->err : std::string();
-    const uint32_t kind = h->xpend;
-    const int src = tr_status(h, rc, x, &rows);
-    if (src) return src;
-    if (!rc && kind && rows[(size_t)h->rank * R + XS_ERR]) {
-      h->xpend = XS_NONE;
-      return xown_fail(h, kind);
-    }
-    for (uint32_t q = 0; q < W; ++q) {
-      const uint64_t e = rows[(size_t)q * R] ? rows[(size_t)q * R] : rows[(size_t)q * R + XS_ERR];
-      if (e) {
-        h->xpend = XS_NONE;
-        if (rc) return fail(h, rc, mine);
-        return fail(h, (int)(int64_t)e, "shard exchange: rank " + std::to_string(q) + " failed");
+    if (!rc && h->xknown != XK_NONE) {
+      // The need bitmaps answer the registrations, and the SYNC_ACK tables the SYNC requests: every
+      // rank's counts of these two exchanges follow from the status rows of the exchange before them
+      // (nothing between them can fail on one rank alone: every rank's SYNC batch is checked against
+      // its rank's capacity at the SYNC status), so they take no status all-gather and no host stop.
+      known_rows(h, h->xknown, &rows);
+      h->xknown = XK_NONE;
+    } else {
+      if (!rc && x.op == SWIM_X_DONE) {  // the period's end: every rank's overflow flag joins the status
+        XsArgs a{};
+        a.kind = XS_DONE;
+        rc = xready(h, h->cur, &x, a);
       }
+      const std::string mine = rc ? h->err : std::string();
+      const uint32_t kind = h->xpend;
+      const int src = tr_status(h, rc, x, &rows);
+      if (src) return src;
+      if (!rc && kind && rows[(size_t)h->rank * R + XS_ERR]) {
+        h->xpend = XS_NONE;
+        return xown_fail(h, kind);
+      }
+      for (uint32_t q = 0; q < W; ++q) {
+        const uint64_t e = rows[(size_t)q * R] ? rows[(size_t)q * R] : rows[(size_t)q * R + XS_ERR];
+        if (e) {
+          h->xpend = XS_NONE;
+          if (rc) return fail(h, rc, mine);
+          return fail(h, (int)(int64_t)e, "shard exchange: rank " + std::to_string(q) + " failed");
+        }
+      }
+      for (uint32_t q = 1; q < W; ++q) {
+        if ((rows[(size_t)q * R + 1] >> 32) != (rows[1] >> 32))
+          return fail(h, SWIM_EINVAL, "shard exchange: ranks disagree on swim_leave calls (rank " + std::to_string(q) + ")");
+        if (rows[(size_t)q * R + 1] != rows[1]) return fail(h, SWIM_EINVAL, "shard exchange: ranks out of step");
+      }
+      if (kind == XS_SYNC)  // every rank's received SYNC batch within its sync_capacity (before the SYNC_ACK)
+        for (uint32_t r = 0; r < W; ++r) {
+          uint64_t in = 0;
+          for (uint32_t q = 0; q < W; ++q) in += rows[(size_t)q * R + XS_CNT + r];
+          if (in / (rows[(size_t)r * R + XS_A0] + 2u) > (rows[(size_t)r * R + XS_A1] >> 32))
+            return fail(h, SWIM_EOVERFLOW, "SYNC exchange over sync_capacity on rank " + std::to_string(r));
+        }
+      if (h->xpend && (rc = xpost(h, &x, &rows[(size_t)h->rank * R]))) return rc;
     }
-    for (uint32_t q = 1; q < W; ++q) {
-      if ((rows[(size_t)q * R + 1] >> 32) != (rows[1] >> 32))
-        return fail(h, SWIM_EINVAL, "shard exchange: ranks disagree on swim_leave calls (rank " + std::to_string(q) + ")");
-      if (rows[(size_t)q * R + 1] != rows[1]) return fail(h, SWIM_EINVAL, "shard exchange: ranks out of step");
-    }
-    if (h->xpend && (rc = xpost(h, &x, &rows[(size_t)h->rank * R]))) return rc;
     if (x.op == SWIM_X_DONE) return SWIM_OK;
     if (x.op == SWIM_X_ALLGATHER) {
       uint64_t m = 0;

@@ -3991,6 +3991,7 @@ __global__ void k_xstatus(const Ctl* c, const uint32_t* woff, uint64_t* row, XsA
       }
       err = a1 > a.cap ? SWIM_EOVERFLOW : 0;
       a0 = rl;
+      a1 |= (uint64_t)a.cap << 32;  // (this rank's sync_capacity: every rank checks every rank's receipts)
       break;
     }
     case XS_DONE:
